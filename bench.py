@@ -1,0 +1,235 @@
+"""Benchmark: Mcells/s forward+backward, 3-D 7-point fp32 1024³ (BASELINE.json metric).
+
+One step = one forward sweep + one TF-MAD adjoint sweep of the 7-point diffusion op
+``out = u + 0.1·(Σ₆ u[nb] − 6u)`` (boundary 'zeros') through the drop-in API
+(``AutoDiffOp(...).create_tensorflow_op(backend='torch_native')`` → ``Op.apply`` +
+``out.backward``), inputs resident in HBM. N>1: the 1024³ domain is split into z-slabs
+(``zslab.py``) with an RCCL halo exchange per sweep — strong scaling, total work fixed.
+
+Run: ``python bench.py [--gpus N] [--steps K] [--warmup W]``; N>1 via
+``torch.distributed.run --nproc-per-node N``.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md), GB/s
+BYTES_PER_CELL_SWEEP = 8       # fp32 7-point: read u once + write out once
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--warmup', type=int, default=3)
+    p.add_argument('--n', type=int, default=1024, help='cube edge (default: the 1024³ north-star config)')
+    p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--cpu-seconds', type=float, default=12.0, help='budget of the CPU baseline sample')
+    p.add_argument('--kernel-only', action='store_true', help='also time the raw kernel loop')
+    return p.parse_args()
+
+
+def cpu_baseline(budget_s):
+    """The oracle's C restatement of the reference CPU kernel (OpenMP), bounded 1024²×64 sample."""
+    import numpy as np
+    from oracle import cref
+    build_dir = os.path.join(ROOT, 'oracle', 'build_native')
+    lib = cref.load(build_dir=build_dir, march='native')
+    threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or len(os.sched_getaffinity(0))
+    os.environ.setdefault('OMP_NUM_THREADS', str(threads))
+    shape = (64, 1024, 1024)
+    rng = np.random.default_rng(0)
+    u = rng.uniform(0, 1, shape).astype(np.float32)
+    d = rng.uniform(-1, 1, shape).astype(np.float32)
+    out = np.empty_like(u)
+    du = np.empty_like(u)
+    lib.diffusion7_f32(u, 0.1, out)          # warm-up (first touch, thread pool)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        lib.diffusion7_f32(u, 0.1, out)      # forward sweep
+        lib.diffusion7_f32(d, 0.1, du)       # adjoint sweep (same symmetric stencil on diffout)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or reps >= 200:
+            break
+    cells = reps * u.size
+    return {'value': round(cells / el / 1e6, 2), 'unit': 'Mcells/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{reps} fwd+bwd sweeps of a 64x1024x1024 fp32 slab of the 1024^3 workload, '
+                      f'oracle/stencil_ref.c (pystencils CPU loop nest restated), gcc -O3 -march=native -fopenmp, '
+                      f'{threads} OpenMP threads, {el:.1f} s'}
+
+
+def load_traffic(workload):
+    """HBM bytes per launch from the committed PMC summary (profiles/traffic.json), if present."""
+    path = os.path.join(ROOT, 'profiles', 'traffic.json')
+    try:
+        with open(path) as fh:
+            data = json.load(fh)
+        return data.get(workload)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    distributed = world > 1
+    if args.gpus != world and distributed:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    if distributed:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+
+    import pystencils_autodiff_amd as pa
+    from pystencils_autodiff_amd import workloads as W
+    from pystencils_autodiff_amd.zslab import ZSlabOp, slab_bounds
+
+    n = args.n
+    lo, hi = slab_bounds(n, world, rank)
+    zl = hi - lo
+    op = pa.AutoDiffOp(W.diffusion_7pt(), boundary_handling='zeros')
+    fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    fwd_k = op.forward_ast_gpu.compile()
+    bwd_k = op.backward_ast_gpu.compile()
+
+    g = torch.Generator(device='cuda').manual_seed(0 + rank)
+    u = torch.rand((zl, n, n), generator=g, device='cuda', dtype=torch.float32)
+    g1 = torch.Generator(device='cuda').manual_seed(1000 + rank)
+    d = torch.rand((zl, n, n), generator=g1, device='cuda', dtype=torch.float32) * 2 - 1
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+    ev = []
+
+    if distributed:
+        zop = ZSlabOp(op, use_cuda=True)
+        out = torch.empty_like(u)
+        du = torch.empty_like(u)
+
+        def step(record):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e2 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            zop.fwd(u=u, out=out)
+            e1.record(stream)
+            zop.bwd(diffout=d, diffu=du)
+            e2.record(stream)
+            if record:
+                ev.append((e0, e1, e2))
+    else:
+        uu = u.requires_grad_(True)
+
+        def step(record):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e2 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            (o,) = fn.apply(uu)
+            e1.record(stream)
+            o.backward(d)
+            e2.record(stream)
+            uu.grad = None
+            if record:
+                ev.append((e0, e1, e2))
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    fwd_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / len(ev)
+    bwd_ms = sum(b.elapsed_time(c) for _, b, c in ev) / len(ev)
+    cells_total = n ** 3
+    value = cells_total * args.steps / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # kernel-level: algorithmic bytes of one forward launch over this rank's slab / its event time
+    bytes_fwd = BYTES_PER_CELL_SWEEP * zl * n * n
+    achieved = bytes_fwd / (fwd_ms * 1e-3) / 1e9
+    result_extra = {}
+    if args.kernel_only and not distributed:
+        out = torch.empty_like(u)
+        du = torch.empty_like(u)
+        for _ in range(2):
+            fwd_k(u=u.detach(), out=out)
+            bwd_k(diffout=d, diffu=du)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            fwd_k(u=u.detach(), out=out)
+            bwd_k(diffout=d, diffu=du)
+        torch.cuda.synchronize()
+        kt = time.perf_counter() - t1
+        result_extra['kernel_only_mcells_s'] = round(cells_total * args.steps / kt / 1e6, 1)
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                cpu = cpu_baseline(args.cpu_seconds)
+            except Exception as exc:  # noqa: BLE001 - report, don't fail the GPU bench
+                cpu = {'value': None, 'unit': 'Mcells/s', 'cores': None, 'kind': 'port', 'sample': f'failed: {exc}'}
+        workload = f'diffusion7_f32_{n}^3'
+        traffic = load_traffic(workload)
+        res = {
+            'metric': f'Mcells/s forward+backward, 3D 7-point fp32 {n}^3',
+            'value': round(value, 1),
+            'unit': 'Mcells/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': round(ms_per_step, 4),
+            'higher_is_better': True,
+            'scaling': 'strong',
+            'vs_baseline': None,
+            'dtype': 'f32',
+            'data': 'synthetic: u~U(0,1), diffout~U(-1,1) (torch generator seeds 0/1000+rank)',
+            'config': {'workload': f'3D 7-point diffusion out=u+0.1*(sum6 u[nb]-6u), boundary zeros, fp32, '
+                                   f'{n}^3 forward + TF-MAD adjoint per step',
+                       'cells': cells_total, 'decomposition': f'z-slab x{world}' if world > 1 else 'single GPU',
+                       'path': 'AutoDiffOp.create_tensorflow_op(backend=torch_native) apply+backward'
+                       if world == 1 else 'ZSlabOp fwd/bwd with RCCL halo exchange'},
+            'fwd_ms': round(fwd_ms, 4),
+            'bwd_ms': round(bwd_ms, 4),
+            'hbm_roofline_frac_step': round(2 * BYTES_PER_CELL_SWEEP * cells_total / (ms_per_step * 1e-3) / 1e9
+                                            / (HBM_PEAK_GBS * world), 4),
+            'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
+                         'kernel': f'{fwd_k.name}_march (forward sweep; adjoint moves the same bytes)',
+                         'bytes_per_launch': bytes_fwd},
+            'cpu_baseline': cpu,
+        }
+        res.update(result_extra)
+        print(json.dumps(res))
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,264 @@
+"""A compiled GPU stencil kernel: schedule choice, hiprtc build, launch.
+
+Replaces the reference's generated ``call_<kernel>`` wrapper
+(``backends/astnodes.py:56-65,143-146``: ``at::Tensor`` → ``data_ptr<T>()``,
+then ``kernel<<<grid, block>>>`` from ``indexing.call_parameters``,
+``printer.py:88-108``). Calling convention kept: ``kernel(x=..., y=..., z=..., a=5.)``
+with every field tensor and scalar passed by name, outputs written in place.
+Launches go to torch's current HIP stream (the reference used the legacy
+default stream, ``printer.py:106``).
+"""
+import math
+import os
+
+import numpy as np
+
+from . import hip_runtime as rt
+from .hip_emitter import MarchConfig, emit_generic, emit_march, emit_pointwise, march_geometry
+
+__all__ = ['HipStencilKernel', 'default_march_config']
+
+
+def default_march_config(ir, ve):
+    """Tile shape per dimensionality (overridable via ``gpu_indexing_params`` or ``PSAD_MARCH``)."""
+    if ir.ndim == 2:
+        cfg = dict(CX=1, WX=4, NR=1)
+    else:
+        cfg = dict(CX=2, WX=1, NR=2)
+    env = os.environ.get('PSAD_MARCH')
+    if env:
+        for kv in env.split(','):
+            k, v = kv.split('=')
+            cfg[k.strip()] = int(v)
+    cfg.pop('ZC', None)
+    cfg.pop('BLOCKS', None)
+    cfg.pop('NT', None)
+    return MarchConfig(VE=ve, **cfg)
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class HipStencilKernel:
+    def __init__(self, kernel):
+        self.kernel = kernel
+        self.ir = kernel.ir
+        self.name = kernel.function_name
+        self._variants = {}            # variant key -> (source, kernel name)
+        self.last_variant = None
+
+    # -- sources --------------------------------------------------------------------------------
+    def schedule(self):
+        ir = self.ir
+        if ir.has_index_dims or ir.ndim not in (1, 2, 3):
+            return 'generic'
+        if ir.pointwise:
+            return 'pointwise'
+        if ir.ndim in (2, 3) and all(all(o == 0 for o in s[1]) for s in ir.stores) and \
+                len({f.dtype for f in ir.fields}) == 1:
+            return 'march'
+        return 'generic'
+
+    def _vec_elems(self):
+        return 16 // self.ir.fields[0].dtype.itemsize
+
+    def _march_cfg(self, ve):
+        cfg = default_march_config(self.ir, ve)
+        over = {k: v for k, v in self.kernel.tuning.items() if k in ('CX', 'WX', 'NR', 'NT_STORE')}
+        if over:
+            d = dict(CX=cfg.CX, WX=cfg.WX, NR=cfg.NR, VE=ve, NT_STORE=cfg.NT_STORE)
+            d.update(over)
+            cfg = MarchConfig(**d)
+        return cfg
+
+    def source(self, variant):
+        if variant not in self._variants:
+            kind = variant[0]
+            kname = f"{self.name}_{kind}"
+            if kind == 'pointwise':
+                src = emit_pointwise(self.ir, kname)
+            elif kind == 'march':
+                src = emit_march(self.ir, kname, variant[1])
+            else:
+                src = emit_generic(self.ir, kname)
+            self._variants[variant] = (src, kname)
+        return self._variants[variant]
+
+    def primary_variant(self):
+        s = self.schedule()
+        if s == 'march':
+            return ('march', self._march_cfg(self._vec_elems()))
+        return (s,)
+
+    @property
+    def code(self):
+        return self.source(self.primary_variant())[0]
+
+    def function(self, variant, device):
+        src, kname = self.source(variant)
+        code = rt.compile_hip(src)
+        if variant[0] == 'pointwise':
+            return {k: rt.load_function(code, f"{kname}_{k}", device) for k in ('v4', 'v1')}
+        return rt.load_function(code, kname, device)
+
+    def build(self):
+        """Compile the primary variant ahead of time (hiprtc works without a GPU)."""
+        src, _ = self.source(self.primary_variant())
+        return rt.compile_hip(src)
+
+    # -- launch ---------------------------------------------------------------------------------
+    def __call__(self, halos=None, stream=None, force_schedule=None, z_range=None, **kwargs):
+        """Launch on the field tensors / scalars given by name.
+
+        ``halos`` = ``{field: (lo_planes, hi_planes)}``: tensors holding the RZ planes just
+        below plane 0 / above plane Z-1 of a stencil field (``None`` = zeros); ``z_range``
+        restricts the written planes of axis 0 (both: z-slab decomposition, ``zslab.py``).
+        """
+        torch = _torch()
+        ir = self.ir
+        tensors = {}
+        for f in ir.fields:
+            if f.name not in kwargs:
+                raise TypeError(f"{self.name}: missing field argument '{f.name}'")
+            t = kwargs[f.name]
+            if not isinstance(t, torch.Tensor) or not t.is_cuda:
+                raise TypeError(f"{self.name}: field '{f.name}' must be a torch tensor on the GPU")
+            if t.dtype != getattr(torch, f.dtype.numpy_dtype.name):
+                raise TypeError(f"{self.name}: field '{f.name}' has dtype {t.dtype}, kernel expects "
+                                f"{f.dtype.numpy_dtype.name}")
+            tensors[f.name] = t
+        scalars = []
+        for s in ir.scalars:
+            if s.name not in kwargs:
+                raise TypeError(f"{self.name}: missing scalar argument '{s.name}'")
+            scalars.append(float(kwargs[s.name]))
+        ref = tensors[ir.fields_written[0].name]
+        shape = tuple(ref.shape[:ir.ndim])
+        for f in ir.fields:
+            t = tensors[f.name]
+            if tuple(t.shape[:ir.ndim]) != shape:
+                raise ValueError(f"{self.name}: field '{f.name}' has spatial shape {tuple(t.shape[:ir.ndim])}, "
+                                 f"expected {shape}")
+            if f.has_fixed_shape and tuple(t.shape) != tuple(int(s) for s in f.shape):
+                raise ValueError(f"{self.name}: field '{f.name}' was declared with shape {f.shape}, got "
+                                 f"{tuple(t.shape)}")
+            if t.dim() != f.spatial_dimensions + f.index_dimensions:
+                raise ValueError(f"{self.name}: field '{f.name}' expects {f.spatial_dimensions + f.index_dimensions} "
+                                 f"dims, got {t.dim()}")
+        device = ref.device.index if ref.device.index is not None else torch.cuda.current_device()
+        if stream is None:
+            stream = torch.cuda.current_stream(ref.device).cuda_stream
+        if any(n == 0 for n in shape):
+            return
+        contiguous = all(t.is_contiguous() for t in tensors.values())
+        sched = force_schedule or self.schedule()
+        if sched != 'generic' and not contiguous:
+            sched = 'generic'
+        if (halos or z_range is not None) and sched != 'march':
+            raise ValueError('halo planes / z ranges are only supported by the march schedule')
+        with torch.cuda.device(device):
+            if sched == 'pointwise':
+                self._launch_pointwise(tensors, scalars, shape, device, stream)
+            elif sched == 'march':
+                self._launch_march(tensors, scalars, shape, device, stream, halos or {}, z_range)
+            else:
+                self._launch_generic(tensors, scalars, shape, device, stream)
+
+    def _scalar_args(self, scalars):
+        kind = 'f64' if self.ir.compute_dtype == np.float64 else 'f32'
+        return [(kind, v) for v in scalars]
+
+    def _launch_pointwise(self, tensors, scalars, shape, device, stream):
+        ir = self.ir
+        variant = ('pointwise',)
+        fns = self.function(variant, device)
+        n = int(np.prod(shape))
+        aligned = all(t.data_ptr() % 32 == 0 for t in tensors.values())
+        args = [('ptr', tensors[f.name].data_ptr()) for f in ir.fields] + [('i64', n)] + self._scalar_args(scalars)
+        per_block = 256 * (4 if aligned else 1)
+        blocks = max(1, min(math.ceil(n / per_block), 256 * 16))
+        self.last_variant = ('pointwise', 'v4' if aligned else 'v1')
+        rt.launch(fns['v4' if aligned else 'v1'], (blocks,), (256,), rt.pack_args(args), stream)
+
+    def _launch_generic(self, tensors, scalars, shape, device, stream):
+        ir = self.ir
+        fn = self.function(('generic',), device)
+        bounds = ir.iteration_bounds(shape)
+        ncell = int(np.prod([hi - lo for lo, hi in bounds]))
+        if ncell <= 0:
+            return
+        args = [('ptr', tensors[f.name].data_ptr()) for f in ir.fields]
+        args += [('i64', int(n)) for n in shape]
+        for f in ir.fields:
+            args += [('i64', int(s)) for s in tensors[f.name].stride()]
+        for lo, hi in bounds:
+            args += [('i64', lo), ('i64', hi)]
+        args += self._scalar_args(scalars)
+        blocks = max(1, min(math.ceil(ncell / 256), 256 * 32))
+        self.last_variant = ('generic',)
+        rt.launch(fn, (blocks,), (256,), rt.pack_args(args), stream)
+
+    def march_launch_geometry(self, shape, cfg, z_range=None):
+        """(Z, Y, X), bounds and grid of the march schedule for a field shape."""
+        ir = self.ir
+        bounds = ir.iteration_bounds(shape)
+        if z_range is not None:
+            lo, hi = bounds[0]
+            bounds = [(max(lo, int(z_range[0])), min(hi, int(z_range[1])))] + list(bounds[1:])
+        if ir.ndim == 3:
+            Z, Y, X = shape
+            (zlo, zhi), (ylo, yhi), (xlo, xhi) = bounds
+        else:
+            Z, X = shape
+            Y = 1
+            (zlo, zhi), (xlo, xhi) = bounds
+            ylo, yhi = 0, 1
+        ntx = max(1, math.ceil(xhi / cfg.TX))
+        nty = max(1, math.ceil(yhi / cfg.TY))
+        nt = ntx * nty
+        nz = max(0, zhi - zlo)
+        target = int(self.kernel.tuning.get('BLOCKS', os.environ.get('PSAD_MARCH_BLOCKS', 2048)))
+        zc = self.kernel.tuning.get('ZC') or int(os.environ.get('PSAD_MARCH_ZC', 0)) or \
+            max(1, min(nz, math.ceil(nz * nt / target)))
+        zc = max(zc, min(nz, 4 * max(1, march_geometry(ir, cfg)['RZ'])))
+        nchunks = math.ceil(nz / zc) if nz else 0
+        return dict(Z=Z, Y=Y, X=X, zlo=zlo, zhi=zhi, ylo=ylo, yhi=yhi, xlo=xlo, xhi=xhi, zc=zc, ntx=ntx,
+                    nty=nty, grid=nt * nchunks)
+
+    def _launch_march(self, tensors, scalars, shape, device, stream, halos, z_range=None):
+        torch = _torch()
+        ir = self.ir
+        ve = self._vec_elems()
+        X = shape[-1]
+        stencil = ir.stencil_fields
+        aligned = X % ve == 0 and all(tensors[f.name].data_ptr() % 16 == 0 for f in stencil)
+        for f in stencil:
+            for h in halos.get(f.name, (None, None)):
+                if h is not None and (h.data_ptr() % 16 != 0):
+                    aligned = False
+        cfg = self._march_cfg(ve if aligned else 1)
+        variant = ('march', cfg)
+        fn = self.function(variant, device)
+        geo = self.march_launch_geometry(shape, cfg, z_range)
+        if geo['grid'] == 0 or geo['yhi'] <= geo['ylo'] or geo['xhi'] <= geo['xlo']:
+            return
+        rz = march_geometry(ir, cfg)['RZ']
+        plane = geo['Y'] * geo['X']
+        args = [('ptr', tensors[f.name].data_ptr()) for f in ir.fields]
+        for f in stencil:
+            lo, hi = halos.get(f.name, (None, None))
+            for h in (lo, hi):
+                if h is not None:
+                    if not isinstance(h, torch.Tensor) or not h.is_contiguous() or h.numel() < rz * plane or \
+                            h.dtype != tensors[f.name].dtype:
+                        raise ValueError(f"halo for '{f.name}' must be a contiguous tensor of >= {rz} planes")
+            args += [('ptr', lo.data_ptr() if lo is not None else 0), ('ptr', hi.data_ptr() if hi is not None else 0)]
+        for k in ('Z', 'Y', 'X', 'zlo', 'zhi', 'ylo', 'yhi', 'xlo', 'xhi', 'zc', 'ntx', 'nty'):
+            args.append(('i32', int(geo[k])))
+        args += self._scalar_args(scalars)
+        if max(geo['Z'], geo['Y'], geo['X']) >= 2 ** 31 or geo['grid'] >= 2 ** 31:
+            raise ValueError('field extent too large for the march schedule')
+        self.last_variant = ('march', cfg)
+        rt.launch(fn, (geo['grid'],), (256,), rt.pack_args(args), stream)

@@ -1,0 +1,269 @@
+"""Lowering of an assignment collection into a stencil kernel description.
+
+This is the MI355X layer's replacement for ``pystencils.create_kernel``
+([ext], called from ``_autodiff.py:479-542``): it fixes the semantics the
+reference's generated kernels have, independent of how they are scheduled:
+
+* iteration space = the common spatial shape of all fields, C layout,
+  coordinate 0 slowest;
+* ``boundary_handling='zeros'`` (``transformations.py:12-36`` +
+  ``ghost_layers=0``): every cell is written; a read outside the domain yields
+  exactly 0 (``ConditionalFieldAccess`` atoms are recognised and stripped —
+  the zero-filled halo load realises them);
+* ``boundary_handling=None`` (``ghost_layers=None``): only the interior
+  ``[g, N-g)`` of every axis is written, ``g`` = largest ``|offset|`` of any
+  access (pystencils' ``required_ghost_layers`` rule), the border keeps what the
+  caller allocated (zeros in the torch op);
+* statements are evaluated in order: subexpressions, then main assignments;
+  free non-field symbols become scalar kernel parameters (sorted by name).
+
+``StencilKernel`` keeps pystencils' ``KernelFunction`` surface the reference
+touches (``function_name``, ``fields_accessed``, ``fields_read``,
+``fields_written``, ``get_parameters()``, ``compile()``) and picks the
+schedule the HIP emitter prints (``hip_emitter.py``).
+"""
+import hashlib
+from dataclasses import dataclass, field as dc_field
+from typing import Dict, List, Tuple
+
+import numpy as np
+import sympy as sp
+
+from ..ps import AssignmentCollection, Field
+from ..ps.conditional import ConditionalFieldAccess
+
+__all__ = ['StencilKernel', 'KernelIR', 'lower', 'Parameter']
+
+
+def _c_ident(s):
+    out = ''.join(ch if ch.isalnum() else '_' for ch in str(s))
+    return out if not out[:1].isdigit() else '_' + out
+
+
+def _offset_tag(offsets):
+    return '_'.join(f"m{-o}" if o < 0 else str(o) for o in offsets)
+
+
+@dataclass(frozen=True)
+class ReadAccess:
+    field: Field
+    offsets: Tuple[int, ...]
+    index: Tuple[int, ...]
+
+    @property
+    def var(self):
+        tag = _offset_tag(self.offsets)
+        idx = ('_i' + '_'.join(str(i) for i in self.index)) if self.index else ''
+        return f"v_{_c_ident(self.field.name)}_{tag}{idx}"
+
+
+@dataclass
+class KernelIR:
+    ndim: int
+    fields: List[Field]                    # pointer-argument order (sorted by name)
+    fields_read: List[Field]
+    fields_written: List[Field]
+    reads: List[ReadAccess]                # unique reads, sorted
+    scalars: List[sp.Symbol]               # scalar parameters, sorted by name
+    subexpressions: List[Tuple[sp.Symbol, sp.Expr]]
+    stores: List[Tuple[Field, Tuple[int, ...], Tuple[int, ...], sp.Expr]]  # field, lhs offsets, index, rhs
+    zeros: bool                            # zero-padded reads, full iteration space
+    ghost_layers: int                      # interior-only iteration when not zeros
+    radius: Tuple[int, ...]                # per-axis max |read offset|
+    compute_dtype: np.dtype
+    symbol_names: Dict[sp.Symbol, str] = dc_field(default_factory=dict)
+
+    @property
+    def pointwise(self):
+        return all(all(o == 0 for o in r.offsets) for r in self.reads) and \
+            all(all(o == 0 for o in s[1]) for s in self.stores)
+
+    @property
+    def has_index_dims(self):
+        return any(f.index_dimensions > 0 for f in self.fields)
+
+    @property
+    def stencil_fields(self):
+        """Read fields with at least one non-zero offset (they need halo data)."""
+        return sorted({r.field for r in self.reads if any(o != 0 for o in r.offsets)}, key=lambda f: f.name)
+
+    @property
+    def point_fields(self):
+        st = set(self.stencil_fields)
+        return sorted({r.field for r in self.reads if r.field not in st}, key=lambda f: f.name)
+
+    def iteration_bounds(self, shape):
+        """Per-axis [lo, hi) of the cells this kernel writes."""
+        g = 0 if self.zeros else self.ghost_layers
+        return [(g, max(g, int(n) - g)) for n in shape]
+
+
+def _strip_conditionals(expr):
+    if not expr.has(ConditionalFieldAccess):
+        return expr, False
+    return expr.replace(lambda e: isinstance(e, ConditionalFieldAccess), lambda e: e.args[0]), True
+
+
+def lower(assignments, boundary_handling=None, data_type=None):
+    """Build the ``KernelIR`` of an assignment collection."""
+    if not isinstance(assignments, AssignmentCollection):
+        assignments = AssignmentCollection(list(assignments), [])
+    zeros = boundary_handling is not None and str(getattr(boundary_handling, 'value', boundary_handling)) \
+        in ('zeros', 'valid')
+
+    subexpressions, stores = [], []
+    had_conditionals = False
+    ordered = list(assignments.subexpressions) + list(assignments.main_assignments)
+    for a in ordered:
+        rhs, had = _strip_conditionals(a.rhs)
+        had_conditionals |= had
+        if isinstance(a.lhs, Field.Access):
+            stores.append((a.lhs.field, tuple(a.lhs.offsets), tuple(a.lhs.index), rhs))
+        else:
+            subexpressions.append((a.lhs, rhs))
+    zeros = zeros or had_conditionals
+    if not stores:
+        raise ValueError('kernel without field writes')
+
+    reads = set()
+    scalars = set()
+    bound = {s for s, _ in subexpressions}
+    all_accesses = []
+    for _, rhs in subexpressions:
+        for s in rhs.free_symbols:
+            if isinstance(s, Field.Access):
+                reads.add(ReadAccess(s.field, tuple(s.offsets), tuple(s.index)))
+                all_accesses.append(s.offsets)
+            elif s not in bound:
+                scalars.add(s)
+    for _, _, _, rhs in stores:
+        for s in rhs.free_symbols:
+            if isinstance(s, Field.Access):
+                reads.add(ReadAccess(s.field, tuple(s.offsets), tuple(s.index)))
+                all_accesses.append(s.offsets)
+            elif s not in bound:
+                scalars.add(s)
+    all_accesses += [s[1] for s in stores]
+
+    fields_written = sorted({s[0] for s in stores}, key=lambda f: f.name)
+    fields_read = sorted({r.field for r in reads}, key=lambda f: f.name)
+    fields = sorted(set(fields_written) | set(fields_read), key=lambda f: f.name)
+    names = [f.name for f in fields]
+    if len(set(names)) != len(names):
+        raise ValueError(f"two different fields share a name: {names}")
+    ndims = {f.spatial_dimensions for f in fields}
+    if len(ndims) != 1:
+        raise ValueError(f"all fields of a kernel must have the same number of spatial dimensions, got {ndims}")
+    ndim = ndims.pop()
+    fixed = [tuple(int(s) for s in f.spatial_shape) for f in fields if f.has_fixed_shape]
+    if fixed and any(s != fixed[0] for s in fixed):
+        raise ValueError(f"fields of one kernel must share their spatial shape, got {fixed}")
+
+    radius = tuple(max([abs(int(r.offsets[d])) for r in reads] + [0]) for d in range(ndim))
+    ghost_layers = max([max([abs(int(o)) for o in offs] + [0]) for offs in all_accesses] + [0])
+
+    dtypes = {f.dtype.numpy_dtype for f in fields}
+    if data_type is not None:
+        from ..ps.data_types import create_type
+        compute = create_type(data_type).numpy_dtype
+    elif np.dtype('float64') in dtypes:
+        compute = np.dtype('float64')
+    else:
+        compute = np.dtype('float32')          # float32 and float16 storage compute in float32
+    for f in fields:
+        if not f.dtype.is_float:
+            raise NotImplementedError(f"field '{f.name}' has non-floating dtype {f.dtype}")
+
+    reads = sorted(reads, key=lambda r: (r.field.name, r.offsets, r.index))
+    scalars = sorted(scalars, key=lambda s: s.name)
+    ir = KernelIR(ndim=ndim, fields=fields, fields_read=fields_read, fields_written=fields_written,
+                  reads=reads, scalars=scalars, subexpressions=subexpressions, stores=stores, zeros=zeros,
+                  ghost_layers=ghost_layers, radius=radius, compute_dtype=compute)
+    sym = {}
+    for r in reads:
+        acc = Field.Access(r.field, r.offsets, r.index)
+        sym[acc] = r.var
+    for s in scalars:
+        sym[s] = f"p_{_c_ident(s.name)}"
+    for i, (s, _) in enumerate(subexpressions):
+        sym[s] = f"s{i}_{_c_ident(s.name)}"
+    ir.symbol_names = sym
+    return ir
+
+
+class Parameter:
+    """Kernel parameter (mirrors pystencils ``KernelFunction.Parameter``: ``.symbol.name``)."""
+
+    def __init__(self, symbol, field=None):
+        self.symbol = symbol
+        self.field = field
+        self.is_field_parameter = field is not None
+
+    @property
+    def field_name(self):
+        return self.field.name if self.field is not None else None
+
+    def __repr__(self):
+        return f"Parameter({self.symbol.name})"
+
+
+class StencilKernel:
+    """One forward or backward kernel of an ``AutoDiffOp`` for one target ('gpu' / 'cpu')."""
+
+    def __init__(self, assignments, boundary_handling=None, function_name='kernel', target='gpu',
+                 data_type=None, cpu_openmp=False, gpu_indexing_params=None, **kwargs):
+        self.assignments = assignments
+        self.boundary_handling = boundary_handling
+        self.function_name = function_name
+        self.target = target
+        self.ir = lower(assignments, boundary_handling, data_type)
+        self.cpu_openmp = cpu_openmp
+        self.tuning = dict(gpu_indexing_params or {})
+        self.extra_kwargs = kwargs
+        self._compiled = None
+
+    # pystencils KernelFunction-like surface -----------------------------------------------------
+    @property
+    def fields_accessed(self):
+        return set(self.ir.fields)
+
+    @property
+    def fields_read(self):
+        return set(self.ir.fields_read)
+
+    @property
+    def fields_written(self):
+        return set(self.ir.fields_written)
+
+    @property
+    def backend(self):
+        return 'hip' if self.target == 'gpu' else 'c'
+
+    def get_parameters(self):
+        params = [Parameter(sp.Symbol(f.name), f) for f in self.ir.fields]
+        params += [Parameter(s) for s in self.ir.scalars]
+        return params
+
+    @property
+    def code(self):
+        return self.compile().code
+
+    @property
+    def hash(self):
+        return hashlib.sha256(self.code.encode()).hexdigest()[:16]
+
+    def compile(self):
+        if self._compiled is None:
+            if self.target == 'gpu':
+                from .hip_kernel import HipStencilKernel
+                self._compiled = HipStencilKernel(self)
+            else:
+                from .cpu_kernel import CpuStencilKernel
+                self._compiled = CpuStencilKernel(self)
+        return self._compiled
+
+    def __call__(self, **kwargs):
+        return self.compile()(**kwargs)
+
+    def __str__(self):
+        return self.code

@@ -1,0 +1,138 @@
+// libpsad_hip.so — C ABI for hiprtc compilation, module loading and kernel launch on MI355X.
+// See include/psad.h for the contract and the reference interfaces each entry point replaces.
+#include "psad.h"
+
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+namespace {
+
+int rtc_code(hiprtcResult r) { return r == HIPRTC_SUCCESS ? 0 : PSAD_HIPRTC_ERROR_BASE + static_cast<int>(r); }
+
+void copy_log(hiprtcProgram prog, char* log, size_t log_size) {
+    if (log == nullptr || log_size == 0) return;
+    log[0] = '\0';
+    size_t n = 0;
+    if (hiprtcGetProgramLogSize(prog, &n) != HIPRTC_SUCCESS || n == 0) return;
+    std::vector<char> buf(n + 1, '\0');
+    if (hiprtcGetProgramLog(prog, buf.data()) != HIPRTC_SUCCESS) return;
+    size_t m = std::min(log_size - 1, std::strlen(buf.data()));
+    std::memcpy(log, buf.data(), m);
+    log[m] = '\0';
+}
+
+}  // namespace
+
+extern "C" {
+
+int psad_abi_version(void) { return 1; }
+
+int psad_rtc_version(void) {
+    int major = 0, minor = 0;
+    if (hiprtcVersion(&major, &minor) != HIPRTC_SUCCESS) return -1;
+    return major * 100 + minor;
+}
+
+int psad_rtc_compile(const char* source, const char* program_name, const char* const* options, int n_options,
+                     void** code, size_t* code_size, char* log, size_t log_size) {
+    if (source == nullptr || code == nullptr || code_size == nullptr) return static_cast<int>(hipErrorInvalidValue);
+    *code = nullptr;
+    *code_size = 0;
+    hiprtcProgram prog;
+    hiprtcResult r = hiprtcCreateProgram(&prog, source, program_name ? program_name : "psad.hip", 0, nullptr, nullptr);
+    if (r != HIPRTC_SUCCESS) return rtc_code(r);
+    r = hiprtcCompileProgram(prog, n_options, const_cast<const char**>(options));
+    copy_log(prog, log, log_size);
+    if (r == HIPRTC_SUCCESS) {
+        size_t n = 0;
+        r = hiprtcGetCodeSize(prog, &n);
+        if (r == HIPRTC_SUCCESS) {
+            void* buf = std::malloc(n);
+            if (buf == nullptr) {
+                hiprtcDestroyProgram(&prog);
+                return static_cast<int>(hipErrorOutOfMemory);
+            }
+            r = hiprtcGetCode(prog, static_cast<char*>(buf));
+            if (r == HIPRTC_SUCCESS) {
+                *code = buf;
+                *code_size = n;
+            } else {
+                std::free(buf);
+            }
+        }
+    }
+    hiprtcDestroyProgram(&prog);
+    return rtc_code(r);
+}
+
+void psad_free(void* p) { std::free(p); }
+
+int psad_module_load(const void* code, size_t code_size, void** module) {
+    (void)code_size;
+    if (code == nullptr || module == nullptr) return static_cast<int>(hipErrorInvalidValue);
+    hipModule_t m = nullptr;
+    hipError_t e = hipModuleLoadData(&m, code);
+    *module = (e == hipSuccess) ? static_cast<void*>(m) : nullptr;
+    return static_cast<int>(e);
+}
+
+int psad_module_unload(void* module) {
+    if (module == nullptr) return 0;
+    return static_cast<int>(hipModuleUnload(static_cast<hipModule_t>(module)));
+}
+
+int psad_module_get_function(void* module, const char* name, void** function) {
+    if (module == nullptr || name == nullptr || function == nullptr) return static_cast<int>(hipErrorInvalidValue);
+    hipFunction_t f = nullptr;
+    hipError_t e = hipModuleGetFunction(&f, static_cast<hipModule_t>(module), name);
+    *function = (e == hipSuccess) ? static_cast<void*>(f) : nullptr;
+    return static_cast<int>(e);
+}
+
+int psad_launch(void* function, unsigned grid_x, unsigned grid_y, unsigned grid_z, unsigned block_x,
+                unsigned block_y, unsigned block_z, unsigned shared_bytes, void* stream, const void* args,
+                size_t args_size) {
+    if (function == nullptr) return static_cast<int>(hipErrorInvalidValue);
+    if (grid_x == 0 || grid_y == 0 || grid_z == 0) return 0;   // empty launch: nothing to do
+    size_t size = args_size;
+    void* config[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, const_cast<void*>(args), HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
+                      HIP_LAUNCH_PARAM_END};
+    hipError_t e = hipModuleLaunchKernel(static_cast<hipFunction_t>(function), grid_x, grid_y, grid_z, block_x,
+                                         block_y, block_z, shared_bytes, static_cast<hipStream_t>(stream), nullptr,
+                                         args_size ? config : nullptr);
+    return static_cast<int>(e);
+}
+
+int psad_function_attributes(void* function, int* num_regs, int* shared_bytes, int* max_threads) {
+    hipFunction_t f = static_cast<hipFunction_t>(function);
+    hipError_t e;
+    if (num_regs && (e = hipFuncGetAttribute(num_regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, f)) != hipSuccess)
+        return static_cast<int>(e);
+    if (shared_bytes && (e = hipFuncGetAttribute(shared_bytes, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, f)) != hipSuccess)
+        return static_cast<int>(e);
+    if (max_threads &&
+        (e = hipFuncGetAttribute(max_threads, HIP_FUNC_ATTRIBUTE_MAX_THREADS_PER_BLOCK, f)) != hipSuccess)
+        return static_cast<int>(e);
+    return 0;
+}
+
+int psad_get_device(int* device) { return static_cast<int>(hipGetDevice(device)); }
+
+int psad_device_count(int* count) { return static_cast<int>(hipGetDeviceCount(count)); }
+
+int psad_last_error(void) { return static_cast<int>(hipGetLastError()); }
+
+int psad_memcpy_d2d_async(void* dst, const void* src, size_t bytes, void* stream) {
+    return static_cast<int>(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
+}
+
+const char* psad_error_string(int code) {
+    if (code >= PSAD_HIPRTC_ERROR_BASE) return hiprtcGetErrorString(static_cast<hiprtcResult>(code - PSAD_HIPRTC_ERROR_BASE));
+    return hipGetErrorString(static_cast<hipError_t>(code));
+}
+
+}  // extern "C"

@@ -1,0 +1,249 @@
+"""GPU parity: HIP kernels (through the C ABI) vs the oracle on the same inputs.
+
+Tolerances (north_star: 1e-6 relative for fp32):
+  fp32: |gpu - ref| <= 1e-6 * max|ref|, ref = float64 evaluation of the same inputs
+  fp64: 1e-12 relative
+  fp16 storage (27-point): output rounded to fp16 -> 1e-3 relative (no fp16 path in the reference)
+"""
+import itertools
+
+import numpy as np
+import pytest
+import sympy as sp
+
+import pystencils_autodiff_amd as pa
+from oracle import evaluate as OE
+from oracle import stencils as S
+from pystencils_autodiff_amd import ps
+from pystencils_autodiff_amd import workloads as W
+from tests.conftest import assert_close_rel, golden
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip('torch')
+
+TOL = {np.float32: 1e-6, np.float64: 1e-12, np.float16: 1e-3}
+
+
+def _op(ac, bh='zeros', **kw):
+    op = pa.AutoDiffOp(ac, boundary_handling=bh, **kw)
+    return op, op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+
+
+def _run(fn, inputs, grads):
+    ins = [torch.from_numpy(np.ascontiguousarray(a)).cuda().requires_grad_(True) for a in inputs]
+    outs = fn.apply(*ins)
+    torch.autograd.backward(list(outs), [torch.from_numpy(np.ascontiguousarray(g)).cuda() for g in grads])
+    torch.cuda.synchronize()
+    return [o.detach().cpu().numpy() for o in outs], [i.grad.cpu().numpy() if i.grad is not None else None
+                                                      for i in ins]
+
+
+@pytest.mark.parametrize('case,builder,bh', [
+    ('diffusion7_f32_32cube', lambda: W.diffusion_7pt(), 'zeros'),
+    ('asym7_f32_16cube', lambda: W.asym_7pt(), 'zeros'),
+    ('laplace5_f32_64x64_zeros', lambda: W.laplace_5pt(), 'zeros'),
+    ('laplace5_f32_64x64_none', lambda: W.laplace_5pt(), None),
+    ('stencil27_f16_16cube', lambda: W.stencil_27pt(), 'zeros'),
+])
+def test_golden_linear_stencils(case, builder, bh):
+    g = golden(case)
+    op, fn = _op(builder(), bh)
+    (out,), (du,) = _run(fn, [g['u']], [g['diffout']])
+    tol = TOL[g['u'].dtype.type]
+    assert_close_rel(out, g['out'], tol, f'{case} forward')
+    assert_close_rel(du, g['diffu'], tol, f'{case} adjoint')
+    k = op.forward_ast_gpu.compile()
+    assert k.last_variant[0] == 'march'
+
+
+def test_golden_readme_op():
+    g = golden('readme_f32_20x30')
+    op, fn = _op(W.readme_op(), None)
+    (z,), (dx, dy) = _run(fn, [g['x'], g['y']], [g['diffz']])
+    assert_close_rel(z, g['z'], 1e-6, 'z')
+    assert_close_rel(dx, g['diffx'], 1e-6, 'diffx')
+    assert_close_rel(dy, g['diffy'], 1e-6, 'diffy')
+    assert op.forward_ast_gpu.compile().last_variant[0] == 'pointwise'
+
+
+def test_golden_tfmad_2d_f64():
+    g = golden('tfmad2d_f64_5x7')
+    a, b, out = ps.fields("a, b, out: float64[5,7]")
+    cont = 2 * ps.fd.Diff(a, 0) - 1.5 * ps.fd.Diff(a, 1) - ps.fd.Diff(b, 0) + 3 * ps.fd.Diff(b, 1)
+    ac = ps.AssignmentCollection([ps.Assignment(out.center(), ps.fd.Discretization2ndOrder(dx=1)(cont)
+                                                + 1.2 * a.center())], [])
+    _, fn = _op(ac)
+    (o,), (da, db) = _run(fn, [g['a'], g['b']], [g['diffout']])
+    assert_close_rel(o, g['out'], 1e-12, 'out')
+    assert_close_rel(da, g['diffa'], 1e-12, 'diffa')
+    assert_close_rel(db, g['diffb'], 1e-12, 'diffb')
+
+
+def test_golden_three_outputs_f64():
+    g = golden('three_outputs_f64_21x13')
+    a, b, o1, o2, o3 = ps.fields("a, b, out1, out2, out3: float64[21,13]")
+    ac = ps.AssignmentCollection({o1.center: a.center + b.center, o2.center: a.center - b.center,
+                                  o3.center: sp.exp(b[-1, 0])})
+    _, fn = _op(ac)
+    outs, (da, db) = _run(fn, [g['a'], g['b']], [g['diffout1'], g['diffout2'], g['diffout3']])
+    for got, name in zip(outs, ('out1', 'out2', 'out3')):
+        assert_close_rel(got, g[name], 1e-12, name)
+    assert_close_rel(da, g['diffa'], 1e-12, 'diffa')
+    assert_close_rel(db, g['diffb'], 1e-12, 'diffb')
+
+
+@pytest.mark.parametrize('with_offsets', (False, True))
+def test_gradcheck_torch_native_gpu(with_offsets):
+    # reference tests/test_tfmad.py:186-231 with with_cuda=True
+    a, b, out = ps.fields("a, b, out: float64[5,7]")
+    if with_offsets:
+        cont = 2 * ps.fd.Diff(a, 0) - 1.5 * ps.fd.Diff(a, 1) - ps.fd.Diff(b, 0) + 3 * ps.fd.Diff(b, 1)
+        asg = ps.Assignment(out.center(), ps.fd.Discretization2ndOrder(dx=1)(cont) + 1.2 * a.center())
+    else:
+        asg = ps.Assignment(out.center(), 1.2 * a.center + 0.1 * b.center)
+    op = pa.AutoDiffOp(ps.AssignmentCollection([asg], []), boundary_handling='zeros',
+                       diff_mode='transposed-forward')
+    fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    at = torch.zeros(*a.shape, dtype=torch.float64, requires_grad=True).cuda()
+    bt = torch.zeros(*b.shape, dtype=torch.float64, requires_grad=True).cuda()
+    assert torch.autograd.gradcheck(fn.apply, (at, bt), atol=1e-4, raise_exception=True)
+    at = torch.rand(*a.shape, dtype=torch.float64).cuda().requires_grad_(True)
+    bt = torch.rand(*b.shape, dtype=torch.float64).cuda().requires_grad_(True)
+    assert torch.autograd.gradcheck(fn.apply, (at, bt), atol=1e-6, raise_exception=True)
+
+
+def test_gradcheck_two_outputs_gpu():
+    # reference tests/test_tfmad.py:234-285 with with_cuda=True
+    a, b, o1, o2, o3 = ps.fields("a, b, out1, out2, out3: float64[21,13]")
+    ac = ps.AssignmentCollection({o1.center: a.center + b.center, o2.center: a.center - b.center,
+                                  o3.center: sp.exp(b[-1, 0])})
+    op = pa.AutoDiffOp(ac, boundary_handling='zeros', diff_mode='transposed-forward')
+    fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    at = torch.zeros(*a.shape, dtype=torch.float64).cuda().requires_grad_(True)
+    bt = torch.zeros(*b.shape, dtype=torch.float64).cuda().requires_grad_(True)
+    assert torch.autograd.gradcheck(fn.apply, (at, bt), atol=1e-4, raise_exception=True)
+
+
+def _random_op_case(shape, dtype, bh, taps_per_field=2, seed=0, nonlinear=False):
+    """A random multi-field stencil, evaluated through every schedule vs the numpy oracle."""
+    rng = np.random.default_rng(seed)
+    nd = len(shape)
+    tname = {np.float32: 'float32', np.float64: 'float64'}[dtype]
+    a, b, out = ps.fields(f"a, b, out: {tname}[{nd}d]")
+    offs = [o for o in itertools.product((-1, 0, 1), repeat=nd)]
+    rhs = 0
+    for f in (a, b):
+        for k in rng.choice(len(offs), taps_per_field, replace=False):
+            rhs += sp.Float(round(float(rng.uniform(-1, 1)), 3)) * f[offs[k]]
+    if nonlinear:
+        rhs += sp.Float(0.25) * sp.sin(a.center) * b[offs[rng.integers(len(offs))]]
+    return ps.AssignmentCollection({out.center: rhs})
+
+
+@pytest.mark.parametrize('shape', [(17, 33, 45), (9, 20, 128), (5, 7, 3), (64, 3, 70), (40, 37), (3, 260)])
+@pytest.mark.parametrize('bh', ['zeros', None])
+@pytest.mark.parametrize('dtype', [np.float32, np.float64])
+def test_schedules_vs_oracle(shape, bh, dtype):
+    ac = _random_op_case(shape, dtype, bh, seed=sum(shape), nonlinear=True)
+    op = pa.AutoDiffOp(ac, boundary_handling=bh)
+    rng = np.random.default_rng(1)
+    a = rng.uniform(-1, 1, shape).astype(dtype)
+    b = rng.uniform(-1, 1, shape).astype(dtype)
+    d = rng.uniform(-1, 1, shape).astype(dtype)
+    ref = OE.evaluate(op.forward_assignments, {'a': a, 'b': b}, boundary_handling=bh)['out']
+    refb = OE.evaluate(op.backward_assignments, {'a': a, 'b': b, 'diffout': d}, boundary_handling=bh)
+    fk = op.forward_ast_gpu.compile()
+    bk = op.backward_ast_gpu.compile()
+    ta, tb, td = (torch.from_numpy(x).cuda() for x in (a, b, d))
+    for sched in ('march', 'generic'):
+        out = torch.zeros(shape, dtype=ta.dtype, device='cuda')
+        fk(a=ta, b=tb, out=out, force_schedule=sched)
+        da = torch.zeros_like(out)
+        db = torch.zeros_like(out)
+        bk(a=ta, b=tb, diffout=td, diffa=da, diffb=db, force_schedule=sched)
+        torch.cuda.synchronize()
+        tol = TOL[dtype]
+        assert_close_rel(out.cpu().numpy(), ref, tol, f'{sched} forward')
+        assert_close_rel(da.cpu().numpy(), refb['diffa'], tol, f'{sched} diffa')
+        assert_close_rel(db.cpu().numpy(), refb['diffb'], tol, f'{sched} diffb')
+
+
+def test_march_unaligned_variant():
+    """X not a multiple of the vector width and an offset base pointer take the VE=1 variant."""
+    ac = W.asym_7pt()
+    op = pa.AutoDiffOp(ac, boundary_handling='zeros')
+    k = op.forward_ast_gpu.compile()
+    rng = np.random.default_rng(3)
+    u = rng.uniform(0, 1, (8, 9, 31)).astype(np.float32)
+    buf = torch.zeros(u.size + 1, device='cuda')
+    tu = buf[1:].view(u.shape)
+    tu.copy_(torch.from_numpy(u))
+    out = torch.zeros(u.shape, device='cuda')
+    k(u=tu, out=out)
+    torch.cuda.synchronize()
+    assert k.last_variant[1].VE == 1
+    assert_close_rel(out.cpu().numpy(), S.linear_stencil(u, S.taps_asym_7pt()), 1e-6)
+
+
+def test_march_halo_planes_equal_full_domain():
+    """Two z-slabs with halo planes from their neighbour == one full-domain launch (bitwise)."""
+    op = pa.AutoDiffOp(W.asym_7pt(), boundary_handling='zeros')
+    k = op.forward_ast_gpu.compile()
+    g = torch.Generator().manual_seed(0)
+    u = torch.rand((24, 20, 64), generator=g).cuda()
+    full = torch.empty_like(u)
+    k(u=u, out=full)
+    lo, hi = u[:10].contiguous(), u[10:].contiguous()
+    out_lo, out_hi = torch.empty_like(lo), torch.empty_like(hi)
+    k(u=lo, out=out_lo, halos={'u': (None, hi[:1].contiguous())})
+    k(u=hi, out=out_hi, halos={'u': (lo[-1:].contiguous(), None)})
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat([out_lo, out_hi]), full)
+
+
+def test_adjoint_dot_product_identity_large():
+    """<A u, d> == <u, A^T d> for the forward / backward kernels at 256^3 (size-independent property)."""
+    op, fn = _op(W.asym_7pt())
+    g = torch.Generator().manual_seed(0)
+    n = 256
+    u = torch.rand((n, n, n), generator=g, dtype=torch.float32).cuda().requires_grad_(True)
+    d = (torch.rand((n, n, n), generator=g, dtype=torch.float32) * 2 - 1).cuda()
+    (out,) = fn.apply(u)
+    out.backward(d)
+    lhs = torch.sum(out.double() * d.double()).item()
+    rhs = torch.sum(u.detach().double() * u.grad.double()).item()
+    assert abs(lhs - rhs) <= 1e-5 * max(abs(lhs), 1.0), (lhs, rhs)
+
+
+def test_diffusion_512_vs_c_oracle():
+    """BASELINE config 3 size: forward + adjoint vs the C restatement of the reference CPU kernel."""
+    from oracle import cref
+    lib = cref.load()
+    op, fn = _op(W.diffusion_7pt())
+    g = torch.Generator().manual_seed(0)
+    n = 512
+    u = torch.rand((n, n, n), generator=g, dtype=torch.float32)
+    d = torch.rand((n, n, n), generator=g, dtype=torch.float32) * 2 - 1
+    uc = u.cuda().requires_grad_(True)
+    (out,) = fn.apply(uc)
+    out.backward(d.cuda())
+    ref_out = lib.diffusion7_f32(u.numpy(), W.ALPHA)
+    ref_du = lib.diffusion7_f32(d.numpy(), W.ALPHA)
+    # fp32 C reference vs fp32 GPU: both round; compare at 2 ulp of the field scale
+    assert_close_rel(out.detach().cpu().numpy(), ref_out, 1e-6, 'out 512^3')
+    assert_close_rel(uc.grad.cpu().numpy(), ref_du, 1e-6, 'diffu 512^3')
+
+
+def test_vector_field_generic_schedule():
+    f, out = ps.fields("f(2), out: float64[12,10]")
+    ac = ps.AssignmentCollection({out.center: f.center(0) * f[1, 0](1) - f[0, -1](0)})
+    op = pa.AutoDiffOp(ac, boundary_handling='zeros')
+    k = op.forward_ast_gpu.compile()
+    rng = np.random.default_rng(0)
+    fa = rng.uniform(-1, 1, (12, 10, 2))
+    o = torch.zeros((12, 10), dtype=torch.float64, device='cuda')
+    k(f=torch.from_numpy(fa).cuda(), out=o)
+    ref = OE.evaluate(op.forward_assignments, {'f': fa}, boundary_handling='zeros')['out']
+    assert k.last_variant[0] == 'generic'
+    assert_close_rel(o.cpu().numpy(), ref, 1e-12)
