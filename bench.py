@@ -55,7 +55,7 @@ def cpu_baseline(budget_s):
         lib.diffusion7_f32(d, 0.1, du)       # adjoint sweep (same symmetric stencil on diffout)
         reps += 1
         el = time.perf_counter() - t0
-        if el >= budget_s or reps >= 200:
+        if el >= budget_s or reps >= 5000:
             break
     cells = reps * u.size
     return {'value': round(cells / el / 1e6, 2), 'unit': 'Mcells/s', 'cores': threads, 'kind': 'port',
@@ -64,15 +64,17 @@ def cpu_baseline(budget_s):
                       f'{threads} OpenMP threads, {el:.1f} s'}
 
 
-def load_traffic(workload):
-    """HBM bytes per launch from the committed PMC summary (profiles/traffic.json), if present."""
+def load_traffic(workload, kernel):
+    """HBM bytes per launch of ``kernel`` from the committed PMC summary (profiles/traffic.json):
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled (gfx950 wide-read correction)."""
     path = os.path.join(ROOT, 'profiles', 'traffic.json')
     try:
         with open(path) as fh:
-            data = json.load(fh)
-        return data.get(workload)
+            entry = json.load(fh).get(workload) or {}
     except (OSError, ValueError):
-        return None
+        return None, None
+    k = entry.get('kernels', {}).get(kernel)
+    return (k['total'] if k else None), entry.get('source')
 
 
 def main():
@@ -196,7 +198,7 @@ def main():
             except Exception as exc:  # noqa: BLE001 - report, don't fail the GPU bench
                 cpu = {'value': None, 'unit': 'Mcells/s', 'cores': None, 'kind': 'port', 'sample': f'failed: {exc}'}
         workload = f'diffusion7_f32_{n}^3'
-        traffic = load_traffic(workload)
+        traffic, traffic_src = load_traffic(workload, f'{fwd_k.name}_march')
         res = {
             'metric': f'Mcells/s forward+backward, 3D 7-point fp32 {n}^3',
             'value': round(value, 1),
@@ -221,6 +223,7 @@ def main():
                                             / (HBM_PEAK_GBS * world), 4),
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
+                         'traffic_source': traffic_src,
                          'kernel': f'{fwd_k.name}_march (forward sweep; adjoint moves the same bytes)',
                          'bytes_per_launch': bytes_fwd},
             'cpu_baseline': cpu,

@@ -19,20 +19,48 @@ from .hip_emitter import MarchConfig, emit_generic, emit_march, emit_pointwise, 
 __all__ = ['HipStencilKernel', 'default_march_config']
 
 
-def default_march_config(ir, ve):
-    """Tile shape per dimensionality (overridable via ``gpu_indexing_params`` or ``PSAD_MARCH``)."""
+def default_march_config(ir, ve, shape=None, tuning=None):
+    """Tile shape for a kernel and field shape (measured on MI355X).
+
+    Star stencils (planes behind the centre read only at (0,0): "lite" ring) take the largest
+    tile, 256×32 (CX=4, NR=8), that keeps LDS ≤ 80 KB (two workgroups per CU); box stencils
+    (27-point: full ring) a 128×16 tile; 2-D fields march their rows with 4 waves across a
+    512-cell row segment ('yx' tiles measured slower at 4096²). Non-temporal stores
+    for the outputs (written once, never re-read by the sweep). Overrides: ``gpu_indexing_params``
+    or ``PSAD_MARCH="CX=..,NR=.."``.
+    """
+    from .hip_emitter import lite_fields
+    cfg = dict(CX=4, WX=1, NR=8, NT_STORE=True, PD=1, FULL_RING=False, VIEW2D='yx')
+    probe = MarchConfig(VE=ve, **cfg)
+    if ir.ndim == 3 and set(ir.stencil_fields) - lite_fields(ir, probe):
+        cfg.update(CX=2, NR=4)                       # box stencil: full ring, LDS/VALU bound
     if ir.ndim == 2:
-        cfg = dict(CX=1, WX=4, NR=1)
-    else:
-        cfg = dict(CX=2, WX=1, NR=2)
+        cfg.update(CX=2, WX=4, NR=1, VIEW2D='zy')    # rows marched, 4 waves across x (4096²: 0.081 ms)
+    if shape is not None:
+        X = int(shape[-1])
+        while cfg['CX'] > 1 and 64 * cfg['CX'] // 2 >= X:
+            cfg['CX'] //= 2
+        ny = int(shape[-2]) if ir.ndim == 3 or cfg['VIEW2D'] == 'yx' else 1
+        while cfg['NR'] > 1 and 4 * cfg['NR'] // 2 >= ny:
+            cfg['NR'] //= 2
+    while march_geometry(ir, MarchConfig(VE=ve, **cfg))['lds_bytes'] > 80 * 1024 and (cfg['NR'] > 1 or cfg['CX'] > 1):
+        if cfg['NR'] >= cfg['CX'] and cfg['NR'] > 1:
+            cfg['NR'] //= 2
+        else:
+            cfg['CX'] //= 2
     env = os.environ.get('PSAD_MARCH')
+    over = dict(tuning or {})
     if env:
         for kv in env.split(','):
             k, v = kv.split('=')
-            cfg[k.strip()] = int(v)
-    cfg.pop('ZC', None)
-    cfg.pop('BLOCKS', None)
-    cfg.pop('NT', None)
+            over[k.strip()] = v.strip() if k.strip() == 'VIEW2D' else int(v)
+    for k, v in over.items():
+        if k in ('CX', 'WX', 'NR', 'PD'):
+            cfg[k] = int(v)
+        elif k in ('NT_STORE', 'FULL_RING'):
+            cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
+        elif k == 'VIEW2D':
+            cfg[k] = str(v)
     return MarchConfig(VE=ve, **cfg)
 
 
@@ -64,14 +92,8 @@ class HipStencilKernel:
     def _vec_elems(self):
         return 16 // self.ir.fields[0].dtype.itemsize
 
-    def _march_cfg(self, ve):
-        cfg = default_march_config(self.ir, ve)
-        over = {k: v for k, v in self.kernel.tuning.items() if k in ('CX', 'WX', 'NR', 'NT_STORE')}
-        if over:
-            d = dict(CX=cfg.CX, WX=cfg.WX, NR=cfg.NR, VE=ve, NT_STORE=cfg.NT_STORE)
-            d.update(over)
-            cfg = MarchConfig(**d)
-        return cfg
+    def _march_cfg(self, ve, shape=None):
+        return default_march_config(self.ir, ve, shape, self.kernel.tuning)
 
     def source(self, variant):
         if variant not in self._variants:
@@ -89,7 +111,11 @@ class HipStencilKernel:
     def primary_variant(self):
         s = self.schedule()
         if s == 'march':
-            return ('march', self._march_cfg(self._vec_elems()))
+            shape = None
+            fixed = [f for f in self.ir.fields if f.has_fixed_shape]
+            if fixed:
+                shape = tuple(int(x) for x in fixed[0].spatial_shape)
+            return ('march', self._march_cfg(self._vec_elems(), shape))
         return (s,)
 
     @property
@@ -210,6 +236,12 @@ class HipStencilKernel:
         if ir.ndim == 3:
             Z, Y, X = shape
             (zlo, zhi), (ylo, yhi), (xlo, xhi) = bounds
+        elif cfg.VIEW2D == 'yx':
+            Z, (Y, X) = 1, shape
+            (zlo, zhi) = (0, 1)
+            (ylo, yhi), (xlo, xhi) = bounds
+            if z_range is not None:
+                raise ValueError("z ranges need the 'zy' view of 2-D fields")
         else:
             Z, X = shape
             Y = 1
@@ -221,7 +253,7 @@ class HipStencilKernel:
         nz = max(0, zhi - zlo)
         target = int(self.kernel.tuning.get('BLOCKS', os.environ.get('PSAD_MARCH_BLOCKS', 2048)))
         zc = self.kernel.tuning.get('ZC') or int(os.environ.get('PSAD_MARCH_ZC', 0)) or \
-            max(1, min(nz, math.ceil(nz * nt / target)))
+            max(min(nz, 32), min(nz, math.ceil(nz * nt / target)))
         zc = max(zc, min(nz, 4 * max(1, march_geometry(ir, cfg)['RZ'])))
         nchunks = math.ceil(nz / zc) if nz else 0
         return dict(Z=Z, Y=Y, X=X, zlo=zlo, zhi=zhi, ylo=ylo, yhi=yhi, xlo=xlo, xhi=xhi, zc=zc, ntx=ntx,
@@ -238,7 +270,9 @@ class HipStencilKernel:
             for h in halos.get(f.name, (None, None)):
                 if h is not None and (h.data_ptr() % 16 != 0):
                     aligned = False
-        cfg = self._march_cfg(ve if aligned else 1)
+        cfg = self._march_cfg(ve if aligned else 1, shape)
+        if halos and ir.ndim == 2 and cfg.VIEW2D == 'yx':
+            cfg = MarchConfig(**{**cfg.__dict__, 'VIEW2D': 'zy'})
         variant = ('march', cfg)
         fn = self.function(variant, device)
         geo = self.march_launch_geometry(shape, cfg, z_range)

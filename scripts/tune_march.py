@@ -1,0 +1,110 @@
+"""Sweep march-schedule tile shapes on the 1024³ 7-point forward sweep (interleaved rounds, one process).
+
+python scripts/tune_march.py [--n 1024] [--rounds 5] [--configs "CX=2,WX=1,NR=2,ZC=512;..."]
+Prints one line per config: median / min forward time and algorithmic GB/s. Kernel names carry the
+config index (tune<i>_...) so a `rocprofv3 --pmc` run of this script attributes counters per config.
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+DEFAULT = ';'.join([
+    'CX=2,WX=1,NR=2,ZC=512', 'CX=2,WX=1,NR=2,ZC=64', 'CX=2,WX=1,NR=2,ZC=32', 'CX=2,WX=1,NR=2,ZC=16',
+    'CX=2,WX=1,NR=4,ZC=512', 'CX=2,WX=1,NR=4,ZC=64', 'CX=2,WX=1,NR=4,ZC=32',
+    'CX=4,WX=1,NR=2,ZC=512', 'CX=4,WX=1,NR=2,ZC=64', 'CX=4,WX=1,NR=4,ZC=64',
+    'CX=1,WX=1,NR=4,ZC=64', 'CX=1,WX=1,NR=8,ZC=64', 'CX=2,WX=2,NR=4,ZC=64', 'CX=4,WX=1,NR=4,ZC=32',
+    'CX=2,WX=1,NR=2,ZC=512,NT_STORE=1', 'CX=2,WX=1,NR=4,ZC=64,NT_STORE=1', 'CX=4,WX=1,NR=4,ZC=64,NT_STORE=1',
+    'CX=2,WX=1,NR=8,ZC=64', 'CX=4,WX=1,NR=8,ZC=64',
+])
+
+
+def parse_cfg(s):
+    d = {}
+    for kv in s.split(','):
+        k, v = kv.split('=')
+        k = k.strip()
+        d[k] = {'0': 'zy', '1': 'yx'}.get(v.strip(), v.strip()) if k == 'VIEW2D' else int(v)
+    return d
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument('--n', type=int, default=1024)
+    p.add_argument('--rounds', type=int, default=5)
+    p.add_argument('--reps', type=int, default=4)
+    p.add_argument('--configs', default=DEFAULT)
+    p.add_argument('--workload', default='diffusion7')
+    p.add_argument('--configs-file')
+    a = p.parse_args()
+    import torch
+
+    from pystencils_autodiff_amd import AutoDiffOp
+    from pystencils_autodiff_amd import workloads as W
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+
+    n = a.n
+    builder = {'diffusion7': (W.diffusion_7pt, torch.float32), 'stencil27': (W.stencil_27pt, torch.float16),
+               'laplace5': (W.laplace_5pt, torch.float32)}[a.workload]
+    op = AutoDiffOp(builder[0](), boundary_handling='zeros')
+    shape = (n, n) if a.workload == 'laplace5' else (n, n, n)
+    cells = 1
+    for s in shape:
+        cells *= s
+    esize = 2 if builder[1] == torch.float16 else 4
+    u = torch.rand(shape, device='cuda').to(builder[1])
+    out = torch.empty_like(u)
+    spec = open(a.configs_file).read().strip() if a.configs_file else a.configs
+    cfgs = [parse_cfg(s) for s in spec.split(';') if s.strip()]
+    kernels = []
+    for i, c in enumerate(cfgs):
+        k = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name=f'tune{i}',
+                          target='gpu', gpu_indexing_params=c)
+        ck = k.compile()
+        ck(u=u, out=out)
+        kernels.append(ck)
+    ref = torch.empty_like(out)
+    op_ref = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='tuneref', target='gpu')
+    op_ref.compile()(u=u, out=ref, force_schedule='generic')
+    torch.cuda.synchronize()
+    maxdiff = [0.0] * len(cfgs)
+    times = [[] for _ in cfgs]
+    for r in range(a.rounds):
+        for i, ck in enumerate(kernels):
+            out.zero_()
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.reps):
+                ck(u=u, out=out)
+            e1.record()
+            torch.cuda.synchronize()
+            times[i].append(e0.elapsed_time(e1) / a.reps)
+            if r == 0:
+                maxdiff[i] = (out.float() - ref.float()).abs().max().item()
+    # achievable copy bandwidth in the same process (read+write of the same bytes)
+    ct = []
+    for _ in range(a.rounds):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out.copy_(u)
+        e1.record()
+        torch.cuda.synchronize()
+        ct.append(e0.elapsed_time(e1))
+    alg = 2 * esize * cells
+    print(f"copy_: median {sorted(ct)[len(ct) // 2]:.4f} ms = {alg / (sorted(ct)[len(ct) // 2] * 1e-3) / 1e9:.0f} GB/s")
+    for i, c in enumerate(cfgs):
+        ts = sorted(times[i])
+        med = ts[len(ts) // 2]
+        geo = kernels[i].march_launch_geometry(shape if len(shape) == 3 else shape, kernels[i].last_variant[1])
+        print(f"tune{i:<3d} {','.join(f'{k}={v}' for k, v in c.items()):34s} median {med:.4f} ms  min {ts[0]:.4f} ms  "
+              f"{alg / (med * 1e-3) / 1e9:7.0f} GB/s  grid {geo['grid']} zc {geo['zc']}  maxdiff_vs_generic {maxdiff[i]:.2e}")
+    sys.stdout.flush()
+
+
+if __name__ == '__main__':
+    main()

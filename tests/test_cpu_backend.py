@@ -1,0 +1,139 @@
+"""``create_tensorflow_op(backend='torch_native', use_cuda=False)`` — the reference's CPU path.
+
+Mirrors tests/test_tfmad.py:186-285 (with_cuda=False) and
+tests/backends/test_torch_native_compilation.py:47-80,153-211 of the reference.
+"""
+import numpy as np
+import pytest
+import sympy as sp
+
+import pystencils_autodiff_amd as pa
+from oracle import evaluate as OE
+from pystencils_autodiff_amd import ps
+from pystencils_autodiff_amd import workloads as W
+from tests.conftest import assert_close_rel, golden
+
+torch = pytest.importorskip('torch')
+
+
+@pytest.mark.parametrize('with_offsets', (False, True))
+def test_tfmad_gradient_check_torch_native_cpu(with_offsets):
+    a, b, out = ps.fields("a, b, out: float64[5,7]")
+    if with_offsets:
+        cont = 2 * ps.fd.Diff(a, 0) - 1.5 * ps.fd.Diff(a, 1) - ps.fd.Diff(b, 0) + 3 * ps.fd.Diff(b, 1)
+        asg = ps.Assignment(out.center(), ps.fd.Discretization2ndOrder(dx=1)(cont) + 1.2 * a.center())
+    else:
+        asg = ps.Assignment(out.center(), 1.2 * a.center + 0.1 * b.center)
+    op = pa.AutoDiffOp(ps.AssignmentCollection([asg], []), boundary_handling='zeros', diff_mode='transposed-forward')
+    fn = op.create_tensorflow_op(use_cuda=False, backend='torch_native')
+    d = {a: torch.zeros(*a.shape, dtype=torch.float64, requires_grad=True),
+         b: torch.zeros(*b.shape, dtype=torch.float64, requires_grad=True)}
+    assert torch.autograd.gradcheck(fn.apply, tuple(d[f] for f in op.forward_input_fields), atol=1e-4)
+
+
+def test_tfmad_gradient_check_two_outputs_cpu():
+    a, b, o1, o2, o3 = ps.fields("a, b, out1, out2, out3: float64[21,13]")
+    ac = ps.AssignmentCollection({o1.center: a.center + b.center, o2.center: a.center - b.center,
+                                  o3.center: sp.exp(b[-1, 0])})
+    op = pa.AutoDiffOp(ac, boundary_handling='zeros', diff_mode='transposed-forward')
+    fn = op.create_tensorflow_op(use_cuda=False, backend='torch_native')
+    at = torch.zeros(*a.shape, dtype=torch.float64, requires_grad=True)
+    bt = torch.zeros(*b.shape, dtype=torch.float64, requires_grad=True)
+    assert torch.autograd.gradcheck(fn.apply, (at, bt), atol=1e-4)
+
+
+def test_op_attributes_and_call():
+    z, y, x = ps.fields("z, y, x: float64[20,40]")
+    a = sp.Symbol('a')
+    op = pa.AutoDiffOp(ps.AssignmentCollection({z[0, 0]: x[0, 0] * sp.log(a * x[0, 0] * y[0, 0])}))
+    fn = op.create_tensorflow_op(use_cuda=False, backend='torch_native')
+    for attr in ('class_kwargs', 'kernel', 'ast', 'parameters', 'forward_parameters', 'forward_ast',
+                 'backward_ast', 'num_regs', 'code'):
+        assert hasattr(fn, attr), attr
+    assert [p.symbol.name for p in fn.forward_parameters] == ['x', 'y']
+    fn.class_kwargs['a'] = 5.0
+    rng = np.random.default_rng(0)
+    xv = torch.from_numpy(rng.uniform(0.5, 1.5, (20, 40))).requires_grad_(True)
+    yv = torch.from_numpy(rng.uniform(0.5, 1.5, (20, 40))).requires_grad_(True)
+    zt = fn.call(x=xv, y=yv)
+    assert isinstance(zt, torch.Tensor)
+    ref = xv.detach().numpy() * np.log(5.0 * xv.detach().numpy() * yv.detach().numpy())
+    assert np.allclose(zt.detach().numpy(), ref, atol=1e-12)
+    tup = fn.apply(xv, yv)
+    assert isinstance(tup, tuple) and len(tup) == 1
+    tup[0].sum().backward()
+    assert np.allclose(xv.grad.numpy(), np.log(5.0 * xv.detach().numpy() * yv.detach().numpy()) + 1)
+
+
+def test_execute_kernel_directly_like_reference():
+    # reference tests/backends/test_torch_native_compilation.py:153-211
+    z, y, x = ps.fields("z, y, x: [20,40]")
+    a = sp.Symbol('a')
+    fa = ps.AssignmentCollection({z[0, 0]: x[0, 0] * sp.log(a * x[0, 0] * y[0, 0])})
+    op = pa.AutoDiffOp(fa)
+    k = op.forward_ast_cpu
+    rng = np.random.default_rng(1)
+    xv, yv = rng.random((20, 40)), rng.random((20, 40))
+    zv = np.zeros((20, 40))
+    k(x=xv, y=yv, z=zv, a=5.)
+    assert np.allclose(zv[1:-1, 1:-1], (xv * np.log(5 * xv * yv))[1:-1, 1:-1], atol=1e-6)
+    assert 'call_' + k.function_name in [w.function_name for w in
+                                          op.create_tensorflow_op(use_cuda=False, backend='torch_native').ast.kernel_wrappers]
+
+
+@pytest.mark.parametrize('case,builder,bh', [
+    ('diffusion7_f32_32cube', W.diffusion_7pt, 'zeros'),
+    ('asym7_f32_16cube', W.asym_7pt, 'zeros'),
+    ('laplace5_f32_64x64_none', W.laplace_5pt, None),
+    ('stencil27_f16_16cube', W.stencil_27pt, 'zeros'),
+])
+def test_cpu_op_vs_golden(case, builder, bh):
+    g = golden(case)
+    op = pa.AutoDiffOp(builder(), boundary_handling=bh)
+    fn = op.create_tensorflow_op(use_cuda=False, backend='torch_native')
+    u = torch.from_numpy(g['u']).requires_grad_(True)
+    (out,) = fn.apply(u)
+    out.backward(torch.from_numpy(g['diffout']))
+    tol = 1e-3 if g['u'].dtype == np.float16 else 1e-6
+    assert_close_rel(out.detach().numpy(), g['out'], tol, 'out')
+    assert_close_rel(u.grad.numpy(), g['diffu'], tol, 'diffu')
+
+
+def test_time_constant_accumulation_cpu():
+    u, out = ps.fields("u, out: float64[6,7]")
+    ac = ps.AssignmentCollection({out.center: 2 * u[1, 0] + u.center ** 2})
+    op = pa.AutoDiffOp(ac, boundary_handling='zeros', time_constant_fields=[u])
+    fn = op.create_tensorflow_op(use_cuda=False, backend='torch_native')
+    rng = np.random.default_rng(0)
+    uv = torch.from_numpy(rng.uniform(-1, 1, (6, 7))).requires_grad_(True)
+    assert torch.autograd.gradcheck(fn.apply, (uv,), atol=1e-8)
+    ref = OE.evaluate(op.backward_assignments, {'u': uv.detach().numpy(), 'diffout': np.ones((6, 7))},
+                      boundary_handling='zeros')['diffu']
+    (o,) = fn.apply(uv)
+    g, = torch.autograd.grad(o, uv, torch.ones(6, 7, dtype=torch.float64))
+    assert_close_rel(g.numpy(), ref, 1e-12)
+
+
+def test_openmp_kernel_matches_serial():
+    op = pa.AutoDiffOp(W.asym_7pt(), boundary_handling='zeros', cpu_openmp=True)
+    op2 = pa.AutoDiffOp(W.asym_7pt(), boundary_handling='zeros')
+    rng = np.random.default_rng(0)
+    u = rng.uniform(0, 1, (12, 13, 14)).astype(np.float32)
+    o1, o2 = np.zeros_like(u), np.zeros_like(u)
+    op.forward_ast_cpu(u=u, out=o1)
+    op2.forward_ast_cpu(u=u, out=o2)
+    assert '#pragma omp' in op.forward_ast_cpu.compile().code
+    assert np.array_equal(o1, o2)
+
+
+def test_strided_inputs_generic_cpu():
+    op = pa.AutoDiffOp(W.laplace_5pt(), boundary_handling='zeros')
+    rng = np.random.default_rng(0)
+    big = rng.uniform(0, 1, (20, 30))
+    u = big[::2, 1::3]                                  # non-contiguous view
+    out = np.zeros(u.shape)
+    op64 = pa.AutoDiffOp(W.laplace_5pt(dtype='float64'), boundary_handling='zeros')
+    op64.forward_ast_cpu(u=u, out=out)
+    ref = OE.evaluate(op64.forward_assignments, {'u': np.ascontiguousarray(u)}, boundary_handling='zeros')['out']
+    assert_close_rel(out, ref, 1e-14)
+    del op

@@ -247,3 +247,49 @@ def test_vector_field_generic_schedule():
     ref = OE.evaluate(op.forward_assignments, {'f': fa}, boundary_handling='zeros')['out']
     assert k.last_variant[0] == 'generic'
     assert_close_rel(o.cpu().numpy(), ref, 1e-12)
+
+
+@pytest.mark.parametrize('params', [
+    dict(CX=4, NR=8, PD=2, NT_STORE=True), dict(CX=1, NR=1), dict(CX=2, WX=2, NR=3, PD=2),
+    dict(CX=2, NR=4, FULL_RING=True), dict(CX=4, NR=8, ZC=5), dict(CX=1, WX=4, NR=2, PD=2, ZC=3),
+])
+@pytest.mark.parametrize('builder', [W.diffusion_7pt, W.asym_7pt, W.stencil_27pt])
+def test_march_tunings_vs_oracle(params, builder):
+    """Every tile shape / pipeline depth / ring kind gives the oracle's result (ragged tiles, short chunks)."""
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
+    is16 = builder is W.stencil_27pt
+    dt = np.float16 if is16 else np.float32
+    shape = (13, 37, 70) if not is16 else (11, 21, 72)
+    rng = np.random.default_rng(5)
+    u = rng.uniform(0, 1, shape).astype(dt)
+    d = rng.uniform(-1, 1, shape).astype(dt)
+    for which, ac, ins, outname in (('f', op.forward_assignments, {'u': u}, 'out'),
+                                    ('b', op.backward_assignments, {'diffout': d}, 'diffu')):
+        k = StencilKernel(ac, boundary_handling='zeros', function_name=f'tn_{which}', target='gpu',
+                          gpu_indexing_params=params).compile()
+        ref = OE.evaluate(ac, ins, boundary_handling='zeros')[outname]
+        out = torch.zeros(shape, dtype=torch.float16 if is16 else torch.float32, device='cuda')
+        k(**{n: torch.from_numpy(v).cuda() for n, v in ins.items()}, **{outname: out})
+        torch.cuda.synchronize()
+        assert k.last_variant[0] == 'march'
+        assert_close_rel(out.cpu().numpy(), ref, 1e-3 if is16 else 1e-6, f'{params} {which}')
+
+
+@pytest.mark.parametrize('params', [dict(VIEW2D='yx'), dict(VIEW2D='zy'), dict(VIEW2D='yx', CX=1, NR=3),
+                                    dict(VIEW2D='zy', CX=2, WX=4, NR=1, PD=2, ZC=7)])
+@pytest.mark.parametrize('bh', ['zeros', None])
+def test_march_2d_views_vs_oracle(params, bh):
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    u, out = ps.fields("u, out: float32[2d]")
+    ac = ps.AssignmentCollection({out.center: 0.3 * u[1, 0] - 0.7 * u[-1, 0] + 0.2 * u[0, 1] + 0.9 * u[0, -1]
+                                  - 1.1 * u[1, 1] + u.center})
+    rng = np.random.default_rng(2)
+    uv = rng.uniform(-1, 1, (45, 300)).astype(np.float32)
+    ref = OE.evaluate(ac, {'u': uv}, boundary_handling=bh)['out']
+    k = StencilKernel(ac, boundary_handling=bh, function_name='v2d', target='gpu', gpu_indexing_params=params).compile()
+    o = torch.zeros(uv.shape, device='cuda')
+    k(u=torch.from_numpy(uv).cuda(), out=o)
+    torch.cuda.synchronize()
+    assert k.last_variant[0] == 'march' and k.last_variant[1].VIEW2D == params['VIEW2D']
+    assert_close_rel(o.cpu().numpy(), ref, 1e-6)
