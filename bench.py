@@ -88,10 +88,15 @@ def main():
     distributed = world > 1
     if args.gpus != world and distributed:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    local_rank = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     if distributed:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+        backend = os.environ.get('PSAD_DIST_BACKEND', 'nccl')   # nccl = RCCL; gloo only to rehearse on 1 GPU
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+        else:
+            dist.init_process_group(backend)
 
     import pystencils_autodiff_amd as pa
     from pystencils_autodiff_amd import workloads as W

@@ -60,6 +60,16 @@ def exchange_halos(t, rz, group=None, bufs=None):
                                                                                  device=t.device)
         ops.append(dist.P2POp(dist.isend, t[-rz:].contiguous(), peer(rank + 1), group))
         ops.append(dist.P2POp(dist.irecv, hi, peer(rank + 1), group))
+    if ops and t.is_cuda and dist.get_backend(group) == 'gloo':
+        # gloo moves host memory only: stage through the CPU (tests / debugging, not the RCCL path)
+        staged = [dist.P2POp(op.op, op.tensor.cpu() if op.op is dist.isend else torch.empty_like(op.tensor, device='cpu'),
+                             op.peer, op.group) for op in ops]
+        for w in dist.batch_isend_irecv(staged):
+            w.wait()
+        for op, st in zip(ops, staged):
+            if op.op is dist.irecv:
+                op.tensor.copy_(st.tensor)
+        return [], lo, hi
     works = dist.batch_isend_irecv(ops) if ops else []
     return works, lo, hi
 
@@ -110,9 +120,10 @@ class ZSlabOp:
             halos[f.name] = (lo, hi)
         ref = kwargs[ir.fields_written[0].name]
         zl = ref.shape[0]
+        split = rz > 0 and dist.is_initialized() and dist.get_world_size(self.group) > 1
         if self.use_cuda:
             compiled = k.compile()
-            if pending:
+            if split:
                 if zl > 2 * rz:
                     compiled(z_range=(rz, zl - rz), **kwargs)          # interior overlaps the exchange
                 for w in pending:

@@ -1,0 +1,96 @@
+"""Z-slab decomposition with halo exchange (world_size 2 and 3, gloo).
+
+CPU: the C kernels on ghosted copies. GPU (marked): two gloo ranks share cuda:0 and run the
+HIP march kernel with halo planes read in place and the interior/boundary z-range split —
+the same code path the RCCL bench runs on 8 GPUs.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), '..'))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, shape, builder_name, use_cuda, result_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import pystencils_autodiff_amd as pa
+    from pystencils_autodiff_amd import workloads as W
+    from pystencils_autodiff_amd.zslab import ZSlabOp, slab_bounds
+    dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank, world_size=world)
+    try:
+        builder = getattr(W, builder_name)
+        op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
+        rng = np.random.default_rng(0)
+        u = rng.uniform(0, 1, shape).astype(np.float32)
+        d = rng.uniform(-1, 1, shape).astype(np.float32)
+        lo, hi = slab_bounds(shape[0], world, rank)
+        dev = 'cuda' if use_cuda else 'cpu'
+        ul = torch.from_numpy(u[lo:hi].copy()).to(dev)
+        dl = torch.from_numpy(d[lo:hi].copy()).to(dev)
+        out = torch.zeros_like(ul)
+        du = torch.zeros_like(ul)
+        z = ZSlabOp(op, use_cuda=use_cuda)
+        z.fwd(u=ul, out=out)
+        z.bwd(diffout=dl, diffu=du)
+        if use_cuda:
+            torch.cuda.synchronize()
+        np.save(os.path.join(result_dir, f'out_{rank}.npy'), out.cpu().numpy())
+        np.save(os.path.join(result_dir, f'du_{rank}.npy'), du.cpu().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, shape, builder_name, use_cuda, tmp_path):
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, shape, builder_name, use_cuda, str(tmp_path)), nprocs=world, join=True)
+    out = np.concatenate([np.load(tmp_path / f'out_{r}.npy') for r in range(world)])
+    du = np.concatenate([np.load(tmp_path / f'du_{r}.npy') for r in range(world)])
+    from oracle import stencils as S
+    taps = {'diffusion_7pt': S.taps_diffusion_7pt(), 'asym_7pt': S.taps_asym_7pt(),
+            'stencil_27pt': S.taps_27pt()}[builder_name]
+    rng = np.random.default_rng(0)
+    u = rng.uniform(0, 1, shape).astype(np.float32)
+    d = rng.uniform(-1, 1, shape).astype(np.float32)
+    return out, du, S.linear_stencil(u, taps), S.linear_stencil(d, S.flip(taps))
+
+
+@pytest.mark.parametrize('world,shape', [(2, (10, 9, 12)), (3, (13, 6, 7))])
+@pytest.mark.parametrize('builder_name', ['asym_7pt', 'diffusion_7pt'])
+def test_zslab_gloo_cpu(world, shape, builder_name, tmp_path):
+    from tests.conftest import assert_close_rel
+    out, du, ref_out, ref_du = _run(world, shape, builder_name, False, tmp_path)
+    assert_close_rel(out, ref_out, 1e-6, 'out')
+    assert_close_rel(du, ref_du, 1e-6, 'diffu')
+
+
+def test_slab_bounds_cover_domain():
+    from pystencils_autodiff_amd.zslab import slab_bounds
+    for n in (1, 7, 1024, 1025):
+        for world in (1, 2, 3, 8):
+            b = [slab_bounds(n, world, r) for r in range(world)]
+            assert b[0][0] == 0 and b[-1][1] == n
+            assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+            assert max(h - lo for lo, h in b) - min(h - lo for lo, h in b) <= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('world,shape', [(2, (24, 40, 64)), (3, (19, 33, 70))])
+@pytest.mark.parametrize('builder_name', ['asym_7pt', 'diffusion_7pt'])
+def test_zslab_gloo_gpu_halo_path(world, shape, builder_name, tmp_path):
+    from tests.conftest import assert_close_rel
+    out, du, ref_out, ref_du = _run(world, shape, builder_name, True, tmp_path)
+    assert_close_rel(out, ref_out, 1e-6, 'out')
+    assert_close_rel(du, ref_du, 1e-6, 'diffu')
