@@ -75,6 +75,9 @@ class HipStencilKernel:
         self.ir = kernel.ir
         self.name = kernel.function_name
         self._variants = {}            # variant key -> (source, kernel name)
+        self._plans = {}               # launch key -> _Plan
+        self._specs = None
+        self._ref_index = [f.name for f in kernel.ir.fields].index(kernel.ir.fields_written[0].name)
         self.last_variant = None
 
     # -- sources --------------------------------------------------------------------------------
@@ -135,96 +138,116 @@ class HipStencilKernel:
         return rt.compile_hip(src)
 
     # -- launch ---------------------------------------------------------------------------------
+    def _field_specs(self):
+        if self._specs is None:
+            torch = _torch()
+            self._specs = [(f.name, getattr(torch, f.dtype.numpy_dtype.name), f.spatial_dimensions + f.index_dimensions,
+                            tuple(int(x) for x in f.shape) if f.has_fixed_shape else None) for f in self.ir.fields]
+        return self._specs
+
     def __call__(self, halos=None, stream=None, force_schedule=None, z_range=None, **kwargs):
         """Launch on the field tensors / scalars given by name.
 
         ``halos`` = ``{field: (lo_planes, hi_planes)}``: tensors holding the RZ planes just
         below plane 0 / above plane Z-1 of a stencil field (``None`` = zeros); ``z_range``
         restricts the written planes of axis 0 (both: z-slab decomposition, ``zslab.py``).
+        The first call for a given (shape, alignment, halo layout, z range) builds a launch plan
+        (variant, function handle, grid, argument layout); later calls only re-pack pointers.
         """
         torch = _torch()
         ir = self.ir
-        tensors = {}
-        for f in ir.fields:
-            if f.name not in kwargs:
-                raise TypeError(f"{self.name}: missing field argument '{f.name}'")
-            t = kwargs[f.name]
+        tensors = []
+        for name, dtype, ndim, fixed in self._field_specs():
+            t = kwargs.get(name)
+            if t is None:
+                raise TypeError(f"{self.name}: missing field argument '{name}'")
             if not isinstance(t, torch.Tensor) or not t.is_cuda:
-                raise TypeError(f"{self.name}: field '{f.name}' must be a torch tensor on the GPU")
-            if t.dtype != getattr(torch, f.dtype.numpy_dtype.name):
-                raise TypeError(f"{self.name}: field '{f.name}' has dtype {t.dtype}, kernel expects "
-                                f"{f.dtype.numpy_dtype.name}")
-            tensors[f.name] = t
+                raise TypeError(f"{self.name}: field '{name}' must be a torch tensor on the GPU")
+            if t.dtype != dtype:
+                raise TypeError(f"{self.name}: field '{name}' has dtype {t.dtype}, kernel expects {dtype}")
+            if t.dim() != ndim:
+                raise ValueError(f"{self.name}: field '{name}' expects {ndim} dims, got {t.dim()}")
+            if fixed is not None and tuple(t.shape) != fixed:
+                raise ValueError(f"{self.name}: field '{name}' was declared with shape {fixed}, got {tuple(t.shape)}")
+            tensors.append(t)
         scalars = []
-        for s in ir.scalars:
-            if s.name not in kwargs:
-                raise TypeError(f"{self.name}: missing scalar argument '{s.name}'")
-            scalars.append(float(kwargs[s.name]))
-        ref = tensors[ir.fields_written[0].name]
+        for s_ in ir.scalars:
+            if s_.name not in kwargs:
+                raise TypeError(f"{self.name}: missing scalar argument '{s_.name}'")
+            scalars.append(float(kwargs[s_.name]))
+        ref = tensors[self._ref_index]
         shape = tuple(ref.shape[:ir.ndim])
-        for f in ir.fields:
-            t = tensors[f.name]
+        for t, (name, _, _, _) in zip(tensors, self._specs):
             if tuple(t.shape[:ir.ndim]) != shape:
-                raise ValueError(f"{self.name}: field '{f.name}' has spatial shape {tuple(t.shape[:ir.ndim])}, "
+                raise ValueError(f"{self.name}: field '{name}' has spatial shape {tuple(t.shape[:ir.ndim])}, "
                                  f"expected {shape}")
-            if f.has_fixed_shape and tuple(t.shape) != tuple(int(s) for s in f.shape):
-                raise ValueError(f"{self.name}: field '{f.name}' was declared with shape {f.shape}, got "
-                                 f"{tuple(t.shape)}")
-            if t.dim() != f.spatial_dimensions + f.index_dimensions:
-                raise ValueError(f"{self.name}: field '{f.name}' expects {f.spatial_dimensions + f.index_dimensions} "
-                                 f"dims, got {t.dim()}")
-        device = ref.device.index if ref.device.index is not None else torch.cuda.current_device()
-        if stream is None:
-            stream = torch.cuda.current_stream(ref.device).cuda_stream
         if any(n == 0 for n in shape):
             return
-        contiguous = all(t.is_contiguous() for t in tensors.values())
+        device = ref.device.index
+        if stream is None:
+            stream = torch.cuda.current_stream(ref.device).cuda_stream
+        halo_list = []
+        if halos:
+            for f in ir.stencil_fields:
+                lo, hi = halos.get(f.name, (None, None))
+                halo_list += [lo, hi]
+        ptrs = [t.data_ptr() for t in tensors]
+        hptrs = [h.data_ptr() if h is not None else 0 for h in halo_list]
+        contiguous = all(t.is_contiguous() for t in tensors)
+        strides = None if contiguous else tuple(tuple(t.stride()) for t in tensors)
+        align = tuple(p % 32 == 0 for p in ptrs + hptrs)
+        key = (force_schedule, shape, strides, align, tuple(h is not None for h in halo_list),
+               tuple(z_range) if z_range is not None else None, device)
+        plan = self._plans.get(key)
+        if plan is None:
+            plan = self._make_plan(tensors, halo_list, shape, device, contiguous, force_schedule, z_range)
+            self._plans[key] = plan
+        self.last_variant = plan.variant
+        if plan.grid == 0:
+            return
+        rt.launch(plan.fn, (plan.grid,), (256,), plan.pack(ptrs, hptrs, scalars), stream)
+
+    def _make_plan(self, tensors, halo_list, shape, device, contiguous, force_schedule, z_range):
+        torch = _torch()
+        ir = self.ir
         sched = force_schedule or self.schedule()
         if sched != 'generic' and not contiguous:
             sched = 'generic'
-        if (halos or z_range is not None) and sched != 'march':
+        if (halo_list or z_range is not None) and sched != 'march':
             raise ValueError('halo planes / z ranges are only supported by the march schedule')
         with torch.cuda.device(device):
             if sched == 'pointwise':
-                self._launch_pointwise(tensors, scalars, shape, device, stream)
-            elif sched == 'march':
-                self._launch_march(tensors, scalars, shape, device, stream, halos or {}, z_range)
-            else:
-                self._launch_generic(tensors, scalars, shape, device, stream)
+                return self._plan_pointwise(tensors, shape, device)
+            if sched == 'march':
+                return self._plan_march(tensors, halo_list, shape, device, z_range)
+            return self._plan_generic(tensors, shape, device)
 
-    def _scalar_args(self, scalars):
-        kind = 'f64' if self.ir.compute_dtype == np.float64 else 'f32'
-        return [(kind, v) for v in scalars]
+    def _scalar_kind(self):
+        return 'f64' if self.ir.compute_dtype == np.float64 else 'f32'
 
-    def _launch_pointwise(self, tensors, scalars, shape, device, stream):
-        ir = self.ir
-        variant = ('pointwise',)
-        fns = self.function(variant, device)
+    def _plan_pointwise(self, tensors, shape, device):
+        fns = self.function(('pointwise',), device)
         n = int(np.prod(shape))
-        aligned = all(t.data_ptr() % 32 == 0 for t in tensors.values())
-        args = [('ptr', tensors[f.name].data_ptr()) for f in ir.fields] + [('i64', n)] + self._scalar_args(scalars)
+        aligned = all(t.data_ptr() % 32 == 0 for t in tensors)
         per_block = 256 * (4 if aligned else 1)
         blocks = max(1, min(math.ceil(n / per_block), 256 * 16))
-        self.last_variant = ('pointwise', 'v4' if aligned else 'v1')
-        rt.launch(fns['v4' if aligned else 'v1'], (blocks,), (256,), rt.pack_args(args), stream)
+        kinds = ['ptr'] * len(tensors) + ['i64'] + [self._scalar_kind()] * len(self.ir.scalars)
+        return _Plan(('pointwise', 'v4' if aligned else 'v1'), fns['v4' if aligned else 'v1'], blocks, kinds,
+                     len(tensors), 0, [n])
 
-    def _launch_generic(self, tensors, scalars, shape, device, stream):
+    def _plan_generic(self, tensors, shape, device):
         ir = self.ir
         fn = self.function(('generic',), device)
         bounds = ir.iteration_bounds(shape)
         ncell = int(np.prod([hi - lo for lo, hi in bounds]))
-        if ncell <= 0:
-            return
-        args = [('ptr', tensors[f.name].data_ptr()) for f in ir.fields]
-        args += [('i64', int(n)) for n in shape]
-        for f in ir.fields:
-            args += [('i64', int(s)) for s in tensors[f.name].stride()]
+        statics = [int(n) for n in shape]
+        for t in tensors:
+            statics += [int(s_) for s_ in t.stride()]
         for lo, hi in bounds:
-            args += [('i64', lo), ('i64', hi)]
-        args += self._scalar_args(scalars)
-        blocks = max(1, min(math.ceil(ncell / 256), 256 * 32))
-        self.last_variant = ('generic',)
-        rt.launch(fn, (blocks,), (256,), rt.pack_args(args), stream)
+            statics += [lo, hi]
+        kinds = ['ptr'] * len(tensors) + ['i64'] * len(statics) + [self._scalar_kind()] * len(ir.scalars)
+        blocks = max(1, min(math.ceil(ncell / 256), 256 * 32)) if ncell > 0 else 0
+        return _Plan(('generic',), fn, blocks, kinds, len(tensors), 0, statics)
 
     def march_launch_geometry(self, shape, cfg, z_range=None):
         """(Z, Y, X), bounds and grid of the march schedule for a field shape."""
@@ -259,40 +282,61 @@ class HipStencilKernel:
         return dict(Z=Z, Y=Y, X=X, zlo=zlo, zhi=zhi, ylo=ylo, yhi=yhi, xlo=xlo, xhi=xhi, zc=zc, ntx=ntx,
                     nty=nty, grid=nt * nchunks)
 
-    def _launch_march(self, tensors, scalars, shape, device, stream, halos, z_range=None):
+    def _plan_march(self, tensors, halo_list, shape, device, z_range):
         torch = _torch()
         ir = self.ir
         ve = self._vec_elems()
         X = shape[-1]
         stencil = ir.stencil_fields
-        aligned = X % ve == 0 and all(tensors[f.name].data_ptr() % 16 == 0 for f in stencil)
-        for f in stencil:
-            for h in halos.get(f.name, (None, None)):
-                if h is not None and (h.data_ptr() % 16 != 0):
-                    aligned = False
+        by_name = {f.name: t for f, t in zip(ir.fields, tensors)}
+        aligned = X % ve == 0 and all(by_name[f.name].data_ptr() % 16 == 0 for f in stencil) and \
+            all(h.data_ptr() % 16 == 0 for h in halo_list if h is not None)
         cfg = self._march_cfg(ve if aligned else 1, shape)
-        if halos and ir.ndim == 2 and cfg.VIEW2D == 'yx':
+        if halo_list and ir.ndim == 2 and cfg.VIEW2D == 'yx':
             cfg = MarchConfig(**{**cfg.__dict__, 'VIEW2D': 'zy'})
         variant = ('march', cfg)
         fn = self.function(variant, device)
         geo = self.march_launch_geometry(shape, cfg, z_range)
-        if geo['grid'] == 0 or geo['yhi'] <= geo['ylo'] or geo['xhi'] <= geo['xlo']:
-            return
+        grid = geo['grid'] if geo['yhi'] > geo['ylo'] and geo['xhi'] > geo['xlo'] else 0
         rz = march_geometry(ir, cfg)['RZ']
         plane = geo['Y'] * geo['X']
-        args = [('ptr', tensors[f.name].data_ptr()) for f in ir.fields]
-        for f in stencil:
-            lo, hi = halos.get(f.name, (None, None))
-            for h in (lo, hi):
-                if h is not None:
-                    if not isinstance(h, torch.Tensor) or not h.is_contiguous() or h.numel() < rz * plane or \
-                            h.dtype != tensors[f.name].dtype:
-                        raise ValueError(f"halo for '{f.name}' must be a contiguous tensor of >= {rz} planes")
-            args += [('ptr', lo.data_ptr() if lo is not None else 0), ('ptr', hi.data_ptr() if hi is not None else 0)]
-        for k in ('Z', 'Y', 'X', 'zlo', 'zhi', 'ylo', 'yhi', 'xlo', 'xhi', 'zc', 'ntx', 'nty'):
-            args.append(('i32', int(geo[k])))
-        args += self._scalar_args(scalars)
-        if max(geo['Z'], geo['Y'], geo['X']) >= 2 ** 31 or geo['grid'] >= 2 ** 31:
+        for i, f in enumerate(stencil):
+            for h in (halo_list[2 * i:2 * i + 2] if halo_list else ()):
+                if h is not None and (not isinstance(h, torch.Tensor) or not h.is_contiguous() or
+                                      h.numel() < rz * plane or h.dtype != by_name[f.name].dtype or
+                                      h.device != by_name[f.name].device):
+                    raise ValueError(f"halo for '{f.name}' must be a contiguous tensor of >= {rz} planes "
+                                     "on the field's device")
+        if max(geo['Z'], geo['Y'], geo['X']) >= 2 ** 31 or grid >= 2 ** 31:
             raise ValueError('field extent too large for the march schedule')
-        self.last_variant = ('march', cfg)
-        rt.launch(fn, (geo['grid'],), (256,), rt.pack_args(args), stream)
+        statics = [int(geo[k]) for k in ('Z', 'Y', 'X', 'zlo', 'zhi', 'ylo', 'yhi', 'xlo', 'xhi', 'zc', 'ntx', 'nty')]
+        kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics) + \
+            [self._scalar_kind()] * len(ir.scalars)
+        return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics)
+
+
+class _Plan:
+    """A resolved launch: variant, function handle, grid and a struct that packs the argument
+    buffer (pointers, then static extents, then scalars) at HIP_LAUNCH_PARAM_BUFFER alignment."""
+
+    _CODES = {'ptr': ('Q', 8), 'i32': ('i', 4), 'i64': ('q', 8), 'f32': ('f', 4), 'f64': ('d', 8)}
+
+    def __init__(self, variant, fn, grid, kinds, n_ptr, n_halo, statics):
+        import struct
+        self.variant = variant
+        self.fn = fn
+        self.grid = grid
+        fmt, off = '<', 0
+        for k in kinds:
+            c, size = self._CODES[k]
+            pad = (-off) % size
+            fmt += 'x' * pad + c
+            off += pad + size
+        fmt += 'x' * ((-off) % 8)
+        self.struct = struct.Struct(fmt)
+        self.n_ptr = n_ptr
+        self.n_halo = n_halo
+        self.statics = list(statics)
+
+    def pack(self, ptrs, hptrs, scalars):
+        return self.struct.pack(*ptrs, *(hptrs if hptrs else [0] * self.n_halo), *self.statics, *scalars)

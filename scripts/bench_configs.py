@@ -1,0 +1,91 @@
+"""Measure every BASELINE.json config on one GPU through the drop-in op (fwd + TF-MAD bwd per step).
+
+Prints one JSON line per config: Mcells/s, fwd/bwd ms (HIP events), algorithmic GB/s of each sweep and
+its fraction of the 8 TB/s HBM peak. Bytes per cell per sweep: (fields read + fields written) x size.
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+PEAK = 8000.0
+
+
+def run(name, builder, shape, dtype, bh, nin, steps=20, warmup=3, bytes_fwd=None, bytes_bwd=None):
+    import torch
+
+    import pystencils_autodiff_amd as pa
+    op = pa.AutoDiffOp(builder(), boundary_handling=bh)
+    fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    g = torch.Generator(device='cuda').manual_seed(0)
+    ins = [(torch.rand(shape, generator=g, device='cuda') + (0.5 if name.startswith('readme') else 0.0)).to(dtype)
+           .requires_grad_(True) for _ in range(nin)]
+    outs = fn.apply(*ins)
+    grads = [(torch.rand(o.shape, generator=g, device='cuda') * 2 - 1).to(dtype) for o in outs]
+    ev = []
+    for i in range(warmup + steps):
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record()
+        outs = fn.apply(*ins)
+        e1.record()
+        torch.autograd.backward(list(outs), grads)
+        e2.record()
+        for t in ins:
+            t.grad = None
+        if i >= warmup:
+            ev.append((e0, e1, e2))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        outs = fn.apply(*ins)
+        torch.autograd.backward(list(outs), grads)
+        for t in ins:
+            t.grad = None
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    cells = 1
+    for s in shape:
+        cells *= s
+    f_ms = sorted(a.elapsed_time(b) for a, b, _ in ev)[len(ev) // 2]
+    b_ms = sorted(b.elapsed_time(c) for _, b, c in ev)[len(ev) // 2]
+    res = {'config': name, 'shape': list(shape), 'dtype': str(dtype).replace('torch.', ''),
+           'mcells_per_s': round(cells * steps / el / 1e6, 1), 'ms_per_step': round(el / steps * 1e3, 4),
+           'fwd_ms': round(f_ms, 4), 'bwd_ms': round(b_ms, 4),
+           'fwd_schedule': op.forward_ast_gpu.compile().last_variant[0],
+           'bwd_schedule': op.backward_ast_gpu.compile().last_variant[0]}
+    if bytes_fwd:
+        res['fwd_GBps'] = round(bytes_fwd * cells / (f_ms * 1e-3) / 1e9, 1)
+        res['bwd_GBps'] = round(bytes_bwd * cells / (b_ms * 1e-3) / 1e9, 1)
+        res['fwd_frac'] = round(res['fwd_GBps'] / PEAK, 4)
+        res['bwd_frac'] = round(res['bwd_GBps'] / PEAK, 4)
+    print(json.dumps(res))
+    sys.stdout.flush()
+    del ins, outs, grads
+    torch.cuda.empty_cache()
+
+
+def main():
+    import torch
+
+    from pystencils_autodiff_amd import workloads as W
+    only = sys.argv[1:]
+    cfgs = [
+        ('readme_op_f32_20x30', W.readme_op, (20, 30), torch.float32, None, 2, 12, 20),
+        ('laplace5_f32_4096^2', lambda: W.laplace_5pt(), (4096, 4096), torch.float32, 'zeros', 1, 8, 8),
+        ('diffusion7_f32_512^3', lambda: W.diffusion_7pt(), (512, 512, 512), torch.float32, 'zeros', 1, 8, 8),
+        ('diffusion7_f32_1024^3', lambda: W.diffusion_7pt(), (1024, 1024, 1024), torch.float32, 'zeros', 1, 8, 8),
+        ('stencil27_f16_768^3', lambda: W.stencil_27pt(), (768, 768, 768), torch.float16, 'zeros', 1, 4, 4),
+        ('diffusion7_f64_512^3', lambda: W.diffusion_7pt(dtype='float64'), (512, 512, 512), torch.float64,
+         'zeros', 1, 16, 16),
+    ]
+    for name, b, shape, dt, bh, nin, bf, bb in cfgs:
+        if only and name not in only:
+            continue
+        run(name, b, shape, dt, bh, nin, bytes_fwd=bf, bytes_bwd=bb)
+
+
+if __name__ == '__main__':
+    main()
