@@ -27,7 +27,7 @@ def parse():
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=3)
-    p.add_argument('--n', type=int, default=1024, help='cube edge (default: the 1024³ north-star config)')
+    p.add_argument('--edge', type=int, default=1024, help='cube edge (default: the 1024³ north-star config)')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-seconds', type=float, default=12.0, help='budget of the CPU baseline sample')
     p.add_argument('--kernel-only', action='store_true', help='also time the raw kernel loop')
@@ -102,7 +102,7 @@ def main():
     from pystencils_autodiff_amd import workloads as W
     from pystencils_autodiff_amd.zslab import ZSlabOp, slab_bounds
 
-    n = args.n
+    n = args.edge
     lo, hi = slab_bounds(n, world, rank)
     zl = hi - lo
     op = pa.AutoDiffOp(W.diffusion_7pt(), boundary_handling='zeros')

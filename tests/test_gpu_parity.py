@@ -293,3 +293,57 @@ def test_march_2d_views_vs_oracle(params, bh):
     torch.cuda.synchronize()
     assert k.last_variant[0] == 'march' and k.last_variant[1].VIEW2D == params['VIEW2D']
     assert_close_rel(o.cpu().numpy(), ref, 1e-6)
+
+
+def _zsum_cases():
+    u, v, out = ps.fields("u, v, out: float32[3d]")
+    mixed = ps.AssignmentCollection({out.center: 0.3 * u[1, 1, -1] - 0.2 * u[-1, 0, 1] + 0.5 * u[0, 1, 0]
+                                     + sp.sin(u.center) * v.center + 0.1 * v.center})
+    return [('27pt', W.stencil_27pt), ('7pt', W.diffusion_7pt), ('asym', W.asym_7pt), ('mixed', lambda: mixed)]
+
+
+@pytest.mark.parametrize('params', [dict(ZSUM=True), dict(ZSUM=True, CX=1, NR=3, ZC=5),
+                                    dict(ZSUM=True, CX=4, NR=8, NT_STORE=True), dict(ZSUM=True, WX=2, CX=2, NR=2)])
+@pytest.mark.parametrize('case', _zsum_cases(), ids=lambda c: c[0])
+@pytest.mark.parametrize('bh', ['zeros', None])
+def test_zsum_schedule_vs_oracle(params, case, bh):
+    """z-partial-sum schedule: forward and adjoint of linear (and linear+centre-nonlinear) stencils."""
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    name, builder = case
+    op = pa.AutoDiffOp(builder(), boundary_handling=bh)
+    is16 = name == '27pt'
+    dt = np.float16 if is16 else np.float32
+    shape = (12, 35, 70)
+    rng = np.random.default_rng(7)
+    arrays = {f.name: rng.uniform(-1, 1, shape).astype(dt) for f in op.forward_input_fields}
+    arrays.update({f.name: rng.uniform(-1, 1, shape).astype(dt) for f in op.backward_input_fields
+                   if f.name not in arrays})
+    for which, ac in (('f', op.forward_assignments), ('b', op.backward_assignments)):
+        k = StencilKernel(ac, boundary_handling=bh, function_name=f'zs_{which}', target='gpu',
+                          gpu_indexing_params=params).compile()
+        ir = k.ir
+        ins = {f.name: arrays[f.name] for f in ir.fields_read}
+        ref = OE.evaluate(ac, ins, boundary_handling=bh)
+        outs = {f.name: torch.zeros(shape, dtype=torch.float16 if is16 else torch.float32, device='cuda')
+                for f in ir.fields_written}
+        k(**{n: torch.from_numpy(a).cuda() for n, a in ins.items()}, **outs)
+        torch.cuda.synchronize()
+        assert k.last_variant[0] == 'march' and k.last_variant[1].ZSUM
+        for n, t in outs.items():
+            assert_close_rel(t.cpu().numpy(), ref[n], 1e-3 if is16 else 1e-6, f'{name} {which} {n}')
+
+
+def test_zsum_halo_planes_equal_full_domain():
+    op = pa.AutoDiffOp(W.stencil_27pt(dtype='float32'), boundary_handling='zeros')
+    k = op.forward_ast_gpu.compile()
+    assert k.primary_variant()[1].ZSUM
+    g = torch.Generator().manual_seed(0)
+    u = torch.rand((20, 24, 64), generator=g).cuda()
+    full = torch.empty_like(u)
+    k(u=u, out=full)
+    lo, hi = u[:9].contiguous(), u[9:].contiguous()
+    out_lo, out_hi = torch.empty_like(lo), torch.empty_like(hi)
+    k(u=lo, out=out_lo, halos={'u': (None, hi[:1].contiguous())})
+    k(u=hi, out=out_hi, halos={'u': (lo[-1:].contiguous(), None)})
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat([out_lo, out_hi]), full)

@@ -66,17 +66,31 @@ def test_all_schedules_compile_for_gfx950(builder, bh):
 
 def test_march_source_structure():
     op = pa.AutoDiffOp(W.diffusion_7pt(), boundary_handling='zeros')
-    src = op.forward_ast_gpu.compile().code
+    k = op.forward_ast_gpu.compile()
+    default = k.primary_variant()[1]
+    assert default.ZSUM and 'zsum schedule' in k.code            # measured default for star stencils
+    src, _ = k.source(('march', MarchConfig(CX=2, NR=2, VE=4)))   # the LDS-ring variant
     assert '__shared__' in src and '__syncthreads' in src
     assert 'XCD-aware' in src
     assert 'f32x4' in src                      # 16-byte plane loads
     # 7-point, NR=2 rows x CX=2 columns per thread, taps shared by the two rows read once:
     # per column 4 centre-column + 4 x-neighbour + 2 plane-above LDS taps; the plane below comes
     # from the register queue (lite ring: 2 LDS planes instead of 3)
-    cfg = op.forward_ast_gpu.compile().primary_variant()[1]
-    if (cfg.CX, cfg.NR) == (2, 2) and not cfg.FULL_RING:
-        assert len(re.findall(r'const float t_u_', src)) == 20
+    assert len(re.findall(r'const float t_u_', src)) == 20
     assert 'q_u_1_' in src
+
+
+def test_zsum_eligibility():
+    from pystencils_autodiff_amd.backends.hip_emitter import zsum_plan
+    u, out = pa.ps.fields("u, out: float32[3d]")
+    nonlinear = pa.ps.AssignmentCollection({out.center: u[1, 0, 0] * u[-1, 0, 0]})
+    op = pa.AutoDiffOp(nonlinear, boundary_handling='zeros')
+    k = op.forward_ast_gpu.compile()
+    assert zsum_plan(k.ir, MarchConfig()) is None
+    assert not k.primary_variant()[1].ZSUM
+    op27 = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
+    plan = zsum_plan(op27.forward_ast_gpu.ir, MarchConfig())
+    assert sorted(plan[0]['lin']) == [-1, 1] and len(plan[0]['lin'][1]) == 9
 
 
 def test_pack_args_alignment():
