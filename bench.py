@@ -203,7 +203,8 @@ def main():
             except Exception as exc:  # noqa: BLE001 - report, don't fail the GPU bench
                 cpu = {'value': None, 'unit': 'Mcells/s', 'cores': None, 'kind': 'port', 'sample': f'failed: {exc}'}
         workload = f'diffusion7_f32_{n}^3'
-        traffic, traffic_src = load_traffic(workload, f'{fwd_k.name}_march')
+        kname = fwd_k.source(fwd_k.last_variant)[1] if fwd_k.last_variant else fwd_k.name
+        traffic, traffic_src = load_traffic(workload, kname)
         res = {
             'metric': f'Mcells/s forward+backward, 3D 7-point fp32 {n}^3',
             'value': round(value, 1),
@@ -229,7 +230,7 @@ def main():
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
                          'traffic_source': traffic_src,
-                         'kernel': f'{fwd_k.name}_march (forward sweep; adjoint moves the same bytes)',
+                         'kernel': f'{kname} (forward sweep; the adjoint sweep moves the same bytes)',
                          'bytes_per_launch': bytes_fwd},
             'cpu_baseline': cpu,
         }

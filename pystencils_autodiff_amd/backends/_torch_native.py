@@ -22,7 +22,6 @@ constant fields; native errors raise ``RuntimeError`` instead of ``exit()``.
 On ``use_cuda=True`` there is no CPU fallback: a missing HIP extension raises.
 """
 import hashlib
-from collections import OrderedDict
 
 import sympy as sp
 
@@ -114,90 +113,99 @@ def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
     fwd_kernel_fields = {f.name for f in forward_kernel.ir.fields}
     bwd_kernel_fields = {f.name for f in backward_kernel.ir.fields} if backward_kernel else set()
     class_kwargs = dict()
-    device_kind = 'cuda' if use_cuda else 'cpu'
+
+    # everything that does not depend on the call's tensors is resolved once here
+    def _tdtype(field):
+        return numpy_dtype_to_torch(field.dtype.numpy_dtype)
+
+    def _fixed(field):
+        return tuple(int(x) for x in field.shape) if field.has_fixed_shape else None
+
+    fwd_call = forward_kernel.compile()
+    bwd_call = backward_kernel.compile() if backward_kernel else None
+    fwd_in = [(i, f.name) for i, f in enumerate(fwd_inputs) if f.name in fwd_kernel_fields]
+    fwd_out = [(f.name, _tdtype(f), _fixed(f)) for f in fwd_outputs]
+    fwd_scalars = [s.name for s in forward_kernel.ir.scalars]
+    fwd_alloc = torch.empty if _full_write(forward_kernel) else torch.zeros
+    saved_fwd = [n for n in [f.name for f in fwd_inputs] + [f.name for f in fwd_outputs] if n in bwd_kernel_fields]
+    if backward_kernel:
+        bwd_reads = {r.field.name for r in backward_kernel.ir.reads}
+        bwd_scalars = [s.name for s in backward_kernel.ir.scalars]
+        grad_specs = []
+        for f in fwd_outputs:
+            a = adj_of[f.name]
+            grad_specs.append((a.name if a is not None and a.name in bwd_kernel_fields else None, _tdtype(f),
+                               _fixed(a) if a is not None else None,
+                               tuple(a.strides) if a is not None and a.has_fixed_shape else None, f.name))
+        full = _full_write(backward_kernel)
+        bwd_out = [(f.name, _tdtype(f), _fixed(f), torch.empty if full and f.name not in bwd_reads else torch.zeros)
+                   for f in bwd_outputs]
+        in_adj = [adj_of[f.name].name if adj_of.get(f.name) is not None else None for f in fwd_inputs]
 
     def _to_device(t):
         if not isinstance(t, torch.Tensor):
             return t
-        t = t.cuda() if use_cuda else t.cpu()
-        return t.contiguous()
-
-    def _alloc(field, like, full):
-        dtype = numpy_dtype_to_torch(field.dtype.numpy_dtype)
-        shape = tuple(int(s) for s in field.shape) if field.has_fixed_shape else tuple(like.shape)
-        alloc = torch.empty if full else torch.zeros
-        return alloc(shape, dtype=dtype, device=like.device)
+        if use_cuda:
+            if not t.is_cuda:
+                t = t.cuda()
+        elif t.is_cuda:
+            t = t.cpu()
+        return t if t.is_contiguous() else t.contiguous()
 
     def forward(ctx, *args):
         args = [_to_device(a) for a in args]
-        kwargs = dict(class_kwargs)
         first = next((a for a in args if isinstance(a, torch.Tensor)), None)
         if first is None:
             raise ValueError(f"{op_name}: at least one input tensor is required")
-        for i, f in enumerate(fwd_inputs):
-            if i < len(args) and f.name in fwd_kernel_fields:
-                kwargs[f.name] = args[i]
-        full = _full_write(forward_kernel)
-        outputs = OrderedDict()
-        for f in fwd_outputs:
-            if f.name not in kwargs:
-                kwargs[f.name] = _alloc(f, first, full)
-            outputs[f.name] = kwargs[f.name]
-        forward_kernel(**{k: v for k, v in kwargs.items()
-                          if k in fwd_kernel_fields or k in {s.name for s in forward_kernel.ir.scalars}})
-        # keep what the backward kernel reads: forward inputs / outputs and scalars
-        saved_names = [n for n in list(kwargs) if n in bwd_kernel_fields and isinstance(kwargs[n], torch.Tensor)]
-        ctx.saved_names = saved_names
-        ctx.scalars = {k: v for k, v in kwargs.items() if not isinstance(v, torch.Tensor)}
-        ctx.save_for_backward(*[kwargs[n] for n in saved_names])
+        kwargs = {}
+        for i, name in fwd_in:
+            if i < len(args):
+                kwargs[name] = args[i]
+        for name in fwd_scalars:
+            if name not in class_kwargs:
+                raise TypeError(f"{op_name}: scalar parameter '{name}' missing: set {op_name}.class_kwargs['{name}']")
+            kwargs[name] = class_kwargs[name]
+        outputs = []
+        for name, dtype, fixed in fwd_out:
+            t = fwd_alloc(fixed if fixed is not None else first.shape, dtype=dtype, device=first.device)
+            kwargs[name] = t
+            outputs.append(t)
+        fwd_call(**kwargs)
+        ctx.saved_names = [n for n in saved_fwd if n in kwargs]
+        ctx.save_for_backward(*[kwargs[n] for n in ctx.saved_names])
+        ctx.scalars = dict(class_kwargs)
         ctx.n_inputs = len(args)
-        return tuple(outputs.values())
+        ctx.like_shape = first.shape
+        ctx.like_device = first.device
+        return tuple(outputs)
 
     def backward(ctx, *grad_outputs):
         if backward_kernel is None:
             return tuple(None for _ in range(ctx.n_inputs))
-        grads = []
-        for g, f in zip(grad_outputs, fwd_outputs):
-            if g is None:
-                a = adj_of[f.name]
-                like = ctx.saved_tensors[0] if ctx.saved_tensors else None
-                shape = tuple(int(s) for s in a.shape) if a is not None and a.has_fixed_shape else \
-                    (tuple(like.shape) if like is not None else None)
-                g = torch.zeros(shape, dtype=numpy_dtype_to_torch(f.dtype.numpy_dtype),
-                                device=device_kind if like is None else like.device)
-            grads.append(g.contiguous().cuda() if use_cuda else g.contiguous().cpu())
-        for g, f in zip(grads, fwd_outputs):
-            a = adj_of[f.name]
-            if a is None:
-                continue
-            if a.has_fixed_shape:
-                assert tuple(a.shape) == tuple(g.shape), f"gradient of {f.name} has shape {tuple(g.shape)}"
-                assert tuple(a.strides) == tuple(g.stride()), f"gradient of {f.name} has strides {g.stride()}"
-            assert g.is_cuda == use_cuda, ("Some of the tensors where on the wrong device. "
-                                           f"Op was compiled for CUDA: {str(use_cuda)}")
-        kwargs = dict(ctx.scalars)
+        kwargs = {n: ctx.scalars[n] for n in bwd_scalars}
         for n, t in zip(ctx.saved_names, ctx.saved_tensors):
             kwargs[n] = t
-        for g, f in zip(grads, fwd_outputs):
-            a = adj_of[f.name]
-            if a is not None and a.name in bwd_kernel_fields:
-                kwargs[a.name] = g
-        full = _full_write(backward_kernel)
-        like = grads[0]
-        result = OrderedDict()
-        for f in bwd_outputs:
-            # time-constant fields accumulate into their adjoint: start from zeros
-            accum = f.name in {r.field.name for r in backward_kernel.ir.reads}
-            result[f.name] = _alloc(f, like, full and not accum)
-            kwargs[f.name] = result[f.name]
-        backward_kernel(**{k: v for k, v in kwargs.items()
-                           if k in bwd_kernel_fields or k in {s.name for s in backward_kernel.ir.scalars}})
-        out = []
-        for i in range(ctx.n_inputs):
-            f = fwd_inputs[i] if i < len(fwd_inputs) else None
-            a = adj_of.get(f.name) if f is not None else None
-            out.append(result.get(a.name) if a is not None else None)
-        return tuple(out)
+        like = None
+        for g, (aname, dtype, fixed, strides, fname) in zip(grad_outputs, grad_specs):
+            if g is None:
+                g = torch.zeros(fixed if fixed is not None else ctx.like_shape, dtype=dtype, device=ctx.like_device)
+            g = _to_device(g)
+            assert g.is_cuda == use_cuda, ("Some of the tensors where on the wrong device. "
+                                           f"Op was compiled for CUDA: {str(use_cuda)}")
+            if fixed is not None:
+                assert tuple(g.shape) == fixed, f"gradient of {fname} has shape {tuple(g.shape)}"
+                assert tuple(g.stride()) == strides, f"gradient of {fname} has strides {g.stride()}"
+            if aname is not None:
+                kwargs[aname] = g
+            like = g if like is None else like
+        result = {}
+        for name, dtype, fixed, alloc in bwd_out:
+            t = alloc(fixed if fixed is not None else like.shape, dtype=dtype, device=like.device)
+            result[name] = t
+            kwargs[name] = t
+        bwd_call(**kwargs)
+        return tuple(result.get(a) if a is not None else None for a in in_adj[:ctx.n_inputs]) + \
+            (None,) * max(0, ctx.n_inputs - len(in_adj))
 
     def call(cls, **kwargs):
         rtn = cls.apply(*[kwargs[p.symbol.name] for p in cls.forward_parameters])

@@ -48,13 +48,14 @@ def main():
 
     n = a.n
     builder = {'diffusion7': (W.diffusion_7pt, torch.float32), 'stencil27': (W.stencil_27pt, torch.float16),
-               'laplace5': (W.laplace_5pt, torch.float32)}[a.workload]
+               'laplace5': (W.laplace_5pt, torch.float32),
+               'diffusion7_f64': (lambda: W.diffusion_7pt(dtype='float64'), torch.float64)}[a.workload]
     op = AutoDiffOp(builder[0](), boundary_handling='zeros')
     shape = (n, n) if a.workload == 'laplace5' else (n, n, n)
     cells = 1
     for s in shape:
         cells *= s
-    esize = 2 if builder[1] == torch.float16 else 4
+    esize = {torch.float16: 2, torch.float32: 4, torch.float64: 8}[builder[1]]
     u = torch.rand(shape, device='cuda').to(builder[1])
     out = torch.empty_like(u)
     spec = open(a.configs_file).read().strip() if a.configs_file else a.configs

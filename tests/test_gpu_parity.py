@@ -347,3 +347,59 @@ def test_zsum_halo_planes_equal_full_domain():
     k(u=hi, out=out_hi, halos={'u': (lo[-1:].contiguous(), None)})
     torch.cuda.synchronize()
     assert torch.equal(torch.cat([out_lo, out_hi]), full)
+
+
+def test_hip_graph_capture_of_op():
+    """The op's launches are capturable: forward in a torch.cuda.graph, fwd+bwd via make_graphed_callables."""
+    op = pa.AutoDiffOp(W.asym_7pt(), boundary_handling='zeros')
+    fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    shape = (16, 40, 64)
+    g = torch.Generator().manual_seed(0)
+    static_u = torch.rand(shape, generator=g).cuda()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            fn.apply(static_u)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        (static_out,) = fn.apply(static_u)
+    new_u = torch.rand(shape, generator=g)
+    static_u.copy_(new_u.cuda())
+    graph.replay()
+    torch.cuda.synchronize()
+    assert_close_rel(static_out.cpu().numpy(), S.linear_stencil(new_u.numpy(), S.taps_asym_7pt()), 1e-6, 'graph fwd')
+
+    class M(torch.nn.Module):
+        def forward(self, u):
+            return fn.apply(u)[0]
+
+    m = torch.cuda.make_graphed_callables(M(), (torch.rand(shape, device='cuda', requires_grad=True),))
+    u = torch.rand(shape, generator=g).cuda().requires_grad_(True)
+    d = torch.rand(shape, generator=g) * 2 - 1
+    out = m(u)
+    out.backward(d.cuda())
+    torch.cuda.synchronize()
+    taps = S.taps_asym_7pt()
+    assert_close_rel(out.detach().cpu().numpy(), S.linear_stencil(u.detach().cpu().numpy(), taps), 1e-6, 'graphed out')
+    assert_close_rel(u.grad.cpu().numpy(), S.linear_stencil(d.numpy(), S.flip(taps)), 1e-6, 'graphed grad')
+
+
+def test_scalar_parameter_op_gpu():
+    z, y, x = ps.fields("z, y, x: float32[20,40]")
+    a = sp.Symbol('a')
+    op = pa.AutoDiffOp(ps.AssignmentCollection({z[0, 0]: x[0, 0] * sp.log(a * x[0, 0] * y[0, 0])}))
+    fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    rng = np.random.default_rng(0)
+    xv = torch.from_numpy(rng.uniform(0.5, 1.5, (20, 40)).astype(np.float32)).cuda().requires_grad_(True)
+    yv = torch.from_numpy(rng.uniform(0.5, 1.5, (20, 40)).astype(np.float32)).cuda().requires_grad_(True)
+    with pytest.raises(TypeError, match='class_kwargs'):
+        fn.apply(xv, yv)
+    fn.class_kwargs['a'] = 5.0
+    zt = fn.call(x=xv, y=yv)
+    zt.sum().backward()
+    xn, yn = xv.detach().cpu().numpy().astype(np.float64), yv.detach().cpu().numpy().astype(np.float64)
+    assert_close_rel(zt.detach().cpu().numpy(), xn * np.log(5 * xn * yn), 1e-6)
+    assert_close_rel(xv.grad.cpu().numpy(), np.log(5 * xn * yn) + 1, 1e-6)
+    assert_close_rel(yv.grad.cpu().numpy(), xn / yn, 1e-6)
