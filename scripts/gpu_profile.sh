@@ -12,7 +12,7 @@ python -m pystencils_autodiff_amd.build > /dev/null || exit 3
 timeout -k 10 500 python scripts/bench_configs.py > "$OUT/configs_$TAG.jsonl" 2> "$OUT/configs_$TAG.err"; fatal $? configs
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o trace -- \
-    python "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/prof_$TAG.log" 2>&1; fatal $? trace
+    python "$ROOT/bench.py" --steps 30 --warmup 2 --no-cpu-baseline > "$OUT/prof_$TAG.log" 2>&1; fatal $? trace
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$TAG" -o pmc -- \
     python "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fetch_$TAG.log" 2>&1; fatal $? pmc_fetch
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$TAG" -o pmc -- \

@@ -96,7 +96,26 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ct.append(e0.elapsed_time(e1))
+    # a 16-byte-per-lane streaming copy through the emitter's pointwise schedule (out = u): the
+    # practical read+write ceiling on this device, measured in the same process
+    from pystencils_autodiff_amd import ps as _ps
+    cu, co = _ps.fields(f"cu, co: {str(u.dtype).replace('torch.', '')}[{len(shape)}d]")
+    ck = StencilKernel(_ps.AssignmentCollection({co.center: cu.center}), function_name='tunecopy',
+                       target='gpu').compile()
+    ck(cu=u, co=out)
+    pt = []
+    for _ in range(a.rounds):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.reps):
+            ck(cu=u, co=out)
+        e1.record()
+        torch.cuda.synchronize()
+        pt.append(e0.elapsed_time(e1) / a.reps)
     alg = 2 * esize * cells
+    pmed = sorted(pt)[len(pt) // 2]
+    print(f"pointwise copy: median {pmed:.4f} ms = {alg / (pmed * 1e-3) / 1e9:.0f} GB/s")
     print(f"copy_: median {sorted(ct)[len(ct) // 2]:.4f} ms = {alg / (sorted(ct)[len(ct) // 2] * 1e-3) / 1e9:.0f} GB/s")
     for i, c in enumerate(cfgs):
         ts = sorted(times[i])
