@@ -45,18 +45,6 @@ def default_march_config(ir, ve, shape=None, tuning=None):
         cfg.update(CX=4, WX=1, NR=4, VIEW2D='yx', NT_STORE=False)   # 256×16 tiles (4096²: 0.024 ms, 5.6 TB/s)
     if np.dtype(ir.compute_dtype).itemsize == 8:
         cfg['CX'] = max(1, cfg['CX'] // 2)                     # fp64: half-width tiles (512³: 0.380 vs 0.536 ms)
-    if shape is not None:
-        X = int(shape[-1])
-        while cfg['CX'] > 1 and 64 * cfg['CX'] // 2 >= X:
-            cfg['CX'] //= 2
-        ny = int(shape[-2]) if ir.ndim == 3 or cfg['VIEW2D'] == 'yx' else 1
-        while cfg['NR'] > 1 and 4 * cfg['NR'] // 2 >= ny:
-            cfg['NR'] //= 2
-    while march_geometry(ir, MarchConfig(VE=ve, **cfg))['lds_bytes'] > 80 * 1024 and (cfg['NR'] > 1 or cfg['CX'] > 1):
-        if cfg['NR'] >= cfg['CX'] and cfg['NR'] > 1:
-            cfg['NR'] //= 2
-        else:
-            cfg['CX'] //= 2
     env = os.environ.get('PSAD_MARCH')
     over = dict(tuning or {})
     if env:
@@ -70,6 +58,24 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
         elif k == 'VIEW2D':
             cfg[k] = str(v)
+    if cfg['ZSUM'] and zsum_plan(ir, MarchConfig(VE=ve, **cfg)) is None:
+        cfg['ZSUM'] = False                                    # not eligible: LDS ring instead
+    if shape is not None:
+        X = int(shape[-1])
+        if 'CX' not in over:
+            while cfg['CX'] > 1 and 64 * cfg['CX'] * cfg['WX'] // 2 >= X:
+                cfg['CX'] //= 2
+        ny = int(shape[-2]) if ir.ndim == 3 or cfg['VIEW2D'] == 'yx' else 1
+        if 'NR' not in over:
+            while cfg['NR'] > 1 and (4 // cfg['WX']) * cfg['NR'] // 2 >= ny:
+                cfg['NR'] //= 2
+    # LDS budget: two workgroups per CU (≤ 80 KB) for the defaults, the 160 KB hardware limit always
+    budget = 80 * 1024 if not ('CX' in over or 'NR' in over) else 160 * 1024
+    while march_geometry(ir, MarchConfig(VE=ve, **cfg))['lds_bytes'] > budget and (cfg['NR'] > 1 or cfg['CX'] > 1):
+        if cfg['NR'] >= cfg['CX'] and cfg['NR'] > 1:
+            cfg['NR'] //= 2
+        else:
+            cfg['CX'] //= 2
     return MarchConfig(VE=ve, **cfg)
 
 

@@ -93,6 +93,9 @@ class FieldShapeSymbol(sp.Symbol):
     def __getnewargs__(self):
         return self.field_names, self.coordinate
 
+    def __getnewargs_ex__(self):
+        return (self.field_names, self.coordinate), {}
+
     def _hashable_content(self):
         return super()._hashable_content() + (self.field_names, self.coordinate)
 
@@ -108,6 +111,9 @@ class FieldStrideSymbol(sp.Symbol):
 
     def __getnewargs__(self):
         return self.field_name, self.coordinate
+
+    def __getnewargs_ex__(self):
+        return (self.field_name, self.coordinate), {}
 
     def _hashable_content(self):
         return super()._hashable_content() + (self.field_name, self.coordinate)

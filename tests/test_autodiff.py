@@ -162,3 +162,15 @@ def test_reproducible_code_generation():
         clear_cache()
         first = first or code
         assert code == first
+
+
+def test_op_pickle_roundtrip():
+    import pickle
+    u, out = ps.fields("u, out: float32[3d]")
+    op = pa.AutoDiffOp(ps.AssignmentCollection({out.center: u[1, 0, 0] - 2 * u[0, -1, 0]}), boundary_handling='zeros',
+                       op_name='pickled')
+    op2 = pickle.loads(pickle.dumps(op))
+    assert str(op2.forward_assignments) == str(op.forward_assignments)
+    assert str(op2.backward_assignments) == str(op.backward_assignments)
+    assert op2.boundary_handling == op.boundary_handling and op2.op_name == 'pickled'
+    assert [f.name for f in op2.backward_output_fields] == ['diffu']

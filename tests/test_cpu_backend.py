@@ -137,3 +137,19 @@ def test_strided_inputs_generic_cpu():
     ref = OE.evaluate(op64.forward_assignments, {'u': np.ascontiguousarray(u)}, boundary_handling='zeros')['out']
     assert_close_rel(out, ref, 1e-14)
     del op
+
+
+def test_readme_op_cpu_backend_fp32_golden():
+    """BASELINE config 1: README op z = x*log(x*y) on [20,30] fp32, CPU backend, forward+backward."""
+    g = golden('readme_f32_20x30')
+    op = pa.AutoDiffOp(W.readme_op())
+    fn = op.create_tensorflow_op(use_cuda=False, backend='torch_native')
+    x = torch.from_numpy(g['x']).requires_grad_(True)
+    y = torch.from_numpy(g['y']).requires_grad_(True)
+    (z,) = fn.apply(x, y)
+    z.backward(torch.from_numpy(g['diffz']))
+    assert_close_rel(z.detach().numpy(), g['z'], 1e-6, 'z')
+    assert_close_rel(x.grad.numpy(), g['diffx'], 1e-6, 'diffx')
+    assert_close_rel(y.grad.numpy(), g['diffy'], 1e-6, 'diffy')
+    # the reference interior-only semantics: boundary_handling=None and offset-free -> every cell written
+    assert op.forward_ast_cpu.ir.ghost_layers == 0

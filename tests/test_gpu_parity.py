@@ -403,3 +403,47 @@ def test_scalar_parameter_op_gpu():
     assert_close_rel(zt.detach().cpu().numpy(), xn * np.log(5 * xn * yn), 1e-6)
     assert_close_rel(xv.grad.cpu().numpy(), np.log(5 * xn * yn) + 1, 1e-6)
     assert_close_rel(yv.grad.cpu().numpy(), xn / yn, 1e-6)
+
+
+def _radius2_cases():
+    u, out = ps.fields("u, out: float32[3d]")
+    star = 0
+    w = [-1 / 12, 4 / 3, -5 / 2, 4 / 3, -1 / 12]                 # 4th-order Laplacian, radius 2
+    for d in range(3):
+        for k, o in enumerate(range(-2, 3)):
+            off = [0, 0, 0]
+            off[d] = o
+            star += sp.Float(w[k]) * u[tuple(off)]
+    asym = 0.3 * u[2, -1, 0] - 0.7 * u[-2, 1, 1] + 0.11 * u[0, 2, -2] + 0.5 * u.center - 0.2 * u[1, 0, 2]
+    nonlin = sp.exp(0.1 * u[-2, 0, 0]) * u[0, 1, 0] + 0.3 * u[2, 0, 0]
+    return [('star4', ps.AssignmentCollection({out.center: star})),
+            ('asym2', ps.AssignmentCollection({out.center: asym})),
+            ('nonlin2', ps.AssignmentCollection({out.center: nonlin}))]
+
+
+@pytest.mark.parametrize('case', _radius2_cases(), ids=lambda c: c[0])
+@pytest.mark.parametrize('params', [dict(), dict(ZSUM=False), dict(ZSUM=False, FULL_RING=True),
+                                    dict(CX=1, NR=3, ZC=7), dict(ZSUM=False, PD=2, CX=2, NR=2)])
+@pytest.mark.parametrize('bh', ['zeros', None])
+def test_radius2_stencils_vs_oracle(case, params, bh):
+    from pystencils_autodiff_amd.backends.hip_emitter import zsum_plan
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    name, ac = case
+    op = pa.AutoDiffOp(ac, boundary_handling=bh)
+    shape = (14, 23, 70)
+    rng = np.random.default_rng(11)
+    arrays = {'u': rng.uniform(-1, 1, shape).astype(np.float32),
+              'diffout': rng.uniform(-1, 1, shape).astype(np.float32)}
+    for which, a in (('f', op.forward_assignments), ('b', op.backward_assignments)):
+        k = StencilKernel(a, boundary_handling=bh, function_name=f'r2_{which}', target='gpu',
+                          gpu_indexing_params=params).compile()
+        ins = {f.name: arrays[f.name] for f in k.ir.fields_read}
+        ref = OE.evaluate(a, ins, boundary_handling=bh)
+        outs = {f.name: torch.zeros(shape, device='cuda') for f in k.ir.fields_written}
+        k(**{n: torch.from_numpy(v).cuda() for n, v in ins.items()}, **outs)
+        torch.cuda.synchronize()
+        assert k.last_variant[0] == 'march'
+        if params.get('ZSUM', True) is not False and zsum_plan(k.ir, k.last_variant[1]) is None:
+            assert not k.last_variant[1].ZSUM
+        for n, t in outs.items():
+            assert_close_rel(t.cpu().numpy(), ref[n], 1e-6, f'{name} {which} {n}')
