@@ -153,3 +153,56 @@ class ZSlabOp:
         for name, t in outs.items():
             if rz:
                 t.copy_(ghosted[name][rz:rz + zl])
+
+    def autograd_function(self):
+        """A ``torch.autograd.Function`` over this rank's slabs with the drop-in op's contract:
+        ``apply(*slabs)`` in ``forward_input_fields`` order returns the output slabs (tuple, in
+        ``forward_output_fields`` order); ``backward`` exchanges the gradient halos and returns the
+        input gradients. Scalars come from ``class_kwargs``."""
+        op = self.op
+        zop = self
+        fwd_inputs = list(op.forward_input_fields)
+        fwd_outputs = list(op.forward_output_fields)
+        fk, bk = self.kernels['forward'], self.kernels['backward']
+        fwd_names = {f.name for f in fk.ir.fields}
+        bwd_names = {f.name for f in bk.ir.fields}
+        bwd_outputs = [f.name for f in op.backward_output_fields]
+        prefix = 'diff'
+
+        def tdtype(f):
+            return getattr(torch, f.dtype.numpy_dtype.name)
+
+        class ZSlabFunction(torch.autograd.Function):
+            class_kwargs = {}
+
+            @staticmethod
+            def forward(ctx, *slabs):
+                kw = {f.name: t.contiguous() for f, t in zip(fwd_inputs, slabs) if f.name in fwd_names}
+                kw.update({s.name: ZSlabFunction.class_kwargs[s.name] for s in fk.ir.scalars})
+                outs = [torch.empty_like(slabs[0], dtype=tdtype(f)) for f in fwd_outputs]
+                kw.update({f.name: t for f, t in zip(fwd_outputs, outs)})
+                zop.fwd(**kw)
+                saved = [n for n in [f.name for f in fwd_inputs + fwd_outputs] if n in bwd_names and n in kw]
+                ctx.saved_names = saved
+                ctx.save_for_backward(*[kw[n] for n in saved])
+                ctx.n_inputs = len(slabs)
+                return tuple(outs)
+
+            @staticmethod
+            def backward(ctx, *grads):
+                kw = dict(zip(ctx.saved_names, ctx.saved_tensors))
+                kw.update({s.name: ZSlabFunction.class_kwargs[s.name] for s in bk.ir.scalars})
+                like = next(g for g in grads if g is not None)
+                for f, g in zip(fwd_outputs, grads):
+                    if prefix + f.name in bwd_names:
+                        kw[prefix + f.name] = (g if g is not None else torch.zeros_like(like)).contiguous()
+                res = {}
+                for name in bwd_outputs:
+                    accum = any(r.field.name == name for r in bk.ir.reads)
+                    res[name] = (torch.zeros_like if accum else torch.empty_like)(like)
+                    kw[name] = res[name]
+                zop.bwd(**kw)
+                return tuple(res.get(prefix + f.name) for f in fwd_inputs[:ctx.n_inputs])
+
+        ZSlabFunction.__name__ = f"{op.op_name}_zslab"
+        return ZSlabFunction

@@ -43,8 +43,16 @@ def _worker(rank, world, port, shape, builder_name, use_cuda, result_dir):
         out = torch.zeros_like(ul)
         du = torch.zeros_like(ul)
         z = ZSlabOp(op, use_cuda=use_cuda)
-        z.fwd(u=ul, out=out)
-        z.bwd(diffout=dl, diffu=du)
+        if os.environ.get('PSAD_TEST_ZSLAB_AUTOGRAD'):
+            fn = z.autograd_function()
+            uu = ul.clone().requires_grad_(True)
+            (o,) = fn.apply(uu)
+            o.backward(dl)
+            out.copy_(o.detach())
+            du.copy_(uu.grad)
+        else:
+            z.fwd(u=ul, out=out)
+            z.bwd(diffout=dl, diffu=du)
         if use_cuda:
             torch.cuda.synchronize()
         np.save(os.path.join(result_dir, f'out_{rank}.npy'), out.cpu().numpy())
@@ -72,6 +80,14 @@ def _run(world, shape, builder_name, use_cuda, tmp_path):
 def test_zslab_gloo_cpu(world, shape, builder_name, tmp_path):
     from tests.conftest import assert_close_rel
     out, du, ref_out, ref_du = _run(world, shape, builder_name, False, tmp_path)
+    assert_close_rel(out, ref_out, 1e-6, 'out')
+    assert_close_rel(du, ref_du, 1e-6, 'diffu')
+
+
+def test_zslab_autograd_function_gloo_cpu(tmp_path, monkeypatch):
+    from tests.conftest import assert_close_rel
+    monkeypatch.setenv('PSAD_TEST_ZSLAB_AUTOGRAD', '1')
+    out, du, ref_out, ref_du = _run(2, (11, 8, 9), 'asym_7pt', False, tmp_path)
     assert_close_rel(out, ref_out, 1e-6, 'out')
     assert_close_rel(du, ref_du, 1e-6, 'diffu')
 
