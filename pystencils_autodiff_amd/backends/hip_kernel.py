@@ -54,7 +54,7 @@ def default_march_config(ir, ve, shape=None, tuning=None):
     for k, v in over.items():
         if k in ('CX', 'WX', 'NR', 'PD', 'WAVES', 'LDS_PAD', 'ZCT'):
             cfg[k] = int(v)
-        elif k in ('NT_STORE', 'FULL_RING', 'LAZY', 'ZSUM'):
+        elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'LAZY', 'ZSUM'):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
         elif k == 'VIEW2D':
             cfg[k] = str(v)
@@ -247,8 +247,9 @@ class HipStencilKernel:
         fns = self.function(('pointwise',), device)
         n = int(np.prod(shape))
         aligned = all(t.data_ptr() % 32 == 0 for t in tensors)
-        per_block = 256 * (4 if aligned else 1)
-        blocks = max(1, min(math.ceil(n / per_block), 256 * 16))
+        from .hip_emitter import POINTWISE_UNROLL
+        per_block = 256 * (4 * POINTWISE_UNROLL if aligned else 1)
+        blocks = max(1, min(math.ceil(n / per_block), 256 * 8 if aligned else 256 * 16))
         kinds = ['ptr'] * len(tensors) + ['i64'] + [self._scalar_kind()] * len(self.ir.scalars)
         return _Plan(('pointwise', 'v4' if aligned else 'v1'), fns['v4' if aligned else 'v1'], blocks, kinds,
                      len(tensors), 0, [n])

@@ -99,23 +99,28 @@ def main():
     # a 16-byte-per-lane streaming copy through the emitter's pointwise schedule (out = u): the
     # practical read+write ceiling on this device, measured in the same process
     from pystencils_autodiff_amd import ps as _ps
+    from pystencils_autodiff_amd.backends import hip_emitter as _he
     cu, co = _ps.fields(f"cu, co: {str(u.dtype).replace('torch.', '')}[{len(shape)}d]")
-    ck = StencilKernel(_ps.AssignmentCollection({co.center: cu.center}), function_name='tunecopy',
-                       target='gpu').compile()
-    ck(cu=u, co=out)
-    pt = []
-    for _ in range(a.rounds):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(a.reps):
-            ck(cu=u, co=out)
-        e1.record()
-        torch.cuda.synchronize()
-        pt.append(e0.elapsed_time(e1) / a.reps)
     alg = 2 * esize * cells
-    pmed = sorted(pt)[len(pt) // 2]
-    print(f"pointwise copy: median {pmed:.4f} ms = {alg / (pmed * 1e-3) / 1e9:.0f} GB/s")
+    for nt_load in (False, True):
+        _he.POINTWISE_NT_LOAD = nt_load
+        ck = StencilKernel(_ps.AssignmentCollection({co.center: cu.center}),
+                           function_name=f'tunecopy{int(nt_load)}', target='gpu').compile()
+        ck(cu=u, co=out)
+        pt = []
+        for _ in range(a.rounds):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.reps):
+                ck(cu=u, co=out)
+            e1.record()
+            torch.cuda.synchronize()
+            pt.append(e0.elapsed_time(e1) / a.reps)
+        pmed = sorted(pt)[len(pt) // 2]
+        print(f"pointwise copy{' (nt loads)' if nt_load else ''}: median {pmed:.4f} ms = "
+              f"{alg / (pmed * 1e-3) / 1e9:.0f} GB/s")
+    _he.POINTWISE_NT_LOAD = False
     print(f"copy_: median {sorted(ct)[len(ct) // 2]:.4f} ms = {alg / (sorted(ct)[len(ct) // 2] * 1e-3) / 1e9:.0f} GB/s")
     for i, c in enumerate(cfgs):
         ts = sorted(times[i])
