@@ -31,12 +31,14 @@ def default_march_config(ir, ve, shape=None, tuning=None):
     ``PSAD_MARCH="CX=..,NR=.."``.
     """
     from .hip_emitter import lite_fields
-    cfg = dict(CX=4, WX=1, NR=8, NT_STORE=True, PD=1, FULL_RING=False, VIEW2D='yx', ZSUM=False, ZCT=0)
+    cfg = dict(CX=4, WX=1, NR=8, NT_STORE=True, PD=1, FULL_RING=False, VIEW2D='yx', ZSUM=False, ZCT=0, PK=False)
     probe = MarchConfig(VE=ve, **cfg)
     zsum_ok = zsum_plan(ir, probe) is not None
     if ir.ndim == 3 and set(ir.stencil_fields) - lite_fields(ir, probe):
         if zsum_ok:      # box stencil linear off-centre (27-point): z partial sums, small tile, short chunks
-            cfg.update(CX=2, NR=4, ZSUM=True, ZCT=32)          # 768³ fp16: 0.477 ms vs 0.70 ms ring
+            # 768³ fp16: 0.460 ms (packed fp32 FMAs over column pairs, 2 waves side by side in x)
+            # vs 0.469 scalar WX=1 vs 0.70 ms LDS ring; unrolling the plane loop 3x is slower (0.53-0.56)
+            cfg.update(CX=2, WX=2, NR=4, ZSUM=True, ZCT=32, PK=True)
         else:
             cfg.update(CX=2, NR=4)                             # box stencil: full ring, LDS/VALU bound
     elif ir.ndim == 3 and zsum_ok:
@@ -54,7 +56,7 @@ def default_march_config(ir, ve, shape=None, tuning=None):
     for k, v in over.items():
         if k in ('CX', 'WX', 'NR', 'PD', 'WAVES', 'LDS_PAD', 'ZCT'):
             cfg[k] = int(v)
-        elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'LAZY', 'ZSUM'):
+        elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'LAZY', 'ZSUM', 'PK', 'ZU'):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
         elif k == 'VIEW2D':
             cfg[k] = str(v)
@@ -65,6 +67,9 @@ def default_march_config(ir, ve, shape=None, tuning=None):
         if 'CX' not in over:
             while cfg['CX'] > 1 and 64 * cfg['CX'] * cfg['WX'] // 2 >= X:
                 cfg['CX'] //= 2
+        if 'WX' not in over:
+            while cfg['WX'] > 1 and 64 * cfg['CX'] * cfg['WX'] // 2 >= X:
+                cfg['WX'] //= 2
         ny = int(shape[-2]) if ir.ndim == 3 or cfg['VIEW2D'] == 'yx' else 1
         if 'NR' not in over:
             while cfg['NR'] > 1 and (4 // cfg['WX']) * cfg['NR'] // 2 >= ny:

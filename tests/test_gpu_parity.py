@@ -303,7 +303,10 @@ def _zsum_cases():
 
 
 @pytest.mark.parametrize('params', [dict(ZSUM=True), dict(ZSUM=True, CX=1, NR=3, ZC=5),
-                                    dict(ZSUM=True, CX=4, NR=8, NT_STORE=True), dict(ZSUM=True, WX=2, CX=2, NR=2)])
+                                    dict(ZSUM=True, CX=4, NR=8, NT_STORE=True), dict(ZSUM=True, WX=2, CX=2, NR=2),
+                                    dict(ZSUM=True, PK=True, CX=2, NR=3, ZC=7),
+                                    dict(ZSUM=True, ZU=True, CX=2, NR=2, ZC=5),
+                                    dict(ZSUM=True, PK=True, ZU=True, WX=2, CX=4, NR=2, ZC=4)])
 @pytest.mark.parametrize('case', _zsum_cases(), ids=lambda c: c[0])
 @pytest.mark.parametrize('bh', ['zeros', None])
 def test_zsum_schedule_vs_oracle(params, case, bh):

@@ -93,6 +93,24 @@ def test_zsum_eligibility():
     assert sorted(plan[0]['lin']) == [-1, 1] and len(plan[0]['lin'][1]) == 9
 
 
+def test_zsum_packed_and_unrolled_variants_compile():
+    op27 = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
+    k = op27.forward_ast_gpu.compile()
+    default = k.primary_variant()[1]
+    assert default.ZSUM and default.PK and default.WX == 2        # measured default for box stencils
+    for cfg in (MarchConfig(VE=8, CX=2, NR=4, ZSUM=True, PK=True),
+                MarchConfig(VE=8, CX=2, NR=4, ZSUM=True, PK=True, ZU=True),
+                MarchConfig(VE=8, CX=3, NR=2, ZSUM=True, PK=True)):       # odd CX: scalar fallback
+        src, name = k.source(('march', cfg))
+        assert ('f32x2 a0_' in src) == (cfg.CX % 2 == 0)
+        assert ('p0 += 3' in src) == cfg.ZU                              # 2*RZ+1 phases, renamed accumulators
+        code = rt.compile_hip(src)
+        assert _is_amdgpu_elf(code) and name.encode() in code
+    # every off-centre tap is one fused multiply-add into its accumulator
+    src, _ = k.source(('march', MarchConfig(VE=8, CX=2, NR=1, ZSUM=True, PK=True)))
+    assert re.search(r'a0_\d_p0_0 = a0_\d_p0_0 \+ \(', src)
+
+
 def test_pack_args_alignment():
     buf = rt.pack_args([('ptr', 0x1000), ('i32', 7), ('i64', 9), ('f32', 1.5), ('f64', 2.0), ('i32', 3)])
     assert len(buf) % 8 == 0
