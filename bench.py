@@ -120,36 +120,23 @@ def main():
     ev = []
 
     if distributed:
-        zop = ZSlabOp(op, use_cuda=True)
-        out = torch.empty_like(u)
-        du = torch.empty_like(u)
+        # the same drop-in contract over this rank's slab: Function.apply + backward, with the
+        # RCCL halo exchange inside the forward and the backward (zslab.py)
+        fn = ZSlabOp(op, use_cuda=True).autograd_function()
+    uu = u.requires_grad_(True)
 
-        def step(record):
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e2 = torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            zop.fwd(u=u, out=out)
-            e1.record(stream)
-            zop.bwd(diffout=d, diffu=du)
-            e2.record(stream)
-            if record:
-                ev.append((e0, e1, e2))
-    else:
-        uu = u.requires_grad_(True)
-
-        def step(record):
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e2 = torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            (o,) = fn.apply(uu)
-            e1.record(stream)
-            o.backward(d)
-            e2.record(stream)
-            uu.grad = None
-            if record:
-                ev.append((e0, e1, e2))
+    def step(record):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e2 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        (o,) = fn.apply(uu)
+        e1.record(stream)
+        o.backward(d)
+        e2.record(stream)
+        uu.grad = None
+        if record:
+            ev.append((e0, e1, e2))
 
     for _ in range(args.warmup):
         step(False)
@@ -221,8 +208,8 @@ def main():
             'config': {'workload': f'3D 7-point diffusion out=u+0.1*(sum6 u[nb]-6u), boundary zeros, fp32, '
                                    f'{n}^3 forward + TF-MAD adjoint per step',
                        'cells': cells_total, 'decomposition': f'z-slab x{world}' if world > 1 else 'single GPU',
-                       'path': 'AutoDiffOp.create_tensorflow_op(backend=torch_native) apply+backward'
-                       if world == 1 else 'ZSlabOp fwd/bwd with RCCL halo exchange'},
+                       'path': ('AutoDiffOp.create_tensorflow_op(backend=torch_native) apply+backward' if world == 1
+                                else 'ZSlabOp(AutoDiffOp).autograd_function() apply+backward, RCCL halo exchange')},
             'fwd_ms': round(fwd_ms, 4),
             'bwd_ms': round(bwd_ms, 4),
             'hbm_roofline_frac_step': round(2 * BYTES_PER_CELL_SWEEP * cells_total / (ms_per_step * 1e-3) / 1e9

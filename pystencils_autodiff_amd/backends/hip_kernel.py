@@ -47,6 +47,10 @@ def default_march_config(ir, ve, shape=None, tuning=None):
         cfg.update(CX=4, WX=1, NR=4, VIEW2D='yx', NT_STORE=False)   # 256×16 tiles (4096²: 0.024 ms, 5.6 TB/s)
     if np.dtype(ir.compute_dtype).itemsize == 8:
         cfg['CX'] = max(1, cfg['CX'] // 2)                     # fp64: half-width tiles (512³: 0.380 vs 0.536 ms)
+    elif ir.ndim == 3 and cfg['ZSUM'] and not cfg['PK']:
+        # star stencils: 128×32 tiles, two workgroups per CU. 512³ / one 8-GPU slab of 1024³
+        # (128×1024²): 0.191 / 0.187 ms vs 0.214 / 0.208 ms with 256×32 tiles; 1024³ a tie
+        cfg['CX'] = 2
     env = os.environ.get('PSAD_MARCH')
     over = dict(tuning or {})
     if env:
@@ -173,7 +177,9 @@ class HipStencilKernel:
 
         ``halos`` = ``{field: (lo_planes, hi_planes)}``: tensors holding the RZ planes just
         below plane 0 / above plane Z-1 of a stencil field (``None`` = zeros); ``z_range``
-        restricts the written planes of axis 0 (both: z-slab decomposition, ``zslab.py``).
+        restricts the written planes of axis 0 — ``(lo, hi)``, or two disjoint ranges of equal
+        length ``((lo0, hi0), (lo1, hi1))`` written by ONE launch (the two slab faces; both:
+        z-slab decomposition, ``zslab.py``).
         The first call for a given (shape, alignment, halo layout, z range) builds a launch plan
         (variant, function handle, grid, argument layout); later calls only re-pack pointers.
         """
@@ -220,7 +226,7 @@ class HipStencilKernel:
         strides = None if contiguous else tuple(tuple(t.stride()) for t in tensors)
         align = tuple(p % 32 == 0 for p in ptrs + hptrs)
         key = (force_schedule, shape, strides, align, tuple(h is not None for h in halo_list),
-               tuple(z_range) if z_range is not None else None, device)
+               _zkey(z_range), device)
         plan = self._plans.get(key)
         if plan is None:
             plan = self._make_plan(tensors, halo_list, shape, device, contiguous, force_schedule, z_range)
@@ -277,6 +283,18 @@ class HipStencilKernel:
         """(Z, Y, X), bounds and grid of the march schedule for a field shape."""
         ir = self.ir
         bounds = ir.iteration_bounds(shape)
+        if z_range is not None and _is_pair(z_range):
+            (a0, a1), (b0, b1) = [(int(a), int(b)) for a, b in z_range]
+            lo, hi = bounds[0]
+            if ir.ndim == 2 and cfg.VIEW2D == 'yx':
+                raise ValueError("z ranges need the 'zy' view of 2-D fields")
+            if not (lo <= a0 < a1 <= b0 < b1 <= hi) or a1 - a0 != b1 - b0:
+                raise ValueError(f'z_range pair {z_range} must be disjoint, ordered, of equal length '
+                                 f'and inside [{lo}, {hi})')
+            geo = self.march_launch_geometry(shape, cfg, (a0, b1))
+            zc = a1 - a0
+            geo.update(zlo=a0, zhi=b1, zc=zc, zstep=b0 - a0, grid=geo['ntx'] * geo['nty'] * 2)
+            return geo
         if z_range is not None:
             lo, hi = bounds[0]
             bounds = [(max(lo, int(z_range[0])), min(hi, int(z_range[1])))] + list(bounds[1:])
@@ -298,14 +316,16 @@ class HipStencilKernel:
         nty = max(1, math.ceil(yhi / cfg.TY))
         nt = ntx * nty
         nz = max(0, zhi - zlo)
-        target = int(self.kernel.tuning.get('BLOCKS', os.environ.get('PSAD_MARCH_BLOCKS', 2048)))
+        # chunk length: aim at ~2 workgroups per CU (512 blocks), 32..128 planes per chunk (each chunk
+        # re-reads 2·RZ halo planes; >128 measured slower at 1024³)
+        target = int(self.kernel.tuning.get('BLOCKS', os.environ.get('PSAD_MARCH_BLOCKS', 512)))
         zc = self.kernel.tuning.get('ZC') or int(os.environ.get('PSAD_MARCH_ZC', 0)) or cfg.ZCT or \
-            max(min(nz, 32), min(nz, math.ceil(nz * nt / target)))
+            min(nz, max(32, min(128, math.ceil(nz * nt / target))))
         zc = min(zc, nz) if nz else zc
         zc = max(zc, min(nz, 4 * max(1, march_geometry(ir, cfg)['RZ'])))
         nchunks = math.ceil(nz / zc) if nz else 0
-        return dict(Z=Z, Y=Y, X=X, zlo=zlo, zhi=zhi, ylo=ylo, yhi=yhi, xlo=xlo, xhi=xhi, zc=zc, ntx=ntx,
-                    nty=nty, grid=nt * nchunks)
+        return dict(Z=Z, Y=Y, X=X, zlo=zlo, zhi=zhi, ylo=ylo, yhi=yhi, xlo=xlo, xhi=xhi, zc=zc, zstep=zc,
+                    ntx=ntx, nty=nty, grid=nt * nchunks)
 
     def _plan_march(self, tensors, halo_list, shape, device, z_range):
         torch = _torch()
@@ -334,10 +354,21 @@ class HipStencilKernel:
                                      "on the field's device")
         if max(geo['Z'], geo['Y'], geo['X']) >= 2 ** 31 or grid >= 2 ** 31:
             raise ValueError('field extent too large for the march schedule')
-        statics = [int(geo[k]) for k in ('Z', 'Y', 'X', 'zlo', 'zhi', 'ylo', 'yhi', 'xlo', 'xhi', 'zc', 'ntx', 'nty')]
+        statics = [int(geo[k]) for k in ('Z', 'Y', 'X', 'zlo', 'zhi', 'ylo', 'yhi', 'xlo', 'xhi', 'zc', 'zstep', 'ntx',
+                                          'nty')]
         kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics) + \
             [self._scalar_kind()] * len(ir.scalars)
         return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics)
+
+
+def _is_pair(z_range):
+    return len(z_range) == 2 and all(isinstance(r, (tuple, list)) for r in z_range)
+
+
+def _zkey(z_range):
+    if z_range is None:
+        return None
+    return tuple(tuple(int(v) for v in r) for r in z_range) if _is_pair(z_range) else tuple(int(v) for v in z_range)
 
 
 class _Plan:

@@ -14,7 +14,8 @@ the MI355X layer's scale-out for the 3-D configs (BASELINE configs 4 and 5):
   boundary of the undivided domain;
 * the exchange overlaps the interior planes: the march kernel first writes
   planes ``[RZ, Zl-RZ)`` (no halo needed) while the faces are in flight, then,
-  after the receive completes, the ``RZ`` planes at each end. The halo planes
+  after the receive completes, the ``RZ`` planes at each end (one launch for both
+  faces: a two-range ``z_range``). The halo planes
   are read by the kernel in place from the receive buffers (no ghosted copy of
   the slab).
 
@@ -128,9 +129,10 @@ class ZSlabOp:
                     compiled(z_range=(rz, zl - rz), **kwargs)          # interior overlaps the exchange
                 for w in pending:
                     w.wait()                                          # current stream waits on RCCL
-                compiled(halos=halos, z_range=(0, min(rz, zl)), **kwargs)
-                if zl > rz:
-                    compiled(halos=halos, z_range=(max(rz, zl - rz), zl), **kwargs)
+                if zl > 2 * rz:                                       # both faces in one launch
+                    compiled(halos=halos, z_range=((0, rz), (zl - rz, zl)), **kwargs)
+                else:
+                    compiled(halos=halos, z_range=(0, zl), **kwargs)
             else:
                 compiled(halos=halos, **kwargs)
             return

@@ -24,6 +24,8 @@ DEFAULT = ';'.join([
 
 def parse_cfg(s):
     d = {}
+    if s.strip() == 'default':
+        return d
     for kv in s.split(','):
         k, v = kv.split('=')
         k = k.strip()
@@ -39,6 +41,7 @@ def main():
     p.add_argument('--configs', default=DEFAULT)
     p.add_argument('--workload', default='diffusion7')
     p.add_argument('--configs-file')
+    p.add_argument('--shape', help='Z,Y,X (overrides --n), e.g. 128,1024,1024 = one rank of 1024³ on 8 GPUs')
     a = p.parse_args()
     import torch
 
@@ -52,6 +55,8 @@ def main():
                'diffusion7_f64': (lambda: W.diffusion_7pt(dtype='float64'), torch.float64)}[a.workload]
     op = AutoDiffOp(builder[0](), boundary_handling='zeros')
     shape = (n, n) if a.workload == 'laplace5' else (n, n, n)
+    if a.shape:
+        shape = tuple(int(v) for v in a.shape.split(','))
     cells = 1
     for s in shape:
         cells *= s
@@ -126,7 +131,7 @@ def main():
         ts = sorted(times[i])
         med = ts[len(ts) // 2]
         geo = kernels[i].march_launch_geometry(shape if len(shape) == 3 else shape, kernels[i].last_variant[1])
-        print(f"tune{i:<3d} {','.join(f'{k}={v}' for k, v in c.items()):34s} median {med:.4f} ms  min {ts[0]:.4f} ms  "
+        print(f"tune{i:<3d} {','.join(f'{k}={v}' for k, v in c.items()) or 'default':34s} median {med:.4f} ms  min {ts[0]:.4f} ms  "
               f"{alg / (med * 1e-3) / 1e9:7.0f} GB/s  grid {geo['grid']} zc {geo['zc']}  maxdiff_vs_generic {maxdiff[i]:.2e}")
     sys.stdout.flush()
 

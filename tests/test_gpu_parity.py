@@ -202,6 +202,32 @@ def test_march_halo_planes_equal_full_domain():
     assert torch.equal(torch.cat([out_lo, out_hi]), full)
 
 
+@pytest.mark.parametrize('builder', [W.asym_7pt, lambda: W.stencil_27pt(dtype='float32')], ids=['asym7', '27pt'])
+def test_split_launches_interior_then_two_faces(builder):
+    """The z-slab launch pattern: interior planes first, then both faces in ONE two-range launch
+    (chunk stride = the gap) with halo planes == one full-domain launch, bitwise."""
+    op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
+    k = op.forward_ast_gpu.compile()
+    g = torch.Generator().manual_seed(3)
+    u = torch.rand((30, 21, 64), generator=g).cuda()
+    full = torch.empty_like(u)
+    k(u=u, out=full)
+    parts = [(0, 11), (11, 19), (19, 30)]
+    outs = []
+    for i, (a, b) in enumerate(parts):
+        sl = u[a:b].contiguous()
+        out = torch.full_like(sl, float('nan'))
+        lo = u[a - 1:a].contiguous() if a > 0 else None
+        hi = u[b:b + 1].contiguous() if b < 30 else None
+        k(u=sl, out=out, z_range=(1, b - a - 1))
+        k(u=sl, out=out, halos={'u': (lo, hi)}, z_range=((0, 1), (b - a - 1, b - a)))
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(outs), full)
+    with pytest.raises(ValueError):
+        k(u=u, out=full, z_range=((0, 2), (1, 3)))
+
+
 def test_adjoint_dot_product_identity_large():
     """<A u, d> == <u, A^T d> for the forward / backward kernels at 256^3 (size-independent property)."""
     op, fn = _op(W.asym_7pt())
