@@ -31,14 +31,17 @@ def default_march_config(ir, ve, shape=None, tuning=None):
     ``PSAD_MARCH="CX=..,NR=.."``.
     """
     from .hip_emitter import lite_fields
-    cfg = dict(CX=4, WX=1, NR=8, NT_STORE=True, PD=1, FULL_RING=False, VIEW2D='yx', ZSUM=False, ZCT=0, PK=False)
+    cfg = dict(CX=4, WX=1, NR=8, NT_STORE=True, PD=1, FULL_RING=False, VIEW2D='yx', ZSUM=False, ZCT=0, PK=False,
+               ZMIN=32, ZMAX=128, BLK=512)
     probe = MarchConfig(VE=ve, **cfg)
     zsum_ok = zsum_plan(ir, probe) is not None
     if ir.ndim == 3 and set(ir.stencil_fields) - lite_fields(ir, probe):
         if zsum_ok:      # box stencil linear off-centre (27-point): z partial sums, small tile, short chunks
             # 768³ fp16: 0.460 ms (packed fp32 FMAs over column pairs, 2 waves side by side in x)
             # vs 0.469 scalar WX=1 vs 0.70 ms LDS ring; unrolling the plane loop 3x is slower (0.53-0.56)
-            cfg.update(CX=2, WX=2, NR=4, ZSUM=True, ZCT=32, PK=True)
+            # chunks of 16..32 planes, ~2048 workgroups: 768³ 32 planes; one 8-GPU slab (96×768²) 16
+            # planes, 0.067 vs 0.073 ms at 32
+            cfg.update(CX=2, WX=2, NR=4, ZSUM=True, PK=True, ZMIN=16, ZMAX=32, BLK=2048)
         else:
             cfg.update(CX=2, NR=4)                             # box stencil: full ring, LDS/VALU bound
     elif ir.ndim == 3 and zsum_ok:
@@ -58,7 +61,7 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             k, v = kv.split('=')
             over[k.strip()] = v.strip() if k.strip() == 'VIEW2D' else int(v)
     for k, v in over.items():
-        if k in ('CX', 'WX', 'NR', 'PD', 'WAVES', 'LDS_PAD', 'ZCT'):
+        if k in ('CX', 'WX', 'NR', 'PD', 'WAVES', 'LDS_PAD', 'ZCT', 'ZMIN', 'ZMAX', 'BLK'):
             cfg[k] = int(v)
         elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'LAZY', 'ZSUM', 'PK', 'ZU'):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
@@ -318,9 +321,9 @@ class HipStencilKernel:
         nz = max(0, zhi - zlo)
         # chunk length: aim at ~2 workgroups per CU (512 blocks), 32..128 planes per chunk (each chunk
         # re-reads 2·RZ halo planes; >128 measured slower at 1024³)
-        target = int(self.kernel.tuning.get('BLOCKS', os.environ.get('PSAD_MARCH_BLOCKS', 512)))
+        target = int(self.kernel.tuning.get('BLOCKS', os.environ.get('PSAD_MARCH_BLOCKS', cfg.BLK)))
         zc = self.kernel.tuning.get('ZC') or int(os.environ.get('PSAD_MARCH_ZC', 0)) or cfg.ZCT or \
-            min(nz, max(32, min(128, math.ceil(nz * nt / target))))
+            min(nz, max(cfg.ZMIN, min(cfg.ZMAX, math.ceil(nz * nt / target))))
         zc = min(zc, nz) if nz else zc
         zc = max(zc, min(nz, 4 * max(1, march_geometry(ir, cfg)['RZ'])))
         nchunks = math.ceil(nz / zc) if nz else 0
