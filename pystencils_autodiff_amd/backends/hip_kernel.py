@@ -32,7 +32,7 @@ def default_march_config(ir, ve, shape=None, tuning=None):
     """
     from .hip_emitter import lite_fields
     cfg = dict(CX=4, WX=1, NR=8, NT_STORE=True, PD=1, FULL_RING=False, VIEW2D='yx', ZSUM=False, ZCT=0, PK=False,
-               ZMIN=32, ZMAX=128, BLK=512)
+               ZMIN=32, ZMAX=64, BLK=512)
     probe = MarchConfig(VE=ve, **cfg)
     zsum_ok = zsum_plan(ir, probe) is not None
     if ir.ndim == 3 and set(ir.stencil_fields) - lite_fields(ir, probe):
@@ -319,8 +319,9 @@ class HipStencilKernel:
         nty = max(1, math.ceil(yhi / cfg.TY))
         nt = ntx * nty
         nz = max(0, zhi - zlo)
-        # chunk length: aim at ~2 workgroups per CU (512 blocks), 32..128 planes per chunk (each chunk
-        # re-reads 2·RZ halo planes; >128 measured slower at 1024³)
+        # chunk length: aim at ~2 workgroups per CU (512 blocks), ZMIN..ZMAX planes per chunk (each chunk
+        # re-reads 2·RZ halo planes). 7-point 1024³, 128×32 tiles: 64-plane chunks 1.536 ms vs 128-plane
+        # 1.570 ms (profiles/r01_tune_cx_ab_1024.log); 512³ and 128×1024² slabs land on 64 by the target
         target = int(self.kernel.tuning.get('BLOCKS', os.environ.get('PSAD_MARCH_BLOCKS', cfg.BLK)))
         zc = self.kernel.tuning.get('ZC') or int(os.environ.get('PSAD_MARCH_ZC', 0)) or cfg.ZCT or \
             min(nz, max(cfg.ZMIN, min(cfg.ZMAX, math.ceil(nz * nt / target))))

@@ -46,6 +46,22 @@ def run(name, builder, shape, dtype, bh, nin, steps=20, warmup=3, bytes_fwd=None
             t.grad = None
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    # the same loop with torch's autograd device thread off (torch.autograd.set_multithreading_enabled):
+    # the backward runs in the calling thread, which removes the engine's thread hand-off (~60-75 µs
+    # per step measured, scripts/op_overhead_2d.py) from launch-bound configs
+    torch.autograd.set_multithreading_enabled(False)
+    try:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            outs = fn.apply(*ins)
+            torch.autograd.backward(list(outs), grads)
+            for t in ins:
+                t.grad = None
+        torch.cuda.synchronize()
+        el_st = time.perf_counter() - t0
+    finally:
+        torch.autograd.set_multithreading_enabled(True)
     cells = 1
     for s in shape:
         cells *= s
@@ -53,6 +69,8 @@ def run(name, builder, shape, dtype, bh, nin, steps=20, warmup=3, bytes_fwd=None
     b_ms = sorted(b.elapsed_time(c) for _, b, c in ev)[len(ev) // 2]
     res = {'config': name, 'shape': list(shape), 'dtype': str(dtype).replace('torch.', ''),
            'mcells_per_s': round(cells * steps / el / 1e6, 1), 'ms_per_step': round(el / steps * 1e3, 4),
+           'mcells_per_s_autograd_1thread': round(cells * steps / el_st / 1e6, 1),
+           'ms_per_step_autograd_1thread': round(el_st / steps * 1e3, 4),
            'fwd_ms': round(f_ms, 4), 'bwd_ms': round(b_ms, 4),
            'fwd_schedule': op.forward_ast_gpu.compile().last_variant[0],
            'bwd_schedule': op.backward_ast_gpu.compile().last_variant[0]}
