@@ -362,6 +362,36 @@ def test_zsum_schedule_vs_oracle(params, case, bh):
             assert_close_rel(t.cpu().numpy(), ref[n], 1e-3 if is16 else 1e-6, f'{name} {which} {n}')
 
 
+@pytest.mark.parametrize('params', [dict(ZSUM=True, CX=1, NR=2, ZC=4), dict(ZSUM=True, CX=2, NR=2, PK=True, PX=True),
+                                    dict(ZSUM=True, CX=2, WX=2, NR=1, PK=True, PX=True, ZC=3),
+                                    dict(ZSUM=True, CX=2, NR=2, FASTLOAD=False), dict(ZSUM=False, CX=1, NR=2)])
+@pytest.mark.parametrize('case', _zsum_cases(), ids=lambda c: c[0])
+def test_interior_tiles_vs_oracle(params, case):
+    """Shapes with interior tiles (unguarded plane loads) AND edge tiles, odd extents in y."""
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    name, builder = case
+    op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
+    is16 = name == '27pt'
+    dt = np.float16 if is16 else np.float32
+    shape = (7, 29, 520)
+    rng = np.random.default_rng(11)
+    arrays = {f.name: rng.uniform(-1, 1, shape).astype(dt) for f in op.forward_input_fields}
+    arrays.update({f.name: rng.uniform(-1, 1, shape).astype(dt) for f in op.backward_input_fields
+                   if f.name not in arrays})
+    for which, ac in (('f', op.forward_assignments), ('b', op.backward_assignments)):
+        k = StencilKernel(ac, boundary_handling='zeros', function_name=f'it_{which}', target='gpu',
+                          gpu_indexing_params=params).compile()
+        ins = {f.name: arrays[f.name] for f in k.ir.fields_read}
+        ref = OE.evaluate(ac, ins, boundary_handling='zeros')
+        outs = {f.name: torch.full(shape, float('nan'), dtype=torch.float16 if is16 else torch.float32, device='cuda')
+                for f in k.ir.fields_written}
+        k(**{n: torch.from_numpy(a).cuda() for n, a in ins.items()}, **outs)
+        torch.cuda.synchronize()
+        assert k.last_variant[0] == 'march'
+        for n, t in outs.items():
+            assert_close_rel(t.cpu().numpy(), ref[n], 1e-3 if is16 else 1e-6, f'{name} {which} {n} {params}')
+
+
 def test_zsum_halo_planes_equal_full_domain():
     op = pa.AutoDiffOp(W.stencil_27pt(dtype='float32'), boundary_handling='zeros')
     k = op.forward_ast_gpu.compile()
