@@ -14,7 +14,8 @@ import os
 import numpy as np
 
 from . import hip_runtime as rt
-from .hip_emitter import MarchConfig, emit_generic, emit_march, emit_pointwise, emit_zsum, march_geometry, zsum_plan
+from .hip_emitter import (MarchConfig, emit_generic, emit_march, emit_pointwise, emit_zsum, march_geometry, ws_geometry,
+                          zsum_plan)
 
 __all__ = ['HipStencilKernel', 'default_march_config']
 
@@ -46,11 +47,16 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             cfg.update(CX=2, NR=4)                             # box stencil: full ring, LDS/VALU bound
     elif ir.ndim == 3 and zsum_ok:
         cfg.update(ZSUM=True)                                  # 1024³ 7-point: 1.495 ms vs 1.629 ms lite ring
+        if ws_geometry(ir, MarchConfig(VE=ve, **{**cfg, 'WS': True})):
+            # star stencils, storage = compute type: LDS-DMA loader wave, 4 planes in flight, 256×16 tiles,
+            # 128-plane chunks (one 5-wave workgroup per CU). 1024³ 7-point 1.411 ms vs 1.506 ms register
+            # prefetch (128×32 tiles); one 8-GPU slab 0.182 vs 0.187 ms (profiles/r01_tune_ws_*.log)
+            cfg.update(WS=True, CX=4, NR=4, D=4, ZMAX=128, BLK=256)
     if ir.ndim == 2:
         cfg.update(CX=4, WX=1, NR=4, VIEW2D='yx', NT_STORE=False)   # 256×16 tiles (4096²: 0.024 ms, 5.6 TB/s)
     if np.dtype(ir.compute_dtype).itemsize == 8:
         cfg['CX'] = max(1, cfg['CX'] // 2)                     # fp64: half-width tiles (512³: 0.380 vs 0.536 ms)
-    elif ir.ndim == 3 and cfg['ZSUM'] and not cfg['PK']:
+    elif ir.ndim == 3 and cfg['ZSUM'] and not cfg['PK'] and not cfg.get('WS'):
         # star stencils: 128×32 tiles, two workgroups per CU. 512³ / one 8-GPU slab of 1024³
         # (128×1024²): 0.191 / 0.187 ms vs 0.214 / 0.208 ms with 256×32 tiles; 1024³ a tie
         cfg['CX'] = 2
@@ -61,9 +67,9 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             k, v = kv.split('=')
             over[k.strip()] = v.strip() if k.strip() == 'VIEW2D' else int(v)
     for k, v in over.items():
-        if k in ('CX', 'WX', 'NR', 'PD', 'WAVES', 'LDS_PAD', 'ZCT', 'ZMIN', 'ZMAX', 'BLK'):
+        if k in ('CX', 'WX', 'NR', 'PD', 'WAVES', 'LDS_PAD', 'ZCT', 'ZMIN', 'ZMAX', 'BLK', 'D'):
             cfg[k] = int(v)
-        elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'LAZY', 'ZSUM', 'PK', 'ZU', 'PX', 'FASTLOAD'):
+        elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'LAZY', 'ZSUM', 'PK', 'ZU', 'PX', 'FASTLOAD', 'WS'):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
         elif k == 'VIEW2D':
             cfg[k] = str(v)
@@ -81,9 +87,17 @@ def default_march_config(ir, ve, shape=None, tuning=None):
         if 'NR' not in over:
             while cfg['NR'] > 1 and (4 // cfg['WX']) * cfg['NR'] // 2 >= ny:
                 cfg['NR'] //= 2
-    # LDS budget: two workgroups per CU (≤ 80 KB) for the defaults, the 160 KB hardware limit always
-    budget = 80 * 1024 if not ('CX' in over or 'NR' in over) else 160 * 1024
-    while march_geometry(ir, MarchConfig(VE=ve, **cfg))['lds_bytes'] > budget and (cfg['NR'] > 1 or cfg['CX'] > 1):
+    # LDS budget: two workgroups per CU (≤ 80 KB) for the register-prefetch defaults, the 160 KB hardware
+    # limit for the LDS-DMA ring and for explicit tile overrides
+    budget = 80 * 1024 if not ('CX' in over or 'NR' in over or cfg.get('WS')) else 160 * 1024
+
+    def lds(c):
+        mc = MarchConfig(VE=ve, **c)
+        ws = ws_geometry(ir, mc)
+        return ws['lds_bytes'] if ws else march_geometry(ir, mc)['lds_bytes']
+    while cfg.get('WS') and cfg.get('D', 3) > 1 and lds(cfg) > 160 * 1024:
+        cfg['D'] = cfg.get('D', 3) - 1                          # fewer planes in flight before smaller tiles
+    while lds(cfg) > budget and (cfg['NR'] > 1 or cfg['CX'] > 1):
         if cfg['NR'] >= cfg['CX'] and cfg['NR'] > 1:
             cfg['NR'] //= 2
         else:
@@ -237,7 +251,7 @@ class HipStencilKernel:
         self.last_variant = plan.variant
         if plan.grid == 0:
             return
-        rt.launch(plan.fn, (plan.grid,), (256,), plan.pack(ptrs, hptrs, scalars), stream)
+        rt.launch(plan.fn, (plan.grid,), (plan.block,), plan.pack(ptrs, hptrs, scalars), stream)
 
     def _make_plan(self, tensors, halo_list, shape, device, contiguous, force_schedule, z_range):
         torch = _torch()
@@ -261,9 +275,10 @@ class HipStencilKernel:
         fns = self.function(('pointwise',), device)
         n = int(np.prod(shape))
         aligned = all(t.data_ptr() % 32 == 0 for t in tensors)
-        from .hip_emitter import POINTWISE_UNROLL
-        per_block = 256 * (4 * POINTWISE_UNROLL if aligned else 1)
-        blocks = max(1, min(math.ceil(n / per_block), 256 * 8 if aligned else 256 * 16))
+        from . import hip_emitter as he
+        per_block = 256 * (4 * he.POINTWISE_UNROLL if aligned else 1)
+        cap = (he.POINTWISE_MAX_BLOCKS or 2 ** 31 - 1) if aligned else 256 * 16
+        blocks = max(1, min(math.ceil(n / per_block), cap))
         kinds = ['ptr'] * len(tensors) + ['i64'] + [self._scalar_kind()] * len(self.ir.scalars)
         return _Plan(('pointwise', 'v4' if aligned else 'v1'), fns['v4' if aligned else 'v1'], blocks, kinds,
                      len(tensors), 0, [n])
@@ -358,11 +373,15 @@ class HipStencilKernel:
                                      "on the field's device")
         if max(geo['Z'], geo['Y'], geo['X']) >= 2 ** 31 or grid >= 2 ** 31:
             raise ValueError('field extent too large for the march schedule')
+        ws = ws_geometry(ir, cfg)
+        if ws and geo['Y'] * geo['X'] * ws['esize'] >= 2 ** 31 - 1024:
+            raise ValueError('plane too large for the LDS-DMA loader (32-bit buffer offsets)')
         statics = [int(geo[k]) for k in ('Z', 'Y', 'X', 'zlo', 'zhi', 'ylo', 'yhi', 'xlo', 'xhi', 'zc', 'zstep', 'ntx',
                                           'nty')]
         kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics) + \
             [self._scalar_kind()] * len(ir.scalars)
-        return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics)
+        return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics,
+                     block=ws['block'] if ws else 256)
 
 
 def _is_pair(z_range):
@@ -381,11 +400,12 @@ class _Plan:
 
     _CODES = {'ptr': ('Q', 8), 'i32': ('i', 4), 'i64': ('q', 8), 'f32': ('f', 4), 'f64': ('d', 8)}
 
-    def __init__(self, variant, fn, grid, kinds, n_ptr, n_halo, statics):
+    def __init__(self, variant, fn, grid, kinds, n_ptr, n_halo, statics, block=256):
         import struct
         self.variant = variant
         self.fn = fn
         self.grid = grid
+        self.block = block
         fmt, off = '<', 0
         for k in kinds:
             c, size = self._CODES[k]

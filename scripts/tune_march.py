@@ -107,10 +107,11 @@ def main():
     from pystencils_autodiff_amd.backends import hip_emitter as _he
     cu, co = _ps.fields(f"cu, co: {str(u.dtype).replace('torch.', '')}[{len(shape)}d]")
     alg = 2 * esize * cells
-    for nt_load in (False, True):
+    for nt_load, maxb in ((False, 2048), (True, 2048), (False, 0), (True, 0)):
         _he.POINTWISE_NT_LOAD = nt_load
+        _he.POINTWISE_MAX_BLOCKS = maxb
         ck = StencilKernel(_ps.AssignmentCollection({co.center: cu.center}),
-                           function_name=f'tunecopy{int(nt_load)}', target='gpu').compile()
+                           function_name=f'tunecopy{int(nt_load)}{maxb}', target='gpu').compile()
         ck(cu=u, co=out)
         pt = []
         for _ in range(a.rounds):
@@ -123,9 +124,23 @@ def main():
             torch.cuda.synchronize()
             pt.append(e0.elapsed_time(e1) / a.reps)
         pmed = sorted(pt)[len(pt) // 2]
-        print(f"pointwise copy{' (nt loads)' if nt_load else ''}: median {pmed:.4f} ms = "
+        print(f"pointwise copy{' (nt loads)' if nt_load else ''}{' one pass' if not maxb else ''}: median {pmed:.4f} ms = "
               f"{alg / (pmed * 1e-3) / 1e9:.0f} GB/s")
-    _he.POINTWISE_NT_LOAD = False
+    _he.POINTWISE_NT_LOAD = True
+    _he.POINTWISE_MAX_BLOCKS = 0
+    # torch's own vectorised elementwise kernel (read + write of the same bytes) for reference
+    mt = []
+    for _ in range(a.rounds):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.reps):
+            torch.mul(u, 1.5, out=out)
+        e1.record()
+        torch.cuda.synchronize()
+        mt.append(e0.elapsed_time(e1) / a.reps)
+    mmed = sorted(mt)[len(mt) // 2]
+    print(f"torch.mul (elementwise): median {mmed:.4f} ms = {alg / (mmed * 1e-3) / 1e9:.0f} GB/s")
     print(f"copy_: median {sorted(ct)[len(ct) // 2]:.4f} ms = {alg / (sorted(ct)[len(ct) // 2] * 1e-3) / 1e9:.0f} GB/s")
     for i, c in enumerate(cfgs):
         ts = sorted(times[i])

@@ -506,3 +506,80 @@ def test_radius2_stencils_vs_oracle(case, params, bh):
             assert not k.last_variant[1].ZSUM
         for n, t in outs.items():
             assert_close_rel(t.cpu().numpy(), ref[n], 1e-6, f'{name} {which} {n}')
+
+
+def _ws_cases():
+    u, v, out = ps.fields("u, v, out: float32[3d]")
+    mixed = ps.AssignmentCollection({out.center: 0.3 * u[1, 1, -1] - 0.2 * u[-1, 0, 1] + 0.5 * u[0, 1, 0]
+                                     + sp.sin(u.center) * v.center + 0.1 * v[0, 0, 1]})
+    two = ps.AssignmentCollection({out.center: 0.3 * u[1, 0, 0] - 0.2 * v[-1, 0, 1] + 0.5 * u[0, -1, 0]
+                                   + 0.25 * v[0, 1, 0] - u.center})
+    return [('7pt', W.diffusion_7pt, np.float32), ('asym', W.asym_7pt, np.float32),
+            ('27pt_f32', lambda: W.stencil_27pt(dtype='float32'), np.float32), ('mixed', lambda: mixed, np.float32),
+            ('two_fields', lambda: two, np.float32), ('7pt_f64', lambda: W.diffusion_7pt(dtype='float64'), np.float64)]
+
+
+@pytest.mark.parametrize('params', [dict(ZSUM=True, WS=True), dict(ZSUM=True, WS=True, D=1, CX=1, NR=3, ZC=5),
+                                    dict(ZSUM=True, WS=True, D=2, CX=2, WX=2, NR=2, ZC=4),
+                                    dict(ZSUM=True, WS=True, D=4, CX=4, NR=4, ZC=6),
+                                    dict(ZSUM=True, WS=True, PK=True, CX=2, NR=3, ZC=7),
+                                    dict(ZSUM=True, WS=True, D=3, CX=2, NR=8, ZC=64)])
+@pytest.mark.parametrize('shape', [(12, 35, 72), (7, 29, 520), (4, 5, 8), (9, 3, 264)])
+@pytest.mark.parametrize('case', _ws_cases(), ids=lambda c: c[0])
+def test_ws_loader_schedule_vs_oracle(params, shape, case):
+    """Warp-specialised zsum: LDS-DMA loader wave, counted vmcnt ring, hardware zero fill at the
+    domain edge (out-of-range pieces, absent halo planes) — forward and adjoint vs the oracle."""
+    from pystencils_autodiff_amd.backends.hip_emitter import ws_geometry
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    name, builder, dt = case
+    op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
+    rng = np.random.default_rng(sum(shape))
+    arrays = {f.name: rng.uniform(-1, 1, shape).astype(dt) for f in op.forward_input_fields}
+    arrays.update({f.name: rng.uniform(-1, 1, shape).astype(dt) for f in op.backward_input_fields
+                   if f.name not in arrays})
+    for which, ac in (('f', op.forward_assignments), ('b', op.backward_assignments)):
+        k = StencilKernel(ac, boundary_handling='zeros', function_name=f'ws_{which}', target='gpu',
+                          gpu_indexing_params=params).compile()
+        ins = {f.name: arrays[f.name] for f in k.ir.fields_read}
+        ref = OE.evaluate(ac, ins, boundary_handling='zeros')
+        outs = {f.name: torch.full(shape, float('nan'), dtype=getattr(torch, np.dtype(dt).name), device='cuda')
+                for f in k.ir.fields_written}
+        k(**{n: torch.from_numpy(a).cuda() for n, a in ins.items()}, **outs)
+        torch.cuda.synchronize()
+        cfg = k.last_variant[1]
+        assert k.last_variant[0] == 'march' and cfg.ZSUM
+        if not (params.get('PK') and dt == np.float64):
+            assert ws_geometry(k.ir, cfg) is not None, cfg
+        for n, t in outs.items():
+            assert_close_rel(t.cpu().numpy(), ref[n], TOL[dt], f'{name} {which} {n} {params}')
+
+
+@pytest.mark.parametrize('params', [dict(), dict(ZSUM=True, WS=True, D=2, CX=1, NR=2, ZC=3),
+                                    dict(ZSUM=True, WS=True, D=4, CX=2, NR=4)])
+def test_ws_halos_and_two_range_launches(params):
+    """z-slab launch pattern through the LDS-DMA loader: halo planes read in place by the DMA,
+    interior planes first, both faces in one two-range launch == one full-domain launch, bitwise."""
+    from pystencils_autodiff_amd.backends.hip_emitter import ws_geometry
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    op = pa.AutoDiffOp(W.asym_7pt(), boundary_handling='zeros')
+    k = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='wsh', target='gpu',
+                      gpu_indexing_params=params).compile()
+    g = torch.Generator().manual_seed(5)
+    u = torch.rand((30, 21, 136), generator=g).cuda()
+    full = torch.empty_like(u)
+    k(u=u, out=full)
+    assert ws_geometry(k.ir, k.last_variant[1]) is not None
+    parts = [(0, 11), (11, 19), (19, 30)]
+    outs = []
+    for a, b in parts:
+        sl = u[a:b].contiguous()
+        out = torch.full_like(sl, float('nan'))
+        lo = u[a - 1:a].contiguous() if a > 0 else None
+        hi = u[b:b + 1].contiguous() if b < 30 else None
+        k(u=sl, out=out, z_range=(1, b - a - 1))
+        k(u=sl, out=out, halos={'u': (lo, hi)}, z_range=((0, 1), (b - a - 1, b - a)))
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(outs), full)
+    ref = S.linear_stencil(u.cpu().numpy(), S.taps_asym_7pt())
+    assert_close_rel(full.cpu().numpy(), ref, 1e-6)

@@ -113,6 +113,32 @@ def test_zsum_packed_and_unrolled_variants_compile():
     assert re.search(r'a0_\d_p0_0 = a0_\d_p0_0 \+ \(', src)
 
 
+def test_ws_loader_variants_compile():
+    """Warp-specialised zsum (LDS-DMA loader wave): the measured default for star stencils in fp32 /
+    fp64, counted vmcnt waits within the 6-bit counter, compiles for gfx950; not used for fp16 storage."""
+    from pystencils_autodiff_amd.backends.hip_emitter import ws_geometry
+    op = pa.AutoDiffOp(W.diffusion_7pt(), boundary_handling='zeros')
+    k = op.forward_ast_gpu.compile()
+    cfg = k._march_cfg(4, (1024, 1024, 1024))
+    assert cfg.ZSUM and cfg.WS and cfg.D == 4 and (cfg.TX, cfg.TY) == (256, 16)
+    ws = ws_geometry(k.ir, cfg)
+    assert ws['block'] == 320 and ws['lds_bytes'] <= 160 * 1024
+    for c in (cfg, MarchConfig(VE=4, CX=1, NR=3, ZSUM=True, WS=True, D=1),
+              MarchConfig(VE=4, CX=2, WX=2, NR=2, ZSUM=True, WS=True, D=2, PK=True)):
+        src, name = k.source(('march', c))
+        assert '__builtin_amdgcn_raw_ptr_buffer_load_lds' in src and 'if (wave == 4)' in src
+        waits = [int(v) for v in re.findall(r'vmcnt\((\d+)\)', src)]
+        assert waits and max(waits) <= 63
+        code = rt.compile_hip(src)
+        assert _is_amdgpu_elf(code) and name.encode() in code
+    two = pa.AutoDiffOp(W.asym_7pt(), boundary_handling='zeros').backward_ast_gpu
+    assert ws_geometry(two.ir, MarchConfig(VE=4, CX=4, NR=8, ZSUM=True, WS=True, D=4))['D'] <= 4
+    op27 = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')       # fp16 storage: register path
+    k27 = op27.forward_ast_gpu.compile()
+    assert ws_geometry(k27.ir, MarchConfig(VE=8, CX=2, NR=4, ZSUM=True, WS=True)) is None
+    assert not k27.primary_variant()[1].WS
+
+
 def test_pack_args_alignment():
     buf = rt.pack_args([('ptr', 0x1000), ('i32', 7), ('i64', 9), ('f32', 1.5), ('f64', 2.0), ('i32', 3)])
     assert len(buf) % 8 == 0
