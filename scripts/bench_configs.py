@@ -85,6 +85,45 @@ def run(name, builder, shape, dtype, bh, nin, steps=20, warmup=3, bytes_fwd=None
     torch.cuda.empty_cache()
 
 
+def run_slab(name, builder, shape, dtype, full_cells, steps=20, warmup=3):
+    """One rank's share of a z-slab decomposed step WITHOUT the exchange: interior planes, then both
+    faces in one two-range launch reading halo planes, for the forward and the adjoint kernel — the
+    per-rank compute time of the N-GPU run (zslab.py launch pattern)."""
+    import torch
+
+    import pystencils_autodiff_amd as pa
+    op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
+    ks = [op.forward_ast_gpu.compile(), op.backward_ast_gpu.compile()]
+    g = torch.Generator(device='cuda').manual_seed(0)
+    args = []
+    for k in ks:
+        kw = {f.name: (torch.rand(shape, generator=g, device='cuda') * 2 - 1).to(dtype) for f in k.ir.fields}
+        halos = {f.name: (kw[f.name][:1].clone(), kw[f.name][-1:].clone()) for f in k.ir.stencil_fields}
+        args.append((k, kw, halos))
+    Z = shape[0]
+
+    def step():
+        for k, kw, halos in args:
+            k(z_range=(1, Z - 1), **kw)
+            k(halos=halos, z_range=((0, 1), (Z - 1, Z)), **kw)
+    for _ in range(warmup):
+        step()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(steps):
+        step()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    res = {'config': name, 'shape': list(shape), 'dtype': str(dtype).replace('torch.', ''),
+           'ms_per_step_rank_compute': round(ms, 4),
+           'implied_full_domain_mcells_per_s_no_exchange': round(full_cells / (ms * 1e-3) / 1e6, 1),
+           'schedule': ks[0].last_variant[0] + ('/ws' if getattr(ks[0].last_variant[1], 'WS', False) else '')}
+    print(json.dumps(res))
+    sys.stdout.flush()
+
+
 def main():
     import torch
 
@@ -103,6 +142,13 @@ def main():
         if only and name not in only:
             continue
         run(name, b, shape, dt, bh, nin, bytes_fwd=bf, bytes_bwd=bb)
+    slabs = [('slab8_diffusion7_f32_128x1024^2', lambda: W.diffusion_7pt(), (128, 1024, 1024), torch.float32, 1024 ** 3),
+             ('slab4_diffusion7_f32_256x1024^2', lambda: W.diffusion_7pt(), (256, 1024, 1024), torch.float32, 1024 ** 3),
+             ('slab8_stencil27_f16_96x768^2', lambda: W.stencil_27pt(), (96, 768, 768), torch.float16, 768 ** 3)]
+    for name, b, shape, dt, cells in slabs:
+        if only and name not in only:
+            continue
+        run_slab(name, b, shape, dt, cells)
 
 
 if __name__ == '__main__':

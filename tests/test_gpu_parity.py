@@ -516,7 +516,8 @@ def _ws_cases():
                                    + 0.25 * v[0, 1, 0] - u.center})
     return [('7pt', W.diffusion_7pt, np.float32), ('asym', W.asym_7pt, np.float32),
             ('27pt_f32', lambda: W.stencil_27pt(dtype='float32'), np.float32), ('mixed', lambda: mixed, np.float32),
-            ('two_fields', lambda: two, np.float32), ('7pt_f64', lambda: W.diffusion_7pt(dtype='float64'), np.float64)]
+            ('two_fields', lambda: two, np.float32), ('7pt_f64', lambda: W.diffusion_7pt(dtype='float64'), np.float64),
+            ('27pt_f16', W.stencil_27pt, np.float16), ('asym_f16', lambda: W.asym_7pt(dtype='float16'), np.float16)]
 
 
 @pytest.mark.parametrize('params', [dict(ZSUM=True, WS=True), dict(ZSUM=True, WS=True, D=1, CX=1, NR=3, ZC=5),
@@ -548,7 +549,7 @@ def test_ws_loader_schedule_vs_oracle(params, shape, case):
         torch.cuda.synchronize()
         cfg = k.last_variant[1]
         assert k.last_variant[0] == 'march' and cfg.ZSUM
-        if not (params.get('PK') and dt == np.float64):
+        if not (params.get('PK') and dt == np.float64) and shape[-1] % (16 // np.dtype(dt).itemsize) == 0:
             assert ws_geometry(k.ir, cfg) is not None, cfg
         for n, t in outs.items():
             assert_close_rel(t.cpu().numpy(), ref[n], TOL[dt], f'{name} {which} {n} {params}')

@@ -133,10 +133,15 @@ def test_ws_loader_variants_compile():
         assert _is_amdgpu_elf(code) and name.encode() in code
     two = pa.AutoDiffOp(W.asym_7pt(), boundary_handling='zeros').backward_ast_gpu
     assert ws_geometry(two.ir, MarchConfig(VE=4, CX=4, NR=8, ZSUM=True, WS=True, D=4))['D'] <= 4
-    op27 = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')       # fp16 storage: register path
+    op27 = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')       # fp16 storage: converting loader
     k27 = op27.forward_ast_gpu.compile()
-    assert ws_geometry(k27.ir, MarchConfig(VE=8, CX=2, NR=4, ZSUM=True, WS=True)) is None
-    assert not k27.primary_variant()[1].WS
+    c27 = MarchConfig(VE=8, CX=2, WX=2, NR=4, ZSUM=True, WS=True, PK=True)
+    ws = ws_geometry(k27.ir, c27)
+    assert ws['kind'] == 'reg' and ws['NS'] == 2
+    src, name = k27.source(('march', c27))
+    assert '__builtin_amdgcn_raw_buffer_load_b128' in src and 'if (wave == 4)' in src
+    assert _is_amdgpu_elf(rt.compile_hip(src))
+    assert ws_geometry(k27.ir, MarchConfig(VE=1, CX=2, NR=4, ZSUM=True, WS=True)) is None   # unaligned
 
 
 def test_pack_args_alignment():
