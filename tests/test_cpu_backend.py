@@ -153,3 +153,19 @@ def test_readme_op_cpu_backend_fp32_golden():
     assert_close_rel(y.grad.numpy(), g['diffy'], 1e-6, 'diffy')
     # the reference interior-only semantics: boundary_handling=None and offset-free -> every cell written
     assert op.forward_ast_cpu.ir.ghost_layers == 0
+
+
+@pytest.mark.parametrize('radius', (1, 2, 3))
+def test_fixed_constant_bh_one_sided_box_cpu(radius):
+    """tests/test_fixed_constant_bh.py:22-48 of the reference on the CPU backend, checked against the oracle."""
+    import itertools
+    x, y = ps.fields("x, y: float64[2d]")
+    offs = list(itertools.product(range(radius + 1), repeat=2))
+    ac = ps.AssignmentCollection({y.center: sp.Add(*[x[o] for o in offs]) / len(offs)})
+    xv = np.random.default_rng(radius).random((20, 30))
+    for bh in ('zeros', None):
+        op = pa.AutoDiffOp(ac, boundary_handling=bh)
+        fn = op.create_tensorflow_op(use_cuda=False, backend='torch_native')
+        (out,) = fn.apply(torch.from_numpy(xv))
+        ref = OE.evaluate(op.forward_assignments, {'x': xv}, boundary_handling=bh)['y']
+        assert_close_rel(out.numpy(), ref, 1e-12, f'{bh}')

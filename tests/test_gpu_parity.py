@@ -584,3 +584,29 @@ def test_ws_halos_and_two_range_launches(params):
     assert torch.equal(torch.cat(outs), full)
     ref = S.linear_stencil(u.cpu().numpy(), S.taps_asym_7pt())
     assert_close_rel(full.cpu().numpy(), ref, 1e-6)
+
+
+@pytest.mark.parametrize('radius', (1, 2, 3))
+@pytest.mark.parametrize('ndim', (2, 3))
+def test_fixed_constant_bh_one_sided_box(radius, ndim):
+    """Mirror of the reference's tests/test_fixed_constant_bh.py:22-48: a one-sided box mean filter
+    (offsets 0..r per axis) with 'zeros' boundary handling (ghost_layers=0) and without (interior
+    only), float64 — forward and adjoint through the drop-in op vs the oracle; both agree inside."""
+    x, y = ps.fields(f"x, y: float64[{ndim}d]")
+    offs = list(itertools.product(range(radius + 1), repeat=ndim))
+    ac = ps.AssignmentCollection({y.center: sp.Add(*[x[o] for o in offs]) / len(offs)})
+    shape = (20, 30, 40)[:ndim]
+    rng = np.random.default_rng(radius)
+    xv = rng.random(shape)
+    dv = rng.uniform(-1, 1, shape)
+    res = {}
+    for bh in ('zeros', None):
+        op, fn = _op(ac, bh)
+        (out,), (dx,) = _run(fn, [xv], [dv])
+        ref = OE.evaluate(op.forward_assignments, {'x': xv}, boundary_handling=bh)['y']
+        refb = OE.evaluate(op.backward_assignments, {'diffy': dv}, boundary_handling=bh)['diffx']
+        assert_close_rel(out, ref, 1e-12, f'{bh} forward')
+        assert_close_rel(dx, refb, 1e-12, f'{bh} adjoint')
+        res[bh] = out
+    inner = tuple(slice(radius, s - radius) for s in shape)
+    np.testing.assert_allclose(res['zeros'][inner], res[None][inner], rtol=0, atol=1e-12)
