@@ -90,7 +90,8 @@ def test_zsum_eligibility():
     assert not k.primary_variant()[1].ZSUM
     op27 = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
     plan = zsum_plan(op27.forward_ast_gpu.ir, MarchConfig())
-    assert sorted(plan[0]['lin']) == [-1, 1] and len(plan[0]['lin'][1]) == 9
+    assert sorted(plan[0]['lin']) == [-1, 0, 1] and all(len(plan[0]['lin'][dz]) == 9 for dz in (-1, 0, 1))
+    assert plan[0]['rest'] == 0                                   # every centre-plane tap is a packed FMA too
 
 
 def test_zsum_packed_and_unrolled_variants_compile():
