@@ -42,7 +42,9 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             # vs 0.469 scalar WX=1 vs 0.70 ms LDS ring; unrolling the plane loop 3x is slower (0.53-0.56)
             # chunks of 16..32 planes, ~2048 workgroups: 768³ 32 planes; one 8-GPU slab (96×768²) 16
             # planes, 0.067 vs 0.073 ms at 32
-            cfg.update(CX=2, WX=2, NR=4, ZSUM=True, PK=True, ZMIN=16, ZMAX=32, BLK=2048)
+            # tap pairs by inline-asm ds_read2_b32 (AR): 0.421 vs 0.459 ms at 768³, 0.062 vs 0.067 ms per
+            # 8-GPU slab (profiles/r01_tune_27pt_ar.log) — the compiler's adjacent-x merges cost 26 v_mov
+            cfg.update(CX=2, WX=2, NR=4, ZSUM=True, PK=True, AR=True, ZMIN=16, ZMAX=32, BLK=2048)
         else:
             cfg.update(CX=2, NR=4)                             # box stencil: full ring, LDS/VALU bound
     elif ir.ndim == 3 and zsum_ok:
@@ -69,7 +71,7 @@ def default_march_config(ir, ve, shape=None, tuning=None):
     for k, v in over.items():
         if k in ('CX', 'WX', 'NR', 'PD', 'WAVES', 'LDS_PAD', 'ZCT', 'ZMIN', 'ZMAX', 'BLK', 'D'):
             cfg[k] = int(v)
-        elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'LAZY', 'ZSUM', 'PK', 'ZU', 'PX', 'FASTLOAD', 'WS'):
+        elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'LAZY', 'ZSUM', 'PK', 'ZU', 'PX', 'FASTLOAD', 'WS', 'AR'):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
         elif k == 'VIEW2D':
             cfg[k] = str(v)

@@ -332,7 +332,9 @@ def _zsum_cases():
                                     dict(ZSUM=True, CX=4, NR=8, NT_STORE=True), dict(ZSUM=True, WX=2, CX=2, NR=2),
                                     dict(ZSUM=True, PK=True, CX=2, NR=3, ZC=7),
                                     dict(ZSUM=True, ZU=True, CX=2, NR=2, ZC=5),
-                                    dict(ZSUM=True, PK=True, ZU=True, WX=2, CX=4, NR=2, ZC=4)])
+                                    dict(ZSUM=True, PK=True, ZU=True, WX=2, CX=4, NR=2, ZC=4),
+                                    dict(ZSUM=True, PK=True, AR=True, CX=2, NR=3, ZC=7),
+                                    dict(ZSUM=True, PK=True, AR=True, WX=2, CX=4, NR=2, ZC=4)])
 @pytest.mark.parametrize('case', _zsum_cases(), ids=lambda c: c[0])
 @pytest.mark.parametrize('bh', ['zeros', None])
 def test_zsum_schedule_vs_oracle(params, case, bh):
@@ -363,6 +365,7 @@ def test_zsum_schedule_vs_oracle(params, case, bh):
 
 
 @pytest.mark.parametrize('params', [dict(ZSUM=True, CX=1, NR=2, ZC=4), dict(ZSUM=True, CX=2, NR=2, PK=True, PX=True),
+                                    dict(ZSUM=True, CX=2, WX=2, NR=4, PK=True, AR=True),
                                     dict(ZSUM=True, CX=2, WX=2, NR=1, PK=True, PX=True, ZC=3),
                                     dict(ZSUM=True, CX=2, NR=2, FASTLOAD=False), dict(ZSUM=False, CX=1, NR=2)])
 @pytest.mark.parametrize('case', _zsum_cases(), ids=lambda c: c[0])
@@ -524,7 +527,8 @@ def _ws_cases():
                                     dict(ZSUM=True, WS=True, D=2, CX=2, WX=2, NR=2, ZC=4),
                                     dict(ZSUM=True, WS=True, D=4, CX=4, NR=4, ZC=6),
                                     dict(ZSUM=True, WS=True, PK=True, CX=2, NR=3, ZC=7),
-                                    dict(ZSUM=True, WS=True, D=3, CX=2, NR=8, ZC=64)])
+                                    dict(ZSUM=True, WS=True, D=3, CX=2, NR=8, ZC=64),
+                                    dict(ZSUM=True, WS=True, PK=True, AR=True, CX=2, WX=2, NR=4, ZC=5)])
 @pytest.mark.parametrize('shape', [(12, 35, 72), (7, 29, 520), (4, 5, 8), (9, 3, 264)])
 @pytest.mark.parametrize('case', _ws_cases(), ids=lambda c: c[0])
 def test_ws_loader_schedule_vs_oracle(params, shape, case):

@@ -98,15 +98,17 @@ def test_zsum_packed_and_unrolled_variants_compile():
     op27 = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
     k = op27.forward_ast_gpu.compile()
     default = k.primary_variant()[1]
-    assert default.ZSUM and default.PK and default.WX == 2        # measured default for box stencils
+    assert default.ZSUM and default.PK and default.AR and default.WX == 2   # measured default for box stencils
     for cfg in (MarchConfig(VE=8, CX=2, NR=4, ZSUM=True, PK=True),
                 MarchConfig(VE=8, CX=2, NR=4, ZSUM=True, PK=True, PX=True),
                 MarchConfig(VE=8, CX=2, NR=4, ZSUM=True, FASTLOAD=False),
                 MarchConfig(VE=8, CX=2, NR=4, ZSUM=True, PK=True, ZU=True),
+                MarchConfig(VE=8, CX=2, WX=2, NR=4, ZSUM=True, PK=True, AR=True),
                 MarchConfig(VE=8, CX=3, NR=2, ZSUM=True, PK=True)):       # odd CX: scalar fallback
         src, name = k.source(('march', cfg))
         assert ('f32x2 a0_' in src) == (cfg.PK and cfg.CX % 2 == 0)
         assert ('p0 += 3' in src) == cfg.ZU                              # 2*RZ+1 phases, renamed accumulators
+        assert ('ds_read2_b32 %0' in src) == (cfg.AR and cfg.CX % 2 == 0)   # paired taps by inline asm
         code = rt.compile_hip(src)
         assert _is_amdgpu_elf(code) and name.encode() in code
     # every off-centre tap is one fused multiply-add into its accumulator
