@@ -131,6 +131,7 @@ def main():
     only = sys.argv[1:]
     cfgs = [
         ('readme_op_f32_20x30', W.readme_op, (20, 30), torch.float32, None, 2, 12, 20),
+        ('readme_op_f32_16384^2', lambda: W.readme_op(shape=None), (16384, 16384), torch.float32, None, 2, 12, 20),
         ('laplace5_f32_4096^2', lambda: W.laplace_5pt(), (4096, 4096), torch.float32, 'zeros', 1, 8, 8),
         ('diffusion7_f32_512^3', lambda: W.diffusion_7pt(), (512, 512, 512), torch.float32, 'zeros', 1, 8, 8),
         ('diffusion7_f32_1024^3', lambda: W.diffusion_7pt(), (1024, 1024, 1024), torch.float32, 'zeros', 1, 8, 8),
