@@ -528,7 +528,9 @@ def _ws_cases():
                                     dict(ZSUM=True, WS=True, D=4, CX=4, NR=4, ZC=6),
                                     dict(ZSUM=True, WS=True, PK=True, CX=2, NR=3, ZC=7),
                                     dict(ZSUM=True, WS=True, D=3, CX=2, NR=8, ZC=64),
-                                    dict(ZSUM=True, WS=True, PK=True, AR=True, CX=2, WX=2, NR=4, ZC=5)])
+                                    dict(ZSUM=True, WS=True, PK=True, AR=True, CX=2, WX=2, NR=4, ZC=5),
+                                    dict(ZSUM=True, WS=True, WSD=True, PK=True, AR=True, CX=2, WX=2, NR=4, D=3),
+                                    dict(ZSUM=True, WS=True, WSD=True, D=2, CX=1, NR=3, ZC=5)])
 @pytest.mark.parametrize('shape', [(12, 35, 72), (7, 29, 520), (4, 5, 8), (9, 3, 264)])
 @pytest.mark.parametrize('case', _ws_cases(), ids=lambda c: c[0])
 def test_ws_loader_schedule_vs_oracle(params, shape, case):
