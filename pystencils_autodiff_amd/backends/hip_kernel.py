@@ -360,6 +360,10 @@ class HipStencilKernel:
         cfg = self._march_cfg(ve if aligned else 1, shape)
         if halo_list and ir.ndim == 2 and cfg.VIEW2D == 'yx':
             cfg = MarchConfig(**{**cfg.__dict__, 'VIEW2D': 'zy'})
+        ws = ws_geometry(ir, cfg)
+        if ws and int(np.prod(shape[1:])) * max(ws['esize'], ws.get('ssize', 0)) >= 2 ** 31 - 1024:
+            # planes beyond the loader's 32-bit buffer offsets: register-prefetch form of the same schedule
+            cfg = MarchConfig(**{**cfg.__dict__, 'WS': False})
         variant = ('march', cfg)
         fn = self.function(variant, device)
         geo = self.march_launch_geometry(shape, cfg, z_range)
@@ -376,8 +380,6 @@ class HipStencilKernel:
         if max(geo['Z'], geo['Y'], geo['X']) >= 2 ** 31 or grid >= 2 ** 31:
             raise ValueError('field extent too large for the march schedule')
         ws = ws_geometry(ir, cfg)
-        if ws and geo['Y'] * geo['X'] * ws['esize'] >= 2 ** 31 - 1024:
-            raise ValueError('plane too large for the LDS-DMA loader (32-bit buffer offsets)')
         statics = [int(geo[k]) for k in ('Z', 'Y', 'X', 'zlo', 'zhi', 'ylo', 'yhi', 'xlo', 'xhi', 'zc', 'zstep', 'ntx',
                                           'nty')]
         kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics) + \
