@@ -169,3 +169,30 @@ def test_fixed_constant_bh_one_sided_box_cpu(radius):
         (out,) = fn.apply(torch.from_numpy(xv))
         ref = OE.evaluate(op.forward_assignments, {'x': xv}, boundary_handling=bh)['y']
         assert_close_rel(out.numpy(), ref, 1e-12, f'{bh}')
+
+
+def test_tfmad_two_outputs_vector_field_cpu():
+    """tests/test_tfmad.py:353-401 of the reference (curl into a vector field) on the CPU backend, with the
+    symbolic adjoint checked term by term and the dot-product identity."""
+    inp = ps.Field.create_fixed_size(field_name='curl_input', shape=(20, 30), index_dimensions=0)
+    u = ps.Field.create_fixed_size(field_name='curl', shape=(20, 30, 2), index_dimensions=1)
+    disc = ps.fd.Discretization2ndOrder(dx=1)
+    ac = ps.AssignmentCollection([ps.Assignment(u.center(0), disc(ps.fd.Diff(inp, 0))),
+                                  ps.Assignment(u.center(1), disc(ps.fd.Diff(inp, 1)))], [])
+    op = pa.AutoDiffOp(ac, diff_mode='transposed-forward', boundary_handling='zeros')
+    (bw,) = op.backward_assignments.main_assignments
+    dc = op.backward_output_fields[0]
+    assert bw.lhs == dc.center
+    g_ = [f for f in op.backward_input_fields if f.name == 'diffcurl'][0]
+    expected = sp.Rational(1, 2) * (g_[-1, 0](0) - g_[1, 0](0) + g_[0, -1](1) - g_[0, 1](1))
+    assert sp.simplify(sp.expand(bw.rhs) - sp.expand(expected)) == 0
+    fn = op.create_tensorflow_op(use_cuda=False, backend='torch_native')
+    rng = np.random.default_rng(4)
+    x = torch.from_numpy(rng.uniform(-1, 1, (20, 30))).requires_grad_(True)
+    g = torch.from_numpy(rng.uniform(-1, 1, (20, 30, 2)))
+    (c,) = fn.apply(x)
+    c.backward(g)
+    cg = float((c.detach() * g).sum())
+    assert abs(cg - float((x.detach() * x.grad).sum())) < 1e-10 * float((c.detach() * g).abs().sum())
+    ref = OE.evaluate(op.forward_assignments, {'curl_input': x.detach().numpy()}, boundary_handling='zeros')['curl']
+    assert_close_rel(c.detach().numpy(), ref, 1e-12, 'curl')

@@ -638,3 +638,32 @@ def test_degenerate_and_empty_shapes(shape, case):
     tol = TOL[dt]
     assert_close_rel(out, ref, tol, f'{name} forward {shape}')
     assert_close_rel(du, refb, tol, f'{name} adjoint {shape}')
+
+
+def _curl_op(bh):
+    """tests/test_tfmad.py:353-401 of the reference: the curl of a scalar field into a 2-component vector
+    field (fixed-size [20, 30] / [20, 30, 2]), diff_mode='transposed-forward'."""
+    inp = ps.Field.create_fixed_size(field_name='curl_input', shape=(20, 30), index_dimensions=0)
+    u = ps.Field.create_fixed_size(field_name='curl', shape=(20, 30, 2), index_dimensions=1)
+    disc = ps.fd.Discretization2ndOrder(dx=1)
+    ac = ps.AssignmentCollection([ps.Assignment(u.center(0), disc(ps.fd.Diff(inp, 0))),
+                                  ps.Assignment(u.center(1), disc(ps.fd.Diff(inp, 1)))], [])
+    return pa.AutoDiffOp(ac, diff_mode='transposed-forward', boundary_handling=bh)
+
+
+@pytest.mark.parametrize('bh', ['zeros', None])
+def test_tfmad_two_outputs_vector_field_gpu(bh):
+    op = _curl_op(bh)
+    fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    rng = np.random.default_rng(4)
+    x = rng.uniform(-1, 1, (20, 30))
+    g = rng.uniform(-1, 1, (20, 30, 2))
+    (c,), (dx,) = _run(fn, [x], [g])
+    ref = OE.evaluate(op.forward_assignments, {'curl_input': x}, boundary_handling=bh)['curl']
+    refb = OE.evaluate(op.backward_assignments, {'diffcurl': g}, boundary_handling=bh)['diffcurl_input']
+    assert_close_rel(c, ref, 1e-12, 'curl')
+    assert_close_rel(dx, refb, 1e-12, 'diffcurl_input')
+    # the adjoint is the transpose of the forward: <A x, g> == <x, A^T g> ('zeros' only: the interior-only
+    # variant leaves border cells untouched, which is not a linear map's transpose)
+    if bh == 'zeros':
+        assert abs(float(np.sum(c * g)) - float(np.sum(x * dx))) < 1e-10 * float(np.sum(np.abs(c * g)))
