@@ -74,9 +74,21 @@ class _Wrapper:
         return [_Parameter(p.symbol.name, p.field) for p in self._kernel.get_parameters()]
 
 
-def _full_write(kernel):
-    """True if the kernel writes every cell of its outputs (no untouched border)."""
-    return kernel.ir.zeros or kernel.ir.ghost_layers == 0
+def _full_write(kernel, field_name=None):
+    """True if the kernel writes every cell of its outputs (no untouched border) and, for the given output
+    (all outputs if None), every component of a vector field — else the output keeps the reference's
+    ``torch.zeros`` allocation (``_torch_native.py:64,108``)."""
+    if not (kernel.ir.zeros or kernel.ir.ghost_layers == 0):
+        return False
+    import itertools
+    for f in kernel.ir.fields_written:
+        if field_name is not None and f.name != field_name:
+            continue
+        if f.index_dimensions:
+            written = {tuple(idx) for fld, _, idx, _ in kernel.ir.stores if fld.name == f.name}
+            if written != set(itertools.product(*[range(int(n)) for n in f.index_shape])):
+                return False
+    return True
 
 
 def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
@@ -124,9 +136,12 @@ def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
     fwd_call = forward_kernel.compile()
     bwd_call = backward_kernel.compile() if backward_kernel else None
     fwd_in = [(i, f.name) for i, f in enumerate(fwd_inputs) if f.name in fwd_kernel_fields]
-    fwd_out = [(f.name, _tdtype(f), _fixed(f)) for f in fwd_outputs]
+    def _index_shape(field):
+        return tuple(int(n) for n in field.index_shape) if field.index_dimensions else ()
+
+    fwd_out = [(f.name, _tdtype(f), _fixed(f), torch.empty if _full_write(forward_kernel, f.name) else torch.zeros,
+                f.spatial_dimensions, _index_shape(f)) for f in fwd_outputs]
     fwd_scalars = [s.name for s in forward_kernel.ir.scalars]
-    fwd_alloc = torch.empty if _full_write(forward_kernel) else torch.zeros
     saved_fwd = [n for n in [f.name for f in fwd_inputs] + [f.name for f in fwd_outputs] if n in bwd_kernel_fields]
     if backward_kernel:
         bwd_reads = {r.field.name for r in backward_kernel.ir.reads}
@@ -137,9 +152,9 @@ def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
             grad_specs.append((a.name if a is not None and a.name in bwd_kernel_fields else None, _tdtype(f),
                                _fixed(a) if a is not None else None,
                                tuple(a.strides) if a is not None and a.has_fixed_shape else None, f.name))
-        full = _full_write(backward_kernel)
-        bwd_out = [(f.name, _tdtype(f), _fixed(f), torch.empty if full and f.name not in bwd_reads else torch.zeros)
-                   for f in bwd_outputs]
+        bwd_out = [(f.name, _tdtype(f), _fixed(f),
+                    torch.empty if _full_write(backward_kernel, f.name) and f.name not in bwd_reads else torch.zeros,
+                    f.spatial_dimensions, _index_shape(f)) for f in bwd_outputs]
         in_adj = [adj_of[f.name].name if adj_of.get(f.name) is not None else None for f in fwd_inputs]
 
     def _to_device(t):
@@ -166,8 +181,11 @@ def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
                 raise TypeError(f"{op_name}: scalar parameter '{name}' missing: set {op_name}.class_kwargs['{name}']")
             kwargs[name] = class_kwargs[name]
         outputs = []
-        for name, dtype, fixed in fwd_out:
-            t = fwd_alloc(fixed if fixed is not None else first.shape, dtype=dtype, device=first.device)
+        for name, dtype, fixed, alloc, sdim, ishape in fwd_out:
+            # variable-size outputs: the first input's spatial extent plus the output's own index shape (the
+            # reference takes the first input's whole shape, _torch_native.py:66-72)
+            t = alloc(fixed if fixed is not None else tuple(first.shape[:sdim]) + ishape, dtype=dtype,
+                      device=first.device)
             kwargs[name] = t
             outputs.append(t)
         fwd_call(**kwargs)
@@ -199,8 +217,9 @@ def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
                 kwargs[aname] = g
             like = g if like is None else like
         result = {}
-        for name, dtype, fixed, alloc in bwd_out:
-            t = alloc(fixed if fixed is not None else like.shape, dtype=dtype, device=like.device)
+        for name, dtype, fixed, alloc, sdim, ishape in bwd_out:
+            t = alloc(fixed if fixed is not None else tuple(like.shape[:sdim]) + ishape, dtype=dtype,
+                      device=like.device)
             result[name] = t
             kwargs[name] = t
         bwd_call(**kwargs)

@@ -10,7 +10,8 @@ import sympy as sp
 
 from . import ps
 
-__all__ = ['diffusion_7pt', 'laplace_5pt', 'stencil_27pt', 'readme_op', 'asym_7pt', 'WEIGHTS_27PT', 'ALPHA']
+__all__ = ['diffusion_7pt', 'laplace_5pt', 'stencil_27pt', 'readme_op', 'asym_7pt', 'vector_laplace_7pt',
+           'WEIGHTS_27PT', 'ALPHA']
 
 ALPHA = 0.1
 WEIGHTS_27PT = [(i - 13.3) / 50.0 for i in range(27)]
@@ -53,3 +54,14 @@ def readme_op(shape=(20, 30), dtype='float32'):
     """``z = x·log(x·y)`` (README.rst:52-68, BASELINE config 1)."""
     z, y, x = _fields('z, y, x', dtype, 2, shape)
     return ps.AssignmentCollection({z[0, 0]: x[0, 0] * sp.log(x[0, 0] * y[0, 0])})
+
+
+def vector_laplace_7pt(shape=None, dtype='float32', ncomp=3):
+    """Component-wise 3-D 7-point Laplacian of a vector field ``u(c)`` (index dimension, components
+    fastest in memory) — the vector-field row of SURVEY.md §8(f) (``_autodiff.py:125-152``)."""
+    spec = f"u({ncomp}), out({ncomp}): {dtype}[{','.join(str(v) for v in shape)}]" if shape else \
+        f"u({ncomp}), out({ncomp}): {dtype}[3d]"
+    u, out = ps.fields(spec)
+    nb = [(1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)]
+    return ps.AssignmentCollection({out.center(c): sp.Add(*[u[o](c) for o in nb]) - 6 * u.center(c)
+                                    for c in range(ncomp)})

@@ -63,7 +63,7 @@ def run(name, builder, shape, dtype, bh, nin, steps=20, warmup=3, bytes_fwd=None
     finally:
         torch.autograd.set_multithreading_enabled(True)
     cells = 1
-    for s in shape:
+    for s in shape[:3]:
         cells *= s
     f_ms = sorted(a.elapsed_time(b) for a, b, _ in ev)[len(ev) // 2]
     b_ms = sorted(b.elapsed_time(c) for _, b, c in ev)[len(ev) // 2]
@@ -138,6 +138,8 @@ def main():
         ('stencil27_f16_768^3', lambda: W.stencil_27pt(), (768, 768, 768), torch.float16, 'zeros', 1, 4, 4),
         ('diffusion7_f64_512^3', lambda: W.diffusion_7pt(dtype='float64'), (512, 512, 512), torch.float64,
          'zeros', 1, 16, 16),
+        ('veclaplace7_f32_384^3x3', lambda: W.vector_laplace_7pt(), (384, 384, 384, 3), torch.float32, 'zeros', 1,
+         24, 24),
     ]
     for name, b, shape, dt, bh, nin, bf, bb in cfgs:
         if only and name not in only:

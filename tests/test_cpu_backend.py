@@ -196,3 +196,36 @@ def test_tfmad_two_outputs_vector_field_cpu():
     assert abs(cg - float((x.detach() * x.grad).sum())) < 1e-10 * float((c.detach() * g).abs().sum())
     ref = OE.evaluate(op.forward_assignments, {'curl_input': x.detach().numpy()}, boundary_handling='zeros')['curl']
     assert_close_rel(c.detach().numpy(), ref, 1e-12, 'curl')
+
+
+def test_vector_field_partial_writes_and_variable_shapes_cpu():
+    """Outputs whose components are not all written keep zero-initialised components (the reference
+    allocates every output with torch.zeros, _torch_native.py:64,108); variable-size vector outputs get the
+    input's spatial extent plus their own index shape. The vector-field TF-MAD branch stores only the last
+    component's adjoint (_autodiff.py:138-152), reproduced on purpose."""
+    op = pa.AutoDiffOp(W.vector_laplace_7pt(), boundary_handling='zeros')
+    (bw,) = op.backward_assignments.main_assignments
+    assert bw.lhs.index == (2,)
+    fn = op.create_tensorflow_op(use_cuda=False, backend='torch_native')
+    rng = np.random.default_rng(2)
+    u = torch.from_numpy(rng.uniform(-1, 1, (5, 6, 7, 3)).astype(np.float32)).requires_grad_(True)
+    g = torch.from_numpy(rng.uniform(-1, 1, (5, 6, 7, 3)).astype(np.float32))
+    (o,) = fn.apply(u)
+    o.backward(g)
+    ref = OE.evaluate(op.forward_assignments, {'u': u.detach().numpy()}, boundary_handling='zeros')['out']
+    assert_close_rel(o.detach().numpy(), ref, 1e-6, 'vector laplacian')
+    assert torch.count_nonzero(u.grad[..., :2]) == 0
+    refb = OE.evaluate(op.backward_assignments, {'diffout': g.numpy()}, boundary_handling='zeros')['diffu']
+    assert_close_rel(u.grad.numpy(), refb, 1e-6, 'quirky adjoint')
+    # curl with variable-size fields: output (20, 30, 2) from a (20, 30) input
+    inp, cu = ps.fields("curl_input, curl(2): float64[2d]")
+    disc = ps.fd.Discretization2ndOrder(dx=1)
+    ac = ps.AssignmentCollection([ps.Assignment(cu.center(0), disc(ps.fd.Diff(inp, 0))),
+                                  ps.Assignment(cu.center(1), disc(ps.fd.Diff(inp, 1)))], [])
+    op2 = pa.AutoDiffOp(ac, diff_mode='transposed-forward', boundary_handling='zeros')
+    fn2 = op2.create_tensorflow_op(use_cuda=False, backend='torch_native')
+    x = torch.from_numpy(rng.uniform(-1, 1, (20, 30))).requires_grad_(True)
+    (c,) = fn2.apply(x)
+    assert tuple(c.shape) == (20, 30, 2)
+    c.backward(torch.ones_like(c))
+    assert tuple(x.grad.shape) == (20, 30)

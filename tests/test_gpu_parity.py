@@ -667,3 +667,27 @@ def test_tfmad_two_outputs_vector_field_gpu(bh):
     # variant leaves border cells untouched, which is not a linear map's transpose)
     if bh == 'zeros':
         assert abs(float(np.sum(c * g)) - float(np.sum(x * dx))) < 1e-10 * float(np.sum(np.abs(c * g)))
+
+
+def test_vector_field_partial_writes_and_variable_shapes_gpu():
+    """GPU twin of test_cpu_backend.test_vector_field_partial_writes_and_variable_shapes_cpu."""
+    op, fn = _op(W.vector_laplace_7pt())
+    rng = np.random.default_rng(2)
+    u = rng.uniform(-1, 1, (5, 6, 7, 3)).astype(np.float32)
+    g = rng.uniform(-1, 1, (5, 6, 7, 3)).astype(np.float32)
+    (o,), (du,) = _run(fn, [u], [g])
+    assert_close_rel(o, OE.evaluate(op.forward_assignments, {'u': u}, boundary_handling='zeros')['out'], 1e-6, 'fwd')
+    assert np.count_nonzero(du[..., :2]) == 0
+    refb = OE.evaluate(op.backward_assignments, {'diffout': g}, boundary_handling='zeros')['diffu']
+    assert_close_rel(du, refb, 1e-6, 'quirky adjoint')
+    inp, cu = ps.fields("curl_input, curl(2): float64[2d]")
+    disc = ps.fd.Discretization2ndOrder(dx=1)
+    ac = ps.AssignmentCollection([ps.Assignment(cu.center(0), disc(ps.fd.Diff(inp, 0))),
+                                  ps.Assignment(cu.center(1), disc(ps.fd.Diff(inp, 1)))], [])
+    op2 = pa.AutoDiffOp(ac, diff_mode='transposed-forward', boundary_handling='zeros')
+    fn2 = op2.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    x = rng.uniform(-1, 1, (20, 30))
+    (c,), (dx,) = _run(fn2, [x], [np.ones((20, 30, 2))])
+    assert c.shape == (20, 30, 2) and dx.shape == (20, 30)
+    assert_close_rel(c, OE.evaluate(op2.forward_assignments, {'curl_input': x}, boundary_handling='zeros')['curl'],
+                     1e-12, 'curl')
