@@ -153,7 +153,7 @@ class HipStencilKernel:
             elif kind == 'march':
                 src = emit_march(self.ir, kname, variant[1])
             else:
-                src = emit_generic(self.ir, kname)
+                src = emit_generic(self.ir, kname, idx32='idx32' in variant[1:], contig='contig' in variant[1:])
             self._variants[variant] = (src, kname)
         return self._variants[variant]
 
@@ -286,18 +286,31 @@ class HipStencilKernel:
                      len(tensors), 0, [n])
 
     def _plan_generic(self, tensors, shape, device):
+        from .hip_emitter import magic_u32
         ir = self.ir
-        fn = self.function(('generic',), device)
         bounds = ir.iteration_bounds(shape)
         ncell = int(np.prod([hi - lo for lo, hi in bounds]))
+        idx32 = 0 < ncell < 2 ** 31
+        contig = all(t.is_contiguous() for t in tensors)
+        variant = ('generic',) + (('idx32',) if idx32 else ()) + (('contig',) if contig else ())
+        fn = self.function(variant, device)
         statics = [int(n) for n in shape]
         for t in tensors:
             statics += [int(s_) for s_ in t.stride()]
         for lo, hi in bounds:
             statics += [lo, hi]
-        kinds = ['ptr'] * len(tensors) + ['i64'] * len(statics) + [self._scalar_kind()] * len(ir.scalars)
-        blocks = max(1, min(math.ceil(ncell / 256), 256 * 32)) if ncell > 0 else 0
-        return _Plan(('generic',), fn, blocks, kinds, len(tensors), 0, statics)
+        kinds = ['ptr'] * len(tensors) + ['i64'] * len(statics)
+        if idx32:
+            extra = [ncell]
+            kinds.append('u32')
+            for lo, hi in bounds[1:]:
+                m, sh = magic_u32(max(1, hi - lo))
+                extra += [m, sh]
+                kinds += ['u32', 'i32']
+            statics += extra
+        kinds += [self._scalar_kind()] * len(ir.scalars)
+        blocks = max(1, min(math.ceil(ncell / 256), 256 * 64)) if ncell > 0 else 0
+        return _Plan(variant, fn, blocks, kinds, len(tensors), 0, statics)
 
     def march_launch_geometry(self, shape, cfg, z_range=None):
         """(Z, Y, X), bounds and grid of the march schedule for a field shape."""
@@ -402,7 +415,7 @@ class _Plan:
     """A resolved launch: variant, function handle, grid and a struct that packs the argument
     buffer (pointers, then static extents, then scalars) at HIP_LAUNCH_PARAM_BUFFER alignment."""
 
-    _CODES = {'ptr': ('Q', 8), 'i32': ('i', 4), 'i64': ('q', 8), 'f32': ('f', 4), 'f64': ('d', 8)}
+    _CODES = {'ptr': ('Q', 8), 'i32': ('i', 4), 'u32': ('I', 4), 'i64': ('q', 8), 'f32': ('f', 4), 'f64': ('d', 8)}
 
     def __init__(self, variant, fn, grid, kinds, n_ptr, n_halo, statics, block=256):
         import struct

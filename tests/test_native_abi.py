@@ -182,3 +182,22 @@ def test_unsupported_backends_raise():
         op.create_tensorflow_op(backend='tensorflow_native')
     with pytest.raises(AssertionError):
         op.create_tensorflow_op(backend='jax')
+
+
+def test_generic_schedule_variants_and_magic_division():
+    """32-bit cell numbering with magic-number division (exact for every 32-bit numerator) and the
+    contiguous-component variant whose grouped reads merge into wide loads."""
+    import random
+    from pystencils_autodiff_amd.backends.hip_emitter import emit_generic, magic_u32
+    rng = random.Random(0)
+    for d in [1, 2, 3, 7, 384, 1000, 1024, 65535, 12345677, 2 ** 31 - 1]:
+        m, sh = magic_u32(d)
+        for n in [0, 1, d - 1, d, d + 1, 2 ** 31 - 1, 2 ** 32 - 1] + [rng.randrange(2 ** 32) for _ in range(500)]:
+            assert (((n * m) >> 32) + n) >> sh == n // d
+    op = pa.AutoDiffOp(W.vector_laplace_7pt(), boundary_handling='zeros')
+    ir = op.forward_ast_gpu.compile().ir
+    for idx32 in (False, True):
+        for contig in (False, True):
+            src = emit_generic(ir, 'g', idx32=idx32, contig=contig)
+            assert ('__umulhi' in src) == idx32 and ('st_u_3' in src.split('{', 1)[1]) == (not contig)
+            assert _is_amdgpu_elf(rt.compile_hip(src))
