@@ -56,6 +56,14 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             cfg.update(WS=True, CX=4, NR=4, D=4, ZMAX=128, BLK=256)
     if ir.ndim == 2:
         cfg.update(CX=4, WX=1, NR=4, VIEW2D='yx', NT_STORE=False)   # 256×16 tiles (4096²: 0.024 ms, 5.6 TB/s)
+    if ir.has_index_dims:
+        # vector fields (components interleaved in the plane image): only the zsum schedule handles them;
+        # narrower tiles keep the image (TX + 2H)·C elements wide
+        from .hip_emitter import ncomp
+        cmax = max([ncomp(f) for f in ir.stencil_fields] + [1])
+        cfg.update(ZSUM=True, PK=False, AR=False)
+        while cfg['CX'] > 1 and cfg['CX'] * cmax > 4:
+            cfg['CX'] //= 2
     if np.dtype(ir.compute_dtype).itemsize == 8:
         cfg['CX'] = max(1, cfg['CX'] // 2)                     # fp64: half-width tiles (512³: 0.380 vs 0.536 ms)
     elif ir.ndim == 3 and cfg['ZSUM'] and not cfg['PK'] and not cfg.get('WS'):
@@ -126,12 +134,17 @@ class HipStencilKernel:
     # -- sources --------------------------------------------------------------------------------
     def schedule(self):
         ir = self.ir
-        if ir.has_index_dims or ir.ndim not in (1, 2, 3):
+        if ir.ndim not in (1, 2, 3):
             return 'generic'
         if ir.pointwise:
-            return 'pointwise'
+            return 'generic' if ir.has_index_dims else 'pointwise'
         if ir.ndim in (2, 3) and all(all(o == 0 for o in s[1]) for s in ir.stores) and \
                 len({f.dtype for f in ir.fields}) == 1:
+            if ir.has_index_dims:
+                # vector fields: the zsum schedule (components interleaved in the plane image) when the
+                # stencil is linear off the centre plane, else one thread per cell
+                probe = MarchConfig(VE=self._vec_elems(), ZSUM=True)
+                return 'march' if ir.stencil_fields and zsum_plan(ir, probe) is not None else 'generic'
             return 'march'
         return 'generic'
 
@@ -373,8 +386,14 @@ class HipStencilKernel:
         cfg = self._march_cfg(ve if aligned else 1, shape)
         if halo_list and ir.ndim == 2 and cfg.VIEW2D == 'yx':
             cfg = MarchConfig(**{**cfg.__dict__, 'VIEW2D': 'zy'})
+        from .hip_emitter import ncomp
+        if ir.has_index_dims and not cfg.ZSUM:
+            if halo_list or z_range is not None:
+                raise ValueError('vector-field kernels take halo planes / z ranges only in the zsum schedule')
+            return self._plan_generic(tensors, shape, device)
+        cmax = max([ncomp(f) for f in stencil] + [1])
         ws = ws_geometry(ir, cfg)
-        if ws and int(np.prod(shape[1:])) * max(ws['esize'], ws.get('ssize', 0)) >= 2 ** 31 - 1024:
+        if ws and int(np.prod(shape[1:])) * cmax * max(ws['esize'], ws.get('ssize', 0)) >= 2 ** 31 - 1024:
             # planes beyond the loader's 32-bit buffer offsets: register-prefetch form of the same schedule
             cfg = MarchConfig(**{**cfg.__dict__, 'WS': False})
         variant = ('march', cfg)
@@ -386,7 +405,7 @@ class HipStencilKernel:
         for i, f in enumerate(stencil):
             for h in (halo_list[2 * i:2 * i + 2] if halo_list else ()):
                 if h is not None and (not isinstance(h, torch.Tensor) or not h.is_contiguous() or
-                                      h.numel() < rz * plane or h.dtype != by_name[f.name].dtype or
+                                      h.numel() < rz * plane * ncomp(f) or h.dtype != by_name[f.name].dtype or
                                       h.device != by_name[f.name].device):
                     raise ValueError(f"halo for '{f.name}' must be a contiguous tensor of >= {rz} planes "
                                      "on the field's device")

@@ -268,11 +268,12 @@ def test_vector_field_generic_schedule():
     k = op.forward_ast_gpu.compile()
     rng = np.random.default_rng(0)
     fa = rng.uniform(-1, 1, (12, 10, 2))
-    o = torch.zeros((12, 10), dtype=torch.float64, device='cuda')
-    k(f=torch.from_numpy(fa).cuda(), out=o)
     ref = OE.evaluate(op.forward_assignments, {'f': fa}, boundary_handling='zeros')['out']
-    assert k.last_variant[0] == 'generic'
-    assert_close_rel(o.cpu().numpy(), ref, 1e-12)
+    for sched in (None, 'generic'):        # the default (2-D view: everything on the centre plane -> zsum)
+        o = torch.zeros((12, 10), dtype=torch.float64, device='cuda')
+        k(f=torch.from_numpy(fa).cuda(), out=o, force_schedule=sched)
+        assert k.last_variant[0] == (sched or 'march')
+        assert_close_rel(o.cpu().numpy(), ref, 1e-12)
 
 
 @pytest.mark.parametrize('params', [
@@ -691,3 +692,76 @@ def test_vector_field_partial_writes_and_variable_shapes_gpu():
     assert c.shape == (20, 30, 2) and dx.shape == (20, 30)
     assert_close_rel(c, OE.evaluate(op2.forward_assignments, {'curl_input': x}, boundary_handling='zeros')['curl'],
                      1e-12, 'curl')
+
+
+def _vector_cases():
+    u, v, out = ps.fields("u(3), v, out(2): float32[3d]")
+    mix = ps.AssignmentCollection({out.center(0): 0.3 * u[1, 0, 0](1) - 0.2 * u[0, -1, 1](2) + 0.5 * u.center(0)
+                                   + sp.sin(v.center) * u.center(1),
+                                   out.center(1): 0.7 * u[-1, 1, 0](0) + 0.1 * u[0, 0, -1](2) - v.center})
+    w, o2 = ps.fields("w(2), o2(2): float64[3d]")
+    d64 = ps.AssignmentCollection({o2.center(c): w[1, 0, 0](c) + w[0, 0, -1](1 - c) - 2.5 * w.center(c)
+                                   for c in range(2)})
+    q, o3 = ps.fields("q(4), o3(4): float32[2d]")
+    two_d = ps.AssignmentCollection({o3.center(c): q[1, 0](c) - q[0, -1]((c + 1) % 4) + 0.25 * q.center(c)
+                                     for c in range(4)})
+    return [('veclap3', W.vector_laplace_7pt, np.float32), ('mixed', lambda: mix, np.float32),
+            ('f64_2comp', lambda: d64, np.float64), ('2d_4comp', lambda: two_d, np.float32)]
+
+
+@pytest.mark.parametrize('params', [dict(), dict(ZSUM=True, WS=False, CX=1, NR=3, ZC=5),
+                                    dict(ZSUM=True, WS=True, D=2, CX=2, NR=2, ZC=4),
+                                    dict(ZSUM=True, WS=False, CX=2, WX=2, NR=2, PK=True)])
+@pytest.mark.parametrize('case', _vector_cases(), ids=lambda c: c[0])
+def test_vector_fields_zsum_vs_oracle(params, case):
+    """Vector fields (components fastest in memory) through the zsum schedule: the plane image holds
+    the interleaved components, taps and stores carry the component offset — forward and the TF-MAD
+    adjoint vs the oracle, ragged shapes with interior and edge tiles."""
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    name, builder, dt = case
+    ac = builder()
+    op = pa.AutoDiffOp(ac, boundary_handling='zeros')
+    is2d = name.startswith('2d')
+    spatial = (37, 72) if is2d else (6, 13, 136)
+    rng = np.random.default_rng(len(name))
+
+    def arr(f):
+        return rng.uniform(-1, 1, spatial + tuple(int(n) for n in f.index_shape)).astype(dt)
+    arrays = {f.name: arr(f) for f in list(op.forward_input_fields) + list(op.backward_input_fields)}
+    for which, a in (('f', op.forward_assignments), ('b', op.backward_assignments)):
+        k = StencilKernel(a, boundary_handling='zeros', function_name=f'vz_{which}', target='gpu',
+                          gpu_indexing_params=params).compile()
+        ins = {f.name: arrays[f.name] for f in k.ir.fields_read}
+        ref = OE.evaluate(a, ins, boundary_handling='zeros')
+        outs = {f.name: torch.full(spatial + tuple(int(n) for n in f.index_shape), float('nan'),
+                                   dtype=getattr(torch, np.dtype(dt).name), device='cuda') for f in k.ir.fields_written}
+        for n, t in outs.items():          # components a kernel does not write stay as allocated (zeros here)
+            t.zero_()
+        k(**{n: torch.from_numpy(v).cuda() for n, v in ins.items()}, **outs)
+        torch.cuda.synchronize()
+        if k.ir.stencil_fields:
+            assert k.last_variant[0] == 'march' and k.last_variant[1].ZSUM, k.last_variant
+        for n, t in outs.items():
+            assert_close_rel(t.cpu().numpy(), ref[n], TOL[dt], f'{name} {which} {n} {params}')
+
+
+def test_vector_field_halos_and_two_range_launches():
+    """z-slab launch pattern for a vector field: halo planes carry all components."""
+    op = pa.AutoDiffOp(W.vector_laplace_7pt(), boundary_handling='zeros')
+    k = op.forward_ast_gpu.compile()
+    g = torch.Generator().manual_seed(9)
+    u = torch.rand((20, 11, 72, 3), generator=g).cuda()
+    full = torch.empty_like(u)
+    k(u=u, out=full)
+    assert k.last_variant[0] == 'march'
+    outs = []
+    for a, b in [(0, 7), (7, 13), (13, 20)]:
+        sl = u[a:b].contiguous()
+        out = torch.full_like(sl, float('nan'))
+        lo = u[a - 1:a].contiguous() if a > 0 else None
+        hi = u[b:b + 1].contiguous() if b < 20 else None
+        k(u=sl, out=out, z_range=(1, b - a - 1))
+        k(u=sl, out=out, halos={'u': (lo, hi)}, z_range=((0, 1), (b - a - 1, b - a)))
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(outs), full)

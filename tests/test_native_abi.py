@@ -201,3 +201,16 @@ def test_generic_schedule_variants_and_magic_division():
             src = emit_generic(ir, 'g', idx32=idx32, contig=contig)
             assert ('__umulhi' in src) == idx32 and ('st_u_3' in src.split('{', 1)[1]) == (not contig)
             assert _is_amdgpu_elf(rt.compile_hip(src))
+
+
+def test_vector_field_zsum_compiles():
+    """Vector fields take the zsum schedule (components interleaved in the plane image)."""
+    from pystencils_autodiff_amd.backends.hip_emitter import march_geometry
+    op = pa.AutoDiffOp(W.vector_laplace_7pt(), boundary_handling='zeros')
+    for k in (op.forward_ast_gpu.compile(), op.backward_ast_gpu.compile()):
+        assert k.schedule() == 'march'
+        v = k.primary_variant()
+        assert v[1].ZSUM
+        g = march_geometry(k.ir, v[1])
+        assert all(fg['C'] == 3 and fg['P'] == 3 * g['P'] for fg in g['FG'].values())
+        assert _is_amdgpu_elf(rt.compile_hip(k.source(v)[0]))
