@@ -52,11 +52,14 @@ def main():
     n = a.n
     builder = {'diffusion7': (W.diffusion_7pt, torch.float32), 'stencil27': (W.stencil_27pt, torch.float16),
                'laplace5': (W.laplace_5pt, torch.float32),
-               'diffusion7_f64': (lambda: W.diffusion_7pt(dtype='float64'), torch.float64)}[a.workload]
+               'diffusion7_f64': (lambda: W.diffusion_7pt(dtype='float64'), torch.float64),
+               'veclap3': (W.vector_laplace_7pt, torch.float32)}[a.workload]
     op = AutoDiffOp(builder[0](), boundary_handling='zeros')
     shape = (n, n) if a.workload == 'laplace5' else (n, n, n)
     if a.shape:
         shape = tuple(int(v) for v in a.shape.split(','))
+    if a.workload == 'veclap3':
+        shape = shape + (3,)
     cells = 1
     for s in shape:
         cells *= s
@@ -105,7 +108,9 @@ def main():
     # practical read+write ceiling on this device, measured in the same process
     from pystencils_autodiff_amd import ps as _ps
     from pystencils_autodiff_amd.backends import hip_emitter as _he
-    cu, co = _ps.fields(f"cu, co: {str(u.dtype).replace('torch.', '')}[{len(shape)}d]")
+    cu, co = _ps.fields(f"cu, co: {str(u.dtype).replace('torch.', '')}[{len(shape) if a.workload != 'veclap3' else 3}d]")
+    if a.workload == 'veclap3':
+        u, out = u.reshape(shape[0], shape[1], -1), out.reshape(shape[0], shape[1], -1)
     alg = 2 * esize * cells
     for nt_load, maxb in ((False, 2048), (True, 2048), (False, 0), (True, 0)):
         _he.POINTWISE_NT_LOAD = nt_load
@@ -145,7 +150,7 @@ def main():
     for i, c in enumerate(cfgs):
         ts = sorted(times[i])
         med = ts[len(ts) // 2]
-        geo = kernels[i].march_launch_geometry(shape if len(shape) == 3 else shape, kernels[i].last_variant[1])
+        geo = kernels[i].march_launch_geometry(shape[:3] if len(shape) >= 3 else shape, kernels[i].last_variant[1])
         print(f"tune{i:<3d} {','.join(f'{k}={v}' for k, v in c.items()) or 'default':34s} median {med:.4f} ms  min {ts[0]:.4f} ms  "
               f"{alg / (med * 1e-3) / 1e9:7.0f} GB/s  grid {geo['grid']} zc {geo['zc']}  maxdiff_vs_generic {maxdiff[i]:.2e}")
     sys.stdout.flush()
