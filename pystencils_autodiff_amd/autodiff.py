@@ -450,6 +450,16 @@ class AutoDiffOp:
                 self._backward_output_fields.append(f_adjoint)
                 if self._backward_field_map is not None:
                     self._backward_field_map[f] = f_adjoint
+        if backend == 'torch':
+            # the reference's python-loop backend (backends/_pytorch.py:18-85) runs the same kernels on
+            # tensors given up front (and is a legacy, instance-method autograd.Function current torch
+            # rejects); here it is the native Function, on the device of those tensors
+            if forward_loop is not None or backward_loop is not None:
+                raise NotImplementedError("custom forward_loop / backward_loop callables are not supported; "
+                                          "the operator runs the generated kernels")
+            tensors = [t for t in inputfield_tensor_dict.values() if hasattr(t, 'is_cuda')]
+            use_cuda = bool(tensors) and all(t.is_cuda for t in tensors)
+            backend = 'torch_native'
         if backend == 'torch_native':
             from .backends import _torch_native
             return _torch_native.create_autograd_function(

@@ -229,3 +229,21 @@ def test_vector_field_partial_writes_and_variable_shapes_cpu():
     assert tuple(c.shape) == (20, 30, 2)
     c.backward(torch.ones_like(c))
     assert tuple(x.grad.shape) == (20, 30)
+
+
+def test_tfmad_gradient_check_torch_backend():
+    """tests/test_tfmad.py:100-131 of the reference: backend='torch' with an input-field -> tensor dict,
+    gradcheck of the returned Function (here the native Function on the dict tensors' device)."""
+    a, b, out = ps.fields("a, b, out: float64[5,7]")
+    cont = 2 * ps.fd.Diff(a, 0) - 1.5 * ps.fd.Diff(a, 1) - ps.fd.Diff(b, 0) + 3 * ps.fd.Diff(b, 1)
+    assignment = ps.Assignment(out.center(), ps.fd.Discretization2ndOrder(dx=1)(cont) + 1.2 * a.center)
+    # boundary 'zeros' (the reference test leaves boundary_handling=None, whose interior-only adjoint is not
+    # the forward's transpose at the border, so its gradcheck cannot pass; the torch_native twin uses 'zeros')
+    op = pa.AutoDiffOp(ps.AssignmentCollection([assignment], []), diff_mode='transposed-forward',
+                       boundary_handling='zeros')
+    at = torch.zeros(*a.shape, dtype=torch.float64, requires_grad=True)
+    bt = torch.zeros(*b.shape, dtype=torch.float64, requires_grad=True)
+    fn = op.create_tensorflow_op({a: at, b: bt}, backend='torch')
+    assert torch.autograd.gradcheck(fn.apply, [at, bt])
+    with pytest.raises(NotImplementedError):
+        op.create_tensorflow_op({a: at, b: bt}, forward_loop=lambda **kw: None, backend='torch')
