@@ -421,6 +421,25 @@ class AutoDiffOp:
     def backward_kernel_cpu(self):
         return self.backward_ast_cpu.compile()
 
+    def _create_kernel(self, which, target='cpu', data_type=None, iteration_slice=None, ghost_layers=None,
+                       **kwargs):
+        """``ps.create_kernel(assignments, *args, **kwargs).compile()`` (``_autodiff.py:592-598``): a
+        compiled kernel of this op's forward / backward assignments with pystencils' defaults — interior
+        only unless ``ghost_layers=0`` (then out-of-domain reads are zeros, the only defined meaning)."""
+        from .backends.kernel_ir import StencilKernel
+        if iteration_slice is not None:
+            raise NotImplementedError('iteration_slice is not supported')
+        ac = self._forward_assignments if which == 'forward' else self._backward_assignments
+        bh = 'zeros' if ghost_layers == 0 else None
+        return StencilKernel(ac, boundary_handling=bh, function_name=f"{self.op_name}_{which}_{target}_custom",
+                             target=target, data_type=data_type, **{**self._kwargs, **kwargs}).compile()
+
+    def create_forward_kernel(self, *args, **kwargs):
+        return self._create_kernel('forward', *args, **kwargs)
+
+    def create_backward_kernel(self, *args, **kwargs):
+        return self._create_kernel('backward', *args, **kwargs)
+
     def get_forward_kernel(self, is_gpu):
         return self.forward_kernel_gpu if is_gpu else self.forward_kernel_cpu
 

@@ -247,3 +247,22 @@ def test_tfmad_gradient_check_torch_backend():
     assert torch.autograd.gradcheck(fn.apply, [at, bt])
     with pytest.raises(NotImplementedError):
         op.create_tensorflow_op({a: at, b: bt}, forward_loop=lambda **kw: None, backend='torch')
+
+
+def test_create_forward_backward_kernel_like_reference():
+    """AutoDiffOp.create_forward_kernel / create_backward_kernel (_autodiff.py:592-598): pystencils'
+    create_kernel defaults (interior only), ghost_layers=0 -> every cell with zero-padded reads."""
+    op = pa.AutoDiffOp(W.asym_7pt(), boundary_handling='zeros')
+    rng = np.random.default_rng(3)
+    u = rng.uniform(-1, 1, (6, 7, 8)).astype(np.float32)
+    for gl, bh in ((None, None), (0, 'zeros')):
+        k = op.create_forward_kernel(ghost_layers=gl) if gl is not None else op.create_forward_kernel()
+        out = np.zeros_like(u)
+        k(u=u, out=out)
+        ref = OE.evaluate(op.forward_assignments, {'u': u}, boundary_handling=bh)['out']
+        assert_close_rel(out, ref, 1e-6, f'forward ghost_layers={gl}')
+    kb = op.create_backward_kernel('cpu', ghost_layers=0)
+    du = np.zeros_like(u)
+    kb(diffout=u, diffu=du)
+    assert_close_rel(du, OE.evaluate(op.backward_assignments, {'diffout': u}, boundary_handling='zeros')['diffu'],
+                     1e-6, 'backward')
