@@ -373,7 +373,7 @@ class HipStencilKernel:
         nchunks = math.ceil(nz / zc) if nz else 0
         if nchunks:
             # equal chunks: same chunk count (same halo re-reads), no short tail chunk — 27-point fp16
-            # 192×768² slab: 27 → 24 planes, 0.129 → 0.119 ms (profiles/r01_tune_zc_slab.log)
+            # 192×768² slab: 27 → 24 planes, 0.129 → 0.113 ms (profiles/r01_tune_zc_slab.log)
             zc = math.ceil(nz / nchunks)
         return dict(Z=Z, Y=Y, X=X, zlo=zlo, zhi=zhi, ylo=ylo, yhi=yhi, xlo=xlo, xhi=xhi, zc=zc, zstep=zc,
                     ntx=ntx, nty=nty, grid=nt * nchunks)
