@@ -122,7 +122,8 @@ def main():
     if distributed:
         # the same drop-in contract over this rank's slab: Function.apply + backward, with the
         # RCCL halo exchange inside the forward and the backward (zslab.py)
-        fn = ZSlabOp(op, use_cuda=True).autograd_function()
+        zop = ZSlabOp(op, use_cuda=True)
+        fn = zop.autograd_function()
     uu = u.requires_grad_(True)
 
     def step(record):
@@ -224,6 +225,7 @@ def main():
         res.update(result_extra)
         print(json.dumps(res))
     if distributed:
+        zop.close()
         dist.destroy_process_group()
 
 

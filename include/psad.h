@@ -68,6 +68,30 @@ int psad_last_error(void);
 /* Stream-ordered device-to-device copy (halo staging). */
 int psad_memcpy_d2d_async(void* dst, const void* src, size_t bytes, void* stream);
 
+/* --- RCCL halo exchange (z-slab decomposition; no counterpart in the reference, which has no
+ * multi-GPU path — SURVEY.md §8e). Codes from RCCL are offset by PSAD_RCCL_ERROR_BASE. --- */
+#define PSAD_RCCL_ERROR_BASE 20000
+
+/* dlopen librccl (e.g. torch's bundled copy) and resolve the NCCL 2.x entry points used below. */
+int psad_rccl_open(const char* library_path);
+
+/* ncclGetUniqueId into `id` (128 bytes), to be broadcast to every rank by the caller. */
+int psad_rccl_unique_id(void* id);
+
+/* ncclCommInitRank over `nranks` ranks (collective: every rank calls it with the same id). */
+int psad_rccl_comm_init(const void* id, int nranks, int rank, void** comm);
+int psad_rccl_comm_destroy(void* comm);
+
+/* Swap slab boundary planes with the neighbouring ranks in ONE ncclGroupStart/End on `stream`: for
+ * each of `n_fields` fields, send `send_lo[i]` to / receive `recv_lo[i]` from `peer_lo`, and
+ * `send_hi[i]` / `recv_hi[i]` with `peer_hi` (`bytes[i]` each; a peer < 0 skips that side).
+ * Stream-ordered and asynchronous, like the kernels that produce and consume the planes. */
+int psad_halo_exchange(void* comm, int n_fields, const void* const* send_lo, void* const* recv_lo,
+                       const void* const* send_hi, void* const* recv_hi, const size_t* bytes, int peer_lo,
+                       int peer_hi, void* stream);
+
+const char* psad_rccl_error_string(int code);
+
 /* Human-readable description of a code returned above. */
 const char* psad_error_string(int code);
 

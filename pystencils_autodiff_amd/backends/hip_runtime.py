@@ -77,7 +77,20 @@ def lib():
         L.psad_memcpy_d2d_async.restype = c_int
         L.psad_error_string.argtypes = [c_int]
         L.psad_error_string.restype = cp
-        if L.psad_abi_version() != 1:
+        L.psad_rccl_open.argtypes = [cp]
+        L.psad_rccl_open.restype = c_int
+        L.psad_rccl_unique_id.argtypes = [vp]
+        L.psad_rccl_unique_id.restype = c_int
+        L.psad_rccl_comm_init.argtypes = [vp, c_int, c_int, ctypes.POINTER(vp)]
+        L.psad_rccl_comm_init.restype = c_int
+        L.psad_rccl_comm_destroy.argtypes = [vp]
+        L.psad_rccl_comm_destroy.restype = c_int
+        L.psad_halo_exchange.argtypes = [vp, c_int, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                         ctypes.POINTER(vp), ctypes.POINTER(c_size), c_int, c_int, vp]
+        L.psad_halo_exchange.restype = c_int
+        L.psad_rccl_error_string.argtypes = [c_int]
+        L.psad_rccl_error_string.restype = cp
+        if L.psad_abi_version() != 2:
             raise HipError('libpsad_hip.so ABI mismatch: rebuild the extension')
         _lib = L
         return _lib

@@ -10,17 +10,17 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = os.path.join(HERE, 'csrc', 'psad_hip.cpp')
+SRCS = [os.path.join(HERE, 'csrc', f) for f in ('psad_hip.cpp', 'psad_halo.cpp')]
 OUT = os.path.join(HERE, 'libpsad_hip.so')
 
 
 def build(force=False, verbose=False):
-    if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= os.path.getmtime(SRC) and \
-            os.path.getmtime(OUT) >= os.path.getmtime(os.path.join(ROOT, 'include', 'psad.h')):
+    deps = SRCS + [os.path.join(ROOT, 'include', 'psad.h')]
+    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
     hipcc = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
     cmd = [hipcc, '-O2', '-fPIC', '-shared', '-std=c++17', f"-I{os.path.join(ROOT, 'include')}",
-           '-o', OUT + '.tmp', SRC, '-lhiprtc']
+           '-o', OUT + '.tmp', *SRCS, '-lhiprtc', '-ldl']
     if verbose:
         print(' '.join(cmd))
     proc = subprocess.run(cmd, capture_output=True, text=True)

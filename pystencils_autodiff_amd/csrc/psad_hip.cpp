@@ -29,7 +29,7 @@ void copy_log(hiprtcProgram prog, char* log, size_t log_size) {
 
 extern "C" {
 
-int psad_abi_version(void) { return 1; }
+int psad_abi_version(void) { return 2; }
 
 int psad_rtc_version(void) {
     int major = 0, minor = 0;
@@ -131,6 +131,7 @@ int psad_memcpy_d2d_async(void* dst, const void* src, size_t bytes, void* stream
 }
 
 const char* psad_error_string(int code) {
+    if (code >= PSAD_RCCL_ERROR_BASE) return psad_rccl_error_string(code);
     if (code >= PSAD_HIPRTC_ERROR_BASE) return hiprtcGetErrorString(static_cast<hiprtcResult>(code - PSAD_HIPRTC_ERROR_BASE));
     return hipGetErrorString(static_cast<hipError_t>(code));
 }

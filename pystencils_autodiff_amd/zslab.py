@@ -7,9 +7,13 @@ the MI355X layer's scale-out for the 3-D configs (BASELINE configs 4 and 5):
   owning planes ``[k·Z/P, (k+1)·Z/P)`` (remainder spread over the first ranks);
 * one exchange step per sweep: each stencil field sends its first / last
   ``RZ`` planes to rank ``k-1`` / ``k+1`` and receives their boundary planes as
-  halos (``torch.distributed.batch_isend_irecv`` — point-to-point, on the
-  ``nccl`` backend that is RCCL over xGMI; neighbours talk over their own link,
-  nothing here is a ring collective). Rank 0's lower and rank ``P-1``'s upper
+  halos — point-to-point over xGMI, neighbours talk over their own link, nothing
+  here is a ring collective. On GPUs with the ``nccl`` (= RCCL) process group the
+  exchange is ONE ``ncclGroupStart; ncclSend/ncclRecv…; ncclGroupEnd`` on a
+  dedicated stream through the C ABI (``psad_halo_exchange``, a communicator of
+  its own, :class:`RcclHalo`); ``torch.distributed.batch_isend_irecv`` (~80 µs
+  of host time per exchange) remains the path for ``gloo`` and for
+  ``PSAD_HALO=torch``. Rank 0's lower and rank ``P-1``'s upper
   halos stay absent, which the kernel reads as zeros — the ``'zeros'``
   boundary of the undivided domain;
 * the exchange overlaps the interior planes: the march kernel first writes
@@ -22,10 +26,67 @@ the MI355X layer's scale-out for the 3-D configs (BASELINE configs 4 and 5):
 On the CPU (``gloo``) the same exchange runs and the C kernel evaluates a
 ghosted copy — used by the multi-process tests.
 """
+import ctypes
+import glob
+import os
+
 import torch
 import torch.distributed as dist
 
-__all__ = ['slab_bounds', 'ZSlabOp', 'exchange_halos']
+__all__ = ['slab_bounds', 'ZSlabOp', 'exchange_halos', 'RcclHalo']
+
+
+def rccl_library_path():
+    """torch's bundled librccl (the copy its process group already loaded), else the ROCm one."""
+    cands = sorted(glob.glob(os.path.join(os.path.dirname(torch.__file__), 'lib', 'librccl.so*')))
+    cands += sorted(glob.glob('/opt/rocm/lib/librccl.so*'))
+    return os.environ.get('PSAD_RCCL_LIBRARY') or (cands[0] if cands else 'librccl.so.1')
+
+
+class RcclHalo:
+    """An RCCL communicator of its own over ``group`` for the slab-face exchange, and the stream the
+    exchange runs on. Construction is collective (``ncclCommInitRank`` on every rank)."""
+
+    def __init__(self, group=None, device=None, loopback=False):
+        """``loopback=True``: a one-rank communicator without ``torch.distributed`` whose exchange
+        sends both faces to itself — the slab then sees its own far faces as halos, a periodic z
+        boundary; it exercises the whole RCCL path on one GPU (tests)."""
+        from .backends import hip_runtime as rt
+        self._rt = rt
+        L = rt.lib()
+        rt._check(L.psad_rccl_open(rccl_library_path().encode()), 'opening librccl')
+        self.loopback = loopback
+        self.rank = 0 if loopback else dist.get_rank(group)
+        self.world = 1 if loopback else dist.get_world_size(group)
+        uid = ctypes.create_string_buffer(128)
+        if self.rank == 0:
+            rt._check(L.psad_rccl_unique_id(uid), 'ncclGetUniqueId')
+        obj = [uid.raw if self.rank == 0 else None]
+        if not loopback:
+            dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                       group=group)
+        self.device = torch.device('cuda', torch.cuda.current_device()) if device is None else device
+        with torch.cuda.device(self.device):
+            comm = ctypes.c_void_p()
+            rt._check(L.psad_rccl_comm_init(obj[0], self.world, self.rank, ctypes.byref(comm)), 'ncclCommInitRank')
+            self.comm = comm
+            self.stream = torch.cuda.Stream(device=self.device)
+
+    def exchange(self, planes, peer_lo, peer_hi):
+        """``planes`` = [(send_lo, recv_lo, send_hi, recv_hi, nbytes)] (device pointers, 0 for an
+        absent side); enqueued on :attr:`stream`, which the caller orders against its own."""
+        n = len(planes)
+        vp = ctypes.c_void_p
+        cols = list(zip(*planes)) if n else [()] * 5
+        arrs = [(vp * n)(*cols[i]) for i in range(4)]
+        sizes = (ctypes.c_size_t * n)(*cols[4])
+        self._rt._check(self._rt.lib().psad_halo_exchange(self.comm, n, *arrs, sizes, peer_lo, peer_hi,
+                                                          self.stream.cuda_stream), 'RCCL halo exchange')
+
+    def close(self):
+        if self.comm:
+            self._rt._check(self._rt.lib().psad_rccl_comm_destroy(self.comm), 'ncclCommDestroy')
+            self.comm = None
 
 
 def slab_bounds(n, world, rank):
@@ -96,6 +157,22 @@ class ZSlabOp:
             if not k.ir.zeros:
                 raise ValueError("z-slab decomposition supports boundary_handling='zeros'")
         self._bufs = {}
+        self._halo = None
+
+    def _rccl(self, device):
+        """The RCCL exchange path (GPU, ``nccl`` process group, ``PSAD_HALO`` not ``torch``)."""
+        if not (self.use_cuda and dist.is_initialized() and dist.get_backend(self.group) == 'nccl'
+                and os.environ.get('PSAD_HALO', 'rccl') == 'rccl'):
+            return None
+        if self._halo is None:
+            self._halo = RcclHalo(self.group, device)
+        return self._halo
+
+    def close(self):
+        """Destroy the halo communicator (collective, before ``destroy_process_group``)."""
+        if self._halo is not None:
+            self._halo.close()
+            self._halo = None
 
     def _radius(self, kernel, field):
         return max([abs(r.offsets[0]) for r in kernel.ir.reads if r.field.name == field.name] + [0])
@@ -111,6 +188,12 @@ class ZSlabOp:
         ir = k.ir
         stencil = ir.stencil_fields
         rz = max([self._radius(k, f) for f in stencil] + [0])
+        ref = kwargs[ir.fields_written[0].name]
+        split = rz > 0 and dist.is_initialized() and dist.get_world_size(self.group) > 1
+        halo = self._rccl(ref.device) if split else None
+        if halo is not None:
+            self._sweep_rccl(k, halo, stencil, rz, kwargs)
+            return
         pending, halos = [], {}
         for f in stencil:
             t = kwargs[f.name]
@@ -119,9 +202,7 @@ class ZSlabOp:
             self._bufs[(which, f.name, t.dtype, tuple(t.shape[1:]), t.device)] = (lo, hi)
             pending += works
             halos[f.name] = (lo, hi)
-        ref = kwargs[ir.fields_written[0].name]
         zl = ref.shape[0]
-        split = rz > 0 and dist.is_initialized() and dist.get_world_size(self.group) > 1
         if self.use_cuda:
             compiled = k.compile()
             if split:
@@ -155,6 +236,53 @@ class ZSlabOp:
         for name, t in outs.items():
             if rz:
                 t.copy_(ghosted[name][rz:rz + zl])
+
+    def _sweep_rccl(self, k, halo, stencil, rz, kwargs):
+        """Faces out on the halo stream (one RCCL group for every stencil field) while the interior
+        planes run on the caller's stream; then the two face ranges in one launch."""
+        rank, world = halo.rank, halo.world
+        peer_lo = rank - 1 if rank > 0 else -1
+        peer_hi = rank + 1 if rank < world - 1 else -1
+        if halo.loopback:
+            peer_lo = peer_hi = 0
+        cur = torch.cuda.current_stream(halo.device)
+        halo.stream.wait_stream(cur)                  # the faces are final; the last sweep's reads are done
+        planes, halos = [], {}
+        for f in stencil:
+            t = kwargs[f.name]
+            if t.shape[0] < rz:
+                raise ValueError(f"slab of {t.shape[0]} planes is thinner than the stencil radius {rz}")
+            if not t.is_contiguous():
+                raise ValueError(f"slab of '{f.name}' must be contiguous for the RCCL face exchange")
+            key = ('rccl', f.name, t.dtype, tuple(t.shape[1:]), t.device)
+            bufs = self._bufs.get(key)
+            if bufs is None:
+                shape = (rz,) + tuple(t.shape[1:])
+                bufs = (torch.empty(shape, dtype=t.dtype, device=t.device) if peer_lo >= 0 else None,
+                        torch.empty(shape, dtype=t.dtype, device=t.device) if peer_hi >= 0 else None)
+                self._bufs[key] = bufs
+            lo, hi = bufs
+            nbytes = rz * t[0].numel() * t.element_size()
+            first = t.data_ptr()
+            last = first + (t.shape[0] - rz) * t[0].numel() * t.element_size()
+            if halo.loopback:
+                # RCCL pairs a peer's sends and receives in issue order: swap the faces so that, as
+                # with real neighbours, the lower halo receives the far (upper) face — periodic z
+                first, last = last, first
+            planes.append((first, lo.data_ptr() if lo is not None else 0, last,
+                           hi.data_ptr() if hi is not None else 0, nbytes))
+            t.record_stream(halo.stream)
+            halos[f.name] = (lo, hi)
+        halo.exchange(planes, peer_lo, peer_hi)
+        compiled = k.compile()
+        zl = kwargs[k.ir.fields_written[0].name].shape[0]
+        if zl > 2 * rz:
+            compiled(z_range=(rz, zl - rz), **kwargs)  # interior overlaps the exchange
+        cur.wait_stream(halo.stream)
+        if zl > 2 * rz:
+            compiled(halos=halos, z_range=((0, rz), (zl - rz, zl)), **kwargs)
+        else:
+            compiled(halos=halos, z_range=(0, zl), **kwargs)
 
     def autograd_function(self):
         """A ``torch.autograd.Function`` over this rank's slabs with the drop-in op's contract:

@@ -110,3 +110,71 @@ def test_zslab_gloo_gpu_halo_path(world, shape, builder_name, tmp_path):
     out, du, ref_out, ref_du = _run(world, shape, builder_name, True, tmp_path)
     assert_close_rel(out, ref_out, 1e-6, 'out')
     assert_close_rel(du, ref_du, 1e-6, 'diffu')
+
+
+@pytest.mark.gpu
+def test_rccl_c_abi_self_exchange():
+    """psad_halo_exchange through a one-rank RCCL communicator, both faces sent to itself: the
+    receive buffers hold the slab's own first / last planes (pointer math, group, stream)."""
+    import ctypes
+    import sys
+    sys.path.insert(0, ROOT)
+    from pystencils_autodiff_amd.zslab import RcclHalo
+    halo = RcclHalo(loopback=True)
+    try:
+        t = torch.rand((7, 33, 40), device='cuda')
+        v = torch.rand((7, 33, 40), device='cuda')
+        bufs = [torch.full((2, 33, 40), -1.0, device='cuda') for _ in range(4)]
+        nb = 2 * 33 * 40 * 4
+        plane = 33 * 40 * 4
+        halo.stream.wait_stream(torch.cuda.current_stream())
+        halo.exchange([(t.data_ptr(), bufs[0].data_ptr(), t.data_ptr() + 5 * plane, bufs[1].data_ptr(), nb),
+                       (v.data_ptr(), bufs[2].data_ptr(), v.data_ptr() + 5 * plane, bufs[3].data_ptr(), nb)], 0, 0)
+        halo.stream.synchronize()
+        assert torch.equal(bufs[0], t[:2]) and torch.equal(bufs[1], t[-2:])
+        assert torch.equal(bufs[2], v[:2]) and torch.equal(bufs[3], v[-2:])
+        assert ctypes is not None
+    finally:
+        halo.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('builder_name,shape', [('asym_7pt', (12, 40, 70)), ('diffusion_7pt', (3, 17, 64)),
+                                                ('diffusion_7pt', (2, 9, 64)), ('diffusion_7pt', (1, 9, 64)),
+                                                ('stencil_27pt', (9, 24, 80))])
+def test_zslab_rccl_loopback_sweep(builder_name, shape):
+    """The RCCL sweep (faces out on the halo stream, interior launch, wait, one two-range face launch)
+    on one GPU with a loopback communicator: equals the stencil with a periodic z boundary."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import pystencils_autodiff_amd as pa
+    from oracle import stencils as S
+    from pystencils_autodiff_amd import workloads as W
+    from pystencils_autodiff_amd.zslab import RcclHalo, ZSlabOp
+    from tests.conftest import assert_close_rel
+    op = pa.AutoDiffOp(getattr(W, builder_name)(), boundary_handling='zeros')
+    taps = {'diffusion_7pt': S.taps_diffusion_7pt(), 'asym_7pt': S.taps_asym_7pt(),
+            'stencil_27pt': S.taps_27pt()}[builder_name]
+    dt = np.float16 if builder_name == 'stencil_27pt' else np.float32
+    tol = 1e-3 if dt == np.float16 else 1e-6
+    rng = np.random.default_rng(5)
+    u = rng.uniform(0, 1, shape).astype(dt)
+    d = rng.uniform(-1, 1, shape).astype(dt)
+    z = ZSlabOp(op, use_cuda=True)
+    z._halo = RcclHalo(loopback=True)
+    try:
+        tu, td = torch.from_numpy(u).cuda(), torch.from_numpy(d).cuda()
+        out, du = torch.empty_like(tu), torch.empty_like(td)
+        for which, kw in (('forward', dict(u=tu, out=out)), ('backward', dict(diffout=td, diffu=du))):
+            k = z.kernels[which]
+            z._sweep_rccl(k, z._halo, k.ir.stencil_fields, 1, kw)
+        torch.cuda.synchronize()
+
+        def periodic(a, tp):
+            a64 = a.astype(np.float64)
+            ext = np.concatenate([a64[-1:], a64, a64[:1]])
+            return S.linear_stencil(ext, tp)[1:-1]
+        assert_close_rel(out.cpu().numpy().astype(np.float64), periodic(u, taps), tol, 'out')
+        assert_close_rel(du.cpu().numpy().astype(np.float64), periodic(d, S.flip(taps)), tol, 'diffu')
+    finally:
+        z.close()
