@@ -191,6 +191,8 @@ class ZSlabOp:
         ref = kwargs[ir.fields_written[0].name]
         split = rz > 0 and dist.is_initialized() and dist.get_world_size(self.group) > 1
         halo = self._rccl(ref.device) if split else None
+        if halo is None and rz > 0 and self._halo is not None and self._halo.loopback:
+            halo = self._halo                         # one-GPU loopback (tests, probes)
         if halo is not None:
             self._sweep_rccl(k, halo, stencil, rz, kwargs)
             return
