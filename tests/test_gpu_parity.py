@@ -341,7 +341,9 @@ def _zsum_cases():
                                     dict(ZSUM=True, WS=False, DB=True, PK=True, AR=True, CX=2, WX=2, NR=2, ZC=6),
                                     dict(ZSUM=True, WS=False, DB=True, DST=True, CX=1, NR=3, ZC=5),
                                     dict(ZSUM=True, IL=True, PK=True, AR=True, CX=2, NR=3, ZC=7),
-                                    dict(ZSUM=True, WS=False, IL=True, CX=1, NR=2, ZC=5)])
+                                    dict(ZSUM=True, WS=False, IL=True, CX=1, NR=2, ZC=5),
+                                    dict(ZSUM=True, PK=True, AR=True, ROWS=True, CX=2, NR=3, ZC=7),
+                                    dict(ZSUM=True, PK=True, AR=True, ROWS=True, WX=2, CX=2, NR=4, ZC=5, PD=2)])
 @pytest.mark.parametrize('case', _zsum_cases(), ids=lambda c: c[0])
 @pytest.mark.parametrize('bh', ['zeros', None])
 def test_zsum_schedule_vs_oracle(params, case, bh):
