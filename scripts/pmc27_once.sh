@@ -1,8 +1,14 @@
 set -u
+# SQ counter passes over the 27-point fp16 768^3 forward kernel (tune_march, one launch per config)
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp PSAD_CACHE_DIR=/tmp/psad_cache
 python -m pystencils_autodiff_amd.build > /dev/null || exit 3
-timeout -s KILL 60 rocprofv3 -L > gpurun_out/rocprof_avail.txt 2>&1 || true
-python scripts/tune_march.py --workload stencil27 --n 768 --rounds 1 --reps 1 --configs "default" > /dev/null 2>&1   # warm the code cache
+python scripts/tune_march.py --workload stencil27 --n 768 --rounds 1 --reps 1 --configs "${C:-default}" > /dev/null 2>&1   # warm the code cache
 cd /tmp
-timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/pmc27" -o pmc -- python "$GRAFT_REPO_ROOT/scripts/tune_march.py" --workload stencil27 --n 768 --rounds 1 --reps 1 --configs "${C:-default}" > "$GRAFT_REPO_ROOT/gpurun_out/pmc27.log" 2>&1
-echo rc=$?
+P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_BUSY_CYCLES"
+P2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_WAVES GRBM_GUI_ACTIVE"
+i=0
+for P in "$P1" "$P2"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/pmc27_$i" -o pmc -- python "$GRAFT_REPO_ROOT/scripts/tune_march.py" --workload stencil27 --n 768 --rounds 1 --reps 1 --configs "${C:-default}" > "$GRAFT_REPO_ROOT/gpurun_out/pmc27_$i.log" 2>&1 || exit $?
+done
+echo done
