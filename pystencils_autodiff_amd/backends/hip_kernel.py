@@ -79,7 +79,7 @@ def default_march_config(ir, ve, shape=None, tuning=None):
     for k, v in over.items():
         if k in ('CX', 'WX', 'NR', 'PD', 'WAVES', 'LDS_PAD', 'ZCT', 'ZMIN', 'ZMAX', 'BLK', 'D'):
             cfg[k] = int(v)
-        elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'LAZY', 'ZSUM', 'PK', 'ZU', 'PX', 'FASTLOAD', 'WS', 'AR', 'WSD', 'DST', 'DB', 'IL', 'ROWS'):
+        elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'LAZY', 'ZSUM', 'PK', 'ZU', 'PX', 'FASTLOAD', 'WS', 'AR', 'WSD', 'DST', 'DB', 'IL', 'ROWS', 'STSW'):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
         elif k == 'VIEW2D':
             cfg[k] = str(v)

@@ -343,7 +343,8 @@ def _zsum_cases():
                                     dict(ZSUM=True, IL=True, PK=True, AR=True, CX=2, NR=3, ZC=7),
                                     dict(ZSUM=True, WS=False, IL=True, CX=1, NR=2, ZC=5),
                                     dict(ZSUM=True, PK=True, AR=True, ROWS=True, CX=2, NR=3, ZC=7),
-                                    dict(ZSUM=True, PK=True, AR=True, ROWS=True, WX=2, CX=2, NR=4, ZC=5, PD=2)])
+                                    dict(ZSUM=True, PK=True, AR=True, ROWS=True, WX=2, CX=2, NR=4, ZC=5, PD=2),
+                                    dict(ZSUM=True, PK=True, AR=True, STSW=True, CX=2, NR=3, ZC=7)])
 @pytest.mark.parametrize('case', _zsum_cases(), ids=lambda c: c[0])
 @pytest.mark.parametrize('bh', ['zeros', None])
 def test_zsum_schedule_vs_oracle(params, case, bh):
