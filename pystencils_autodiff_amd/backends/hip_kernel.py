@@ -77,12 +77,14 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             k, v = kv.split('=')
             over[k.strip()] = v.strip() if k.strip() == 'VIEW2D' else int(v)
     for k, v in over.items():
-        if k in ('CX', 'WX', 'NR', 'PD', 'WAVES', 'LDS_PAD', 'ZCT', 'ZMIN', 'ZMAX', 'BLK', 'D'):
+        if k in ('CX', 'WX', 'NR', 'PD', 'WAVES', 'LDS_PAD', 'ZCT', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW'):
             cfg[k] = int(v)
         elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'LAZY', 'ZSUM', 'PK', 'ZU', 'PX', 'FASTLOAD', 'WS', 'AR', 'WSD', 'DST', 'DB', 'IL', 'ROWS', 'STSW'):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
         elif k == 'VIEW2D':
             cfg[k] = str(v)
+    if 'NW' in over and 'WX' not in over:
+        cfg['WX'] = min(cfg['WX'], cfg['NW'])
     if cfg['ZSUM'] and zsum_plan(ir, MarchConfig(VE=ve, **cfg)) is None:
         cfg['ZSUM'] = False                                    # not eligible: LDS ring instead
     if shape is not None:
@@ -95,7 +97,7 @@ def default_march_config(ir, ve, shape=None, tuning=None):
                 cfg['WX'] //= 2
         ny = int(shape[-2]) if ir.ndim == 3 or cfg['VIEW2D'] == 'yx' else 1
         if 'NR' not in over:
-            while cfg['NR'] > 1 and (4 // cfg['WX']) * cfg['NR'] // 2 >= ny:
+            while cfg['NR'] > 1 and (cfg.get('NW', 4) // cfg['WX']) * cfg['NR'] // 2 >= ny:
                 cfg['NR'] //= 2
     # LDS budget: two workgroups per CU (≤ 80 KB) for the register-prefetch defaults, the 160 KB hardware
     # limit for the LDS-DMA ring and for explicit tile overrides
@@ -421,7 +423,7 @@ class HipStencilKernel:
         kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics) + \
             [self._scalar_kind()] * len(ir.scalars)
         return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics,
-                     block=ws['block'] if ws else 256)
+                     block=ws['block'] if ws else cfg.NT)
 
 
 def _is_pair(z_range):

@@ -279,6 +279,7 @@ def test_vector_field_generic_schedule():
 @pytest.mark.parametrize('params', [
     dict(CX=4, NR=8, PD=2, NT_STORE=True), dict(CX=1, NR=1), dict(CX=2, WX=2, NR=3, PD=2),
     dict(CX=2, NR=4, FULL_RING=True), dict(CX=4, NR=8, ZC=5), dict(CX=1, WX=4, NR=2, PD=2, ZC=3),
+    dict(CX=2, NR=3, NW=1, ZC=4), dict(CX=1, WX=2, NW=2, NR=2, PD=2),
 ])
 @pytest.mark.parametrize('builder', [W.diffusion_7pt, W.asym_7pt, W.stencil_27pt])
 def test_march_tunings_vs_oracle(params, builder):
@@ -344,7 +345,9 @@ def _zsum_cases():
                                     dict(ZSUM=True, WS=False, IL=True, CX=1, NR=2, ZC=5),
                                     dict(ZSUM=True, PK=True, AR=True, ROWS=True, CX=2, NR=3, ZC=7),
                                     dict(ZSUM=True, PK=True, AR=True, ROWS=True, WX=2, CX=2, NR=4, ZC=5, PD=2),
-                                    dict(ZSUM=True, PK=True, AR=True, STSW=True, CX=2, NR=3, ZC=7)])
+                                    dict(ZSUM=True, PK=True, AR=True, STSW=True, CX=2, NR=3, ZC=7),
+                                    dict(ZSUM=True, WS=False, NW=1, CX=2, NR=3, ZC=5),
+                                    dict(ZSUM=True, WS=False, NW=2, WX=2, PK=True, AR=True, CX=2, NR=2, ZC=6)])
 @pytest.mark.parametrize('case', _zsum_cases(), ids=lambda c: c[0])
 @pytest.mark.parametrize('bh', ['zeros', None])
 def test_zsum_schedule_vs_oracle(params, case, bh):

@@ -214,3 +214,24 @@ def test_vector_field_zsum_compiles():
         g = march_geometry(k.ir, v[1])
         assert all(fg['C'] == 3 and fg['P'] == 3 * g['P'] for fg in g['FG'].values())
         assert _is_amdgpu_elf(rt.compile_hip(k.source(v)[0]))
+
+
+def test_waves_per_workgroup_option():
+    """NW (waves per workgroup) scales the block and the loaders' thread stride; WS keeps 4 + loader."""
+    import pytest
+    from pystencils_autodiff_amd import workloads as W
+    from pystencils_autodiff_amd.backends.hip_emitter import MarchConfig, emit_zsum, ws_geometry
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    import pystencils_autodiff_amd as pa
+    with pytest.raises(ValueError):
+        MarchConfig(NW=3)
+    with pytest.raises(ValueError):
+        MarchConfig(NW=1, WX=2)
+    op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
+    k = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='nw', target='gpu',
+                      gpu_indexing_params={'NW': 1}).compile()
+    cfg = k._march_cfg(k._vec_elems(), (64, 64, 256))
+    assert cfg.NW == 1 and cfg.WX == 1 and cfg.NT == 64 and cfg.TY == cfg.NR
+    src = emit_zsum(k.ir, 'nw_zsum', cfg)
+    assert '__launch_bounds__(64)' in src and 'tid + k * 64' in src and 'tid + k * 256' not in src
+    assert ws_geometry(k.ir, MarchConfig(VE=4, WS=True, ZSUM=True, NW=2, WX=1)) is None
