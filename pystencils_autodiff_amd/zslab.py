@@ -190,9 +190,11 @@ class ZSlabOp:
         rz = max([self._radius(k, f) for f in stencil] + [0])
         ref = kwargs[ir.fields_written[0].name]
         split = rz > 0 and dist.is_initialized() and dist.get_world_size(self.group) > 1
-        halo = self._rccl(ref.device) if split else None
-        if halo is None and rz > 0 and self._halo is not None and self._halo.loopback:
-            halo = self._halo                         # one-GPU loopback (tests, probes)
+        halo = None
+        if rz > 0 and self._halo is not None:
+            halo = self._halo                         # created by _rccl, or preset (loopback / emulation tests)
+        elif split:
+            halo = self._rccl(ref.device)
         if halo is not None:
             self._sweep_rccl(k, halo, stencil, rz, kwargs)
             return

@@ -23,6 +23,54 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _dtype(builder_name):
+    return np.float16 if builder_name == 'stencil_27pt' else np.float32
+
+
+class _GlooHalo:
+    """Stand-in for zslab.RcclHalo with RcclHalo's exchange contract (device pointers, peers, its own
+    stream) carried over gloo through host staging: drives ZSlabOp._sweep_rccl — peers, face
+    pointers, stream order, the two-range face launch — with 2-3 real ranks on one GPU, which RCCL
+    itself refuses."""
+    loopback = False
+
+    def __init__(self):
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.device = torch.device('cuda', torch.cuda.current_device())
+        self.stream = torch.cuda.Stream()
+
+    def exchange(self, planes, peer_lo, peer_hi):
+        from pystencils_autodiff_amd.backends import hip_runtime as rt
+        L, s = rt.lib(), self.stream.cuda_stream
+
+        def stage_out(ptr, n):
+            t = torch.empty(n, dtype=torch.uint8, device=self.device)
+            rt._check(L.psad_memcpy_d2d_async(t.data_ptr(), ptr, n, s), 'stage')
+            return t
+        self.stream.synchronize()          # the faces are final (the caller made this stream wait)
+        ops, recvs = [], []
+        for send_lo, recv_lo, send_hi, recv_hi, n in planes:
+            for peer, snd, rcv in ((peer_lo, send_lo, recv_lo), (peer_hi, send_hi, recv_hi)):
+                if peer < 0:
+                    continue
+                out = stage_out(snd, n)
+                self.stream.synchronize()
+                ops.append(dist.P2POp(dist.isend, out.cpu(), peer))
+                buf = torch.empty(n, dtype=torch.uint8)
+                ops.append(dist.P2POp(dist.irecv, buf, peer))
+                recvs.append((buf, rcv, n))
+        for w in dist.batch_isend_irecv(ops) if ops else []:
+            w.wait()
+        for buf, rcv, n in recvs:
+            d = buf.to(self.device)
+            torch.cuda.current_stream().synchronize()
+            rt._check(L.psad_memcpy_d2d_async(rcv, d.data_ptr(), n, s), 'unstage')
+        self.stream.synchronize()
+
+    def close(self):
+        pass
+
+
 def _worker(rank, world, port, shape, builder_name, use_cuda, result_dir):
     import sys
     sys.path.insert(0, ROOT)
@@ -34,8 +82,9 @@ def _worker(rank, world, port, shape, builder_name, use_cuda, result_dir):
         builder = getattr(W, builder_name)
         op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
         rng = np.random.default_rng(0)
-        u = rng.uniform(0, 1, shape).astype(np.float32)
-        d = rng.uniform(-1, 1, shape).astype(np.float32)
+        dt = _dtype(builder_name)
+        u = rng.uniform(0, 1, shape).astype(dt)
+        d = rng.uniform(-1, 1, shape).astype(dt)
         lo, hi = slab_bounds(shape[0], world, rank)
         dev = 'cuda' if use_cuda else 'cpu'
         ul = torch.from_numpy(u[lo:hi].copy()).to(dev)
@@ -43,6 +92,8 @@ def _worker(rank, world, port, shape, builder_name, use_cuda, result_dir):
         out = torch.zeros_like(ul)
         du = torch.zeros_like(ul)
         z = ZSlabOp(op, use_cuda=use_cuda)
+        if os.environ.get('PSAD_TEST_EMULATED_RCCL'):
+            z._halo = _GlooHalo()
         if os.environ.get('PSAD_TEST_ZSLAB_AUTOGRAD'):
             fn = z.autograd_function()
             uu = ul.clone().requires_grad_(True)
@@ -70,8 +121,9 @@ def _run(world, shape, builder_name, use_cuda, tmp_path):
     taps = {'diffusion_7pt': S.taps_diffusion_7pt(), 'asym_7pt': S.taps_asym_7pt(),
             'stencil_27pt': S.taps_27pt()}[builder_name]
     rng = np.random.default_rng(0)
-    u = rng.uniform(0, 1, shape).astype(np.float32)
-    d = rng.uniform(-1, 1, shape).astype(np.float32)
+    dt = _dtype(builder_name)
+    u = rng.uniform(0, 1, shape).astype(dt)
+    d = rng.uniform(-1, 1, shape).astype(dt)
     return out, du, S.linear_stencil(u, taps), S.linear_stencil(d, S.flip(taps))
 
 
@@ -178,3 +230,16 @@ def test_zslab_rccl_loopback_sweep(builder_name, shape):
         assert_close_rel(du.cpu().numpy().astype(np.float64), periodic(d, S.flip(taps)), tol, 'diffu')
     finally:
         z.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('world,shape', [(2, (24, 40, 64)), (3, (19, 33, 70)), (3, (7, 9, 64))])
+@pytest.mark.parametrize('builder_name', ['asym_7pt', 'stencil_27pt'])
+def test_zslab_rccl_sweep_emulated_ranks(world, shape, builder_name, tmp_path, monkeypatch):
+    """ZSlabOp's RCCL sweep with 2-3 ranks on one GPU, the exchange carried by _GlooHalo."""
+    from tests.conftest import assert_close_rel
+    monkeypatch.setenv('PSAD_TEST_EMULATED_RCCL', '1')
+    out, du, ref_out, ref_du = _run(world, shape, builder_name, True, tmp_path)
+    tol = 1e-3 if builder_name == 'stencil_27pt' else 1e-6
+    assert_close_rel(out, ref_out, tol, 'out')
+    assert_close_rel(du, ref_du, tol, 'diffu')
