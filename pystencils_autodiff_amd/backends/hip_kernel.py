@@ -77,7 +77,7 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             k, v = kv.split('=')
             over[k.strip()] = v.strip() if k.strip() == 'VIEW2D' else int(v)
     for k, v in over.items():
-        if k in ('CX', 'WX', 'NR', 'PD', 'WAVES', 'LDS_PAD', 'ZCT', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW'):
+        if k in ('CX', 'WX', 'NR', 'PD', 'WAVES', 'LDS_PAD', 'ZCT', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'DMA_AUX'):
             cfg[k] = int(v)
         elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'LAZY', 'ZSUM', 'PK', 'ZU', 'PX', 'FASTLOAD', 'WS', 'AR', 'WSD', 'DST', 'DB', 'IL', 'ROWS', 'STSW'):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
@@ -91,6 +91,11 @@ def default_march_config(ir, ve, shape=None, tuning=None):
         X = int(shape[-1])
         if 'CX' not in over:
             while cfg['CX'] > 1 and 64 * cfg['CX'] * cfg['WX'] // 2 >= X:
+                cfg['CX'] //= 2
+            tx = 64 * cfg['CX'] * cfg['WX']
+            if cfg.get('WS') and cfg['CX'] > 1 and -(-X // (tx // 2)) * (tx // 2) < -(-X // tx) * tx:
+                # WS tiles: half width when it pads x less (384³ 7-point: 0.116 → 0.081 ms with 48-plane
+                # chunks, profiles/r01_tune_odd_sizes.log)
                 cfg['CX'] //= 2
         if 'WX' not in over:
             while cfg['WX'] > 1 and 64 * cfg['CX'] * cfg['WX'] // 2 >= X:
@@ -327,8 +332,38 @@ class HipStencilKernel:
         blocks = max(1, min(math.ceil(ncell / 256), 256 * 64)) if ncell > 0 else 0
         return _Plan(variant, fn, blocks, kinds, len(tensors), 0, statics)
 
-    def march_launch_geometry(self, shape, cfg, z_range=None):
-        """(Z, Y, X), bounds and grid of the march schedule for a field shape."""
+    def _resident_slots(self, fn, block, device):
+        """Workgroups of this kernel resident on the whole GPU at once (LDS, VGPR and wave limits per CU
+        × CU count), from the loaded code object's attributes."""
+        torch = _torch()
+        a = rt.function_attributes(fn)
+        regs, lds = a['num_regs'], a['shared_bytes']
+        waves = -(-block // 64)
+        per_simd = max(1, min(8, 512 // max(8, -(-regs // 8) * 8)))
+        per_cu = max(1, min(4 * per_simd // waves, 163840 // max(1, lds), 32 // waves))
+        return per_cu * torch.cuda.get_device_properties(device).multi_processor_count
+
+    @staticmethod
+    def quantized_chunk(nz, nt, slots, zmin, zmax, rz, wsat):
+        """Chunk length for the WS schedule (few resident workgroups, each with a fixed number of bytes
+        in flight): the chunk count c minimising Σ_rounds (planes per chunk + halo + fill) ·
+        max(1, active / wsat) — a round takes at least one workgroup's march (latency bound below
+        ``wsat`` concurrent workgroups, bandwidth bound above). The short last round of 128-plane
+        chunks is what makes 768³ slower per cell than 1024³ (profiles/r01_tune_odd_sizes.log)."""
+        best = None
+        c0 = max(1, -(-nz // zmax))
+        for c in range(c0, max(c0, nz // max(1, zmin)) + 1):
+            zc = -(-nz // c)
+            n = nt * -(-nz // zc)
+            full, rem = divmod(n, slots)
+            t = (zc + 2 * rz + 2) * (full * max(1.0, slots / wsat) + (max(1.0, rem / wsat) if rem else 0.0))
+            if best is None or t < best[0] - 1e-9:
+                best = (t, zc)
+        return best[1]
+
+    def march_launch_geometry(self, shape, cfg, z_range=None, slots=None):
+        """(Z, Y, X), bounds and grid of the march schedule for a field shape; ``slots`` = resident
+        workgroups (``_resident_slots``) switches the WS schedule to quantisation-aware chunks."""
         ir = self.ir
         bounds = ir.iteration_bounds(shape)
         if z_range is not None and _is_pair(z_range):
@@ -370,6 +405,14 @@ class HipStencilKernel:
         target = int(self.kernel.tuning.get('BLOCKS', os.environ.get('PSAD_MARCH_BLOCKS', cfg.BLK)))
         zc = self.kernel.tuning.get('ZC') or int(os.environ.get('PSAD_MARCH_ZC', 0)) or cfg.ZCT or \
             min(nz, max(cfg.ZMIN, min(cfg.ZMAX, math.ceil(nz * nt / target))))
+        explicit = self.kernel.tuning.get('ZC') or os.environ.get('PSAD_MARCH_ZC') or cfg.ZCT or \
+            'BLOCKS' in self.kernel.tuning or os.environ.get('PSAD_MARCH_BLOCKS')
+        if slots and cfg.WS and nz and not explicit:
+            ws = ws_geometry(ir, cfg)
+            cus = _torch().cuda.get_device_properties(_torch().cuda.current_device()).multi_processor_count
+            # workgroups that saturate HBM: ~64 KiB in flight per CU (one 256×16 fp32 ring of 4 planes)
+            wsat = max(cus, math.ceil(cus * 65536 / (ws['D'] * ws['per_plane'] * 1024)))
+            zc = self.quantized_chunk(nz, nt, slots, cfg.ZMIN, cfg.ZMAX, march_geometry(ir, cfg)['RZ'], wsat)
         zc = min(zc, nz) if nz else zc
         zc = max(zc, min(nz, 4 * max(1, march_geometry(ir, cfg)['RZ'])))
         nchunks = math.ceil(nz / zc) if nz else 0
@@ -404,7 +447,9 @@ class HipStencilKernel:
             cfg = MarchConfig(**{**cfg.__dict__, 'WS': False})
         variant = ('march', cfg)
         fn = self.function(variant, device)
-        geo = self.march_launch_geometry(shape, cfg, z_range)
+        ws = ws_geometry(ir, cfg)
+        slots = self._resident_slots(fn, ws['block'], device) if ws else None
+        geo = self.march_launch_geometry(shape, cfg, z_range, slots=slots)
         grid = geo['grid'] if geo['yhi'] > geo['ylo'] and geo['xhi'] > geo['xlo'] else 0
         rz = march_geometry(ir, cfg)['RZ']
         plane = geo['Y'] * geo['X']
@@ -417,7 +462,6 @@ class HipStencilKernel:
                                      "on the field's device")
         if max(geo['Z'], geo['Y'], geo['X']) >= 2 ** 31 or grid >= 2 ** 31:
             raise ValueError('field extent too large for the march schedule')
-        ws = ws_geometry(ir, cfg)
         statics = [int(geo[k]) for k in ('Z', 'Y', 'X', 'zlo', 'zhi', 'ylo', 'yhi', 'xlo', 'xhi', 'zc', 'zstep', 'ntx',
                                           'nty')]
         kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics) + \

@@ -150,7 +150,8 @@ def main():
     for i, c in enumerate(cfgs):
         ts = sorted(times[i])
         med = ts[len(ts) // 2]
-        geo = kernels[i].march_launch_geometry(shape[:3] if len(shape) >= 3 else shape, kernels[i].last_variant[1])
+        plan = list(kernels[i]._plans.values())[-1]          # the launch actually timed
+        geo = {'grid': plan.grid, 'zc': plan.statics[9]}
         print(f"tune{i:<3d} {','.join(f'{k}={v}' for k, v in c.items()) or 'default':34s} median {med:.4f} ms  min {ts[0]:.4f} ms  "
               f"{alg / (med * 1e-3) / 1e9:7.0f} GB/s  grid {geo['grid']} zc {geo['zc']}  maxdiff_vs_generic {maxdiff[i]:.2e}")
     sys.stdout.flush()
