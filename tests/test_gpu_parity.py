@@ -777,3 +777,17 @@ def test_vector_field_halos_and_two_range_launches():
         outs.append(out)
     torch.cuda.synchronize()
     assert torch.equal(torch.cat(outs), full)
+
+
+@pytest.mark.parametrize('shape', [(100, 40, 384), (37, 24, 640), (130, 17, 768)])
+def test_ws_residency_chunking_shapes_vs_oracle(shape):
+    """Default 7-point op at x extents that trigger half-width WS tiles / residency-aware chunk counts."""
+    g = np.random.default_rng(sum(shape))
+    u = g.uniform(0, 1, shape).astype(np.float32)
+    d = g.uniform(-1, 1, shape).astype(np.float32)
+    op, fn = _op(W.asym_7pt())
+    (out,), (du,) = _run(fn, [u], [d])
+    taps = S.taps_asym_7pt()
+    assert_close_rel(out, S.linear_stencil(u, taps), 1e-6, 'out')
+    assert_close_rel(du, S.linear_stencil(d, S.flip(taps)), 1e-6, 'diffu')
+    assert op.forward_ast_gpu.compile().last_variant[1].WS

@@ -235,3 +235,14 @@ def test_waves_per_workgroup_option():
     src = emit_zsum(k.ir, 'nw_zsum', cfg)
     assert '__launch_bounds__(64)' in src and 'tid + k * 64' in src and 'tid + k * 256' not in src
     assert ws_geometry(k.ir, MarchConfig(VE=4, WS=True, ZSUM=True, NW=2, WX=1)) is None
+
+
+def test_quantized_chunk_model():
+    """WS chunk count: power-of-two cubes / 1024² slabs keep 128-plane chunks; 768³ avoids a short last round."""
+    from pystencils_autodiff_amd.backends.hip_kernel import HipStencilKernel
+    q = HipStencilKernel.quantized_chunk
+    assert q(1024, 256, 256, 32, 128, 1, 256) == 128
+    assert q(512, 64, 256, 32, 128, 1, 256) == 128
+    assert q(128, 256, 256, 32, 128, 1, 256) == 128
+    assert q(768, 144, 256, 32, 128, 1, 256) == 110
+    assert q(5, 7, 256, 32, 128, 1, 256) == 5
