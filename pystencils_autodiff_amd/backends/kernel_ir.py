@@ -26,6 +26,8 @@ import hashlib
 from dataclasses import dataclass, field as dc_field
 from typing import Dict, List, Tuple
 
+import itertools
+
 import numpy as np
 import sympy as sp
 
@@ -161,6 +163,22 @@ def lower(assignments, boundary_handling=None, data_type=None):
 
     radius = tuple(max([abs(int(r.offsets[d])) for r in reads] + [0]) for d in range(ndim))
     ghost_layers = max([max([abs(int(o)) for o in offs] + [0]) for offs in all_accesses] + [0])
+    if zeros or ghost_layers == 0:
+        # components of a vector output that no assignment writes are the zeros of the reference's
+        # torch.zeros allocation (_torch_native.py:61-73); with every cell written they become zero
+        # stores, so the output is allocated uninitialised and written in one pass (no memset sweep)
+        read_names = {r.field.name for r in reads}
+        for f in fields_written:
+            if not f.index_dimensions or f.name in read_names:
+                continue
+            mine = [st for st in stores if st[0] == f]
+            offs = {st[1] for st in mine}
+            written = {st[2] for st in mine}
+            if len(offs) == 1:
+                off = next(iter(offs))
+                for idx in itertools.product(*[range(int(n)) for n in f.index_shape]):
+                    if idx not in written:
+                        stores.append((f, off, idx, sp.Integer(0)))
 
     dtypes = {f.dtype.numpy_dtype for f in fields}
     if data_type is not None:
