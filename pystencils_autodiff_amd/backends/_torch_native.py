@@ -15,8 +15,8 @@ Same contract as the reference's ``backends/_torch_native.py:10-142``:
 Differences, all deliberate: kernels run on torch's current HIP stream
 (not the legacy default stream); outputs every cell of which the kernel writes
 are allocated with ``torch.empty`` (the reference memsets with ``torch.zeros``,
-an extra HBM pass) — ``boundary_handling=None`` keeps ``torch.zeros`` because the
-border is not written; only tensors the backward kernel reads are saved on
+an extra HBM pass); with ``boundary_handling=None`` only the untouched border slabs
+are zero-filled (``_allocator``); only tensors the backward kernel reads are saved on
 ``ctx``; gradients are returned in forward-input order with ``None`` for
 constant fields; native errors raise ``RuntimeError`` instead of ``exit()``.
 On ``use_cuda=True`` there is no CPU fallback: a missing HIP extension raises.
@@ -74,12 +74,8 @@ class _Wrapper:
         return [_Parameter(p.symbol.name, p.field) for p in self._kernel.get_parameters()]
 
 
-def _full_write(kernel, field_name=None):
-    """True if the kernel writes every cell of its outputs (no untouched border) and, for the given output
-    (all outputs if None), every component of a vector field — else the output keeps the reference's
-    ``torch.zeros`` allocation (``_torch_native.py:64,108``)."""
-    if not (kernel.ir.zeros or kernel.ir.ghost_layers == 0):
-        return False
+def _components_complete(kernel, field_name=None):
+    """Every component of the given vector output (all outputs if None) is assigned."""
     import itertools
     for f in kernel.ir.fields_written:
         if field_name is not None and f.name != field_name:
@@ -89,6 +85,63 @@ def _full_write(kernel, field_name=None):
             if written != set(itertools.product(*[range(int(n)) for n in f.index_shape])):
                 return False
     return True
+
+
+def _full_write(kernel, field_name=None):
+    """True if the kernel writes every cell of its outputs (no untouched border) and, for the given output
+    (all outputs if None), every component of a vector field — else the output keeps the reference's
+    ``torch.zeros`` allocation (``_torch_native.py:64,108``)."""
+    if not (kernel.ir.zeros or kernel.ir.ghost_layers == 0):
+        return False
+    return _components_complete(kernel, field_name)
+
+
+# CPU: below this many elements one memset is cheaper than 2·ndim border fills
+BORDER_ZERO_MIN = 1 << 22
+# GPU: zero the border with one hiprtc kernel (hip_kernel.zero_border) instead of a full memset
+BORDER_KERNEL = True
+
+
+def _allocator(kernel, field_name, read_names=()):
+    """How an output is allocated: ``torch.empty`` when the kernel writes all of it; for an interior-only
+    kernel (``boundary_handling=None``, the reference's default) that assigns every component at offset 0,
+    ``torch.empty`` plus zero fills of the untouched border slabs — the reference's ``torch.zeros``
+    values without a memset pass over the whole field; otherwise ``torch.zeros``."""
+    import torch
+    if field_name in read_names:
+        return torch.zeros
+    if _full_write(kernel, field_name):
+        return torch.empty
+    ir = kernel.ir
+    if not _components_complete(kernel, field_name) or \
+            any(any(o != 0 for o in off) for fld, off, _, _ in ir.stores if fld.name == field_name):
+        return torch.zeros
+    sdim = ir.ndim
+
+    ncomp = 1
+    for f in ir.fields_written:
+        if f.name == field_name:
+            for n in (f.index_shape if f.index_dimensions else ()):
+                ncomp *= int(n)
+
+    def alloc(shape, dtype, device):
+        t = torch.empty(shape, dtype=dtype, device=device)
+        if t.is_cuda:
+            if not BORDER_KERNEL:
+                return t.zero_()
+            from .hip_kernel import zero_border
+            zero_border(t, ir.iteration_bounds(tuple(shape[:sdim])), ncomp)
+            return t
+        if t.numel() < BORDER_ZERO_MIN:
+            return t.zero_()
+        for d, (lo, hi) in enumerate(ir.iteration_bounds(tuple(shape[:sdim]))):
+            n = int(shape[d])
+            if lo > 0:
+                t.narrow(d, 0, min(lo, n)).zero_()
+            if hi < n:
+                t.narrow(d, hi, n - hi).zero_()
+        return t
+    return alloc
 
 
 def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
@@ -139,7 +192,8 @@ def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
     def _index_shape(field):
         return tuple(int(n) for n in field.index_shape) if field.index_dimensions else ()
 
-    fwd_out = [(f.name, _tdtype(f), _fixed(f), torch.empty if _full_write(forward_kernel, f.name) else torch.zeros,
+    fwd_reads = {r.field.name for r in forward_kernel.ir.reads}
+    fwd_out = [(f.name, _tdtype(f), _fixed(f), _allocator(forward_kernel, f.name, fwd_reads),
                 f.spatial_dimensions, _index_shape(f)) for f in fwd_outputs]
     fwd_scalars = [s.name for s in forward_kernel.ir.scalars]
     saved_fwd = [n for n in [f.name for f in fwd_inputs] + [f.name for f in fwd_outputs] if n in bwd_kernel_fields]
@@ -152,8 +206,7 @@ def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
             grad_specs.append((a.name if a is not None and a.name in bwd_kernel_fields else None, _tdtype(f),
                                _fixed(a) if a is not None else None,
                                tuple(a.strides) if a is not None and a.has_fixed_shape else None, f.name))
-        bwd_out = [(f.name, _tdtype(f), _fixed(f),
-                    torch.empty if _full_write(backward_kernel, f.name) and f.name not in bwd_reads else torch.zeros,
+        bwd_out = [(f.name, _tdtype(f), _fixed(f), _allocator(backward_kernel, f.name, bwd_reads),
                     f.spatial_dimensions, _index_shape(f)) for f in bwd_outputs]
         in_adj = [adj_of[f.name].name if adj_of.get(f.name) is not None else None for f in fwd_inputs]
 

@@ -506,3 +506,40 @@ class _Plan:
 
     def pack(self, ptrs, hptrs, scalars):
         return self.struct.pack(*ptrs, *(hptrs if hptrs else [0] * self.n_halo), *self.statics, *scalars)
+
+
+_zero_border_fns = {}
+
+
+def zero_border(t, bounds, ncomp=1, stream=None):
+    """Zero, in one launch on the current stream, every cell of the contiguous GPU tensor ``t`` outside the
+    per-axis ``[lo, hi)`` ``bounds`` of its spatial axes (components, if any, last) — the border an
+    interior-only kernel leaves to the reference's ``torch.zeros`` allocation."""
+    import struct
+    torch = _torch()
+    from .hip_emitter import emit_zero_border
+    nd = len(bounds)
+    shape = [int(s) for s in t.shape[:nd]]
+    bounds = [(int(a), int(b)) for a, b in bounds]
+    while len(shape) < 3:
+        shape.insert(0, 1)
+        bounds.insert(0, (0, 1))
+    (zlo, zhi), (ylo, yhi), (xlo, xhi) = bounds
+    Z, Y, X = shape
+    L = X * ncomp
+    total = (Z - (zhi - zlo)) * Y * L + (zhi - zlo) * (Y - (yhi - ylo)) * L + \
+        (zhi - zlo) * (yhi - ylo) * (L - (xhi - xlo) * ncomp)
+    if total <= 0:
+        return
+    if not t.is_contiguous() or t.numel() != Z * Y * L:
+        raise ValueError('zero_border needs a contiguous tensor of the kernel shape')
+    device = t.device.index
+    key = (t.element_size(), device)
+    fn = _zero_border_fns.get(key)
+    if fn is None:
+        src, name = emit_zero_border(t.element_size())
+        fn = _zero_border_fns[key] = rt.load_function(rt.compile_hip(src), name, device)
+    if stream is None:
+        stream = torch._C._cuda_getCurrentRawStream(device)
+    args = struct.pack('<Q9q', t.data_ptr(), Z, Y, L, zlo, zhi, ylo, yhi, xlo * ncomp, xhi * ncomp)
+    rt.launch(fn, (min(math.ceil(total / 256), 256 * 64),), (256,), args, stream)

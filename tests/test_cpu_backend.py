@@ -266,3 +266,29 @@ def test_create_forward_backward_kernel_like_reference():
     kb(diffout=u, diffu=du)
     assert_close_rel(du, OE.evaluate(op.backward_assignments, {'diffout': u}, boundary_handling='zeros')['diffu'],
                      1e-6, 'backward')
+
+
+@pytest.mark.parametrize('bmin', [0, 1 << 30])
+@pytest.mark.parametrize('builder', [W.asym_7pt, W.stencil_27pt])
+def test_interior_only_border_allocation(monkeypatch, bmin, builder):
+    """boundary_handling=None (the reference default): outputs are torch.empty + zeroed border slabs
+    (BORDER_ZERO_MIN=0) or one memset; uninitialised memory is poisoned with NaN so a missed border
+    cell shows up."""
+    from pystencils_autodiff_amd.backends import _torch_native as TN
+    monkeypatch.setattr(TN, 'BORDER_ZERO_MIN', bmin)
+    empty = torch.empty
+    monkeypatch.setattr(torch, 'empty', lambda *a, **k: empty(*a, **k).fill_(float('nan')))
+    op = pa.AutoDiffOp(builder(), boundary_handling=None)
+    fn = op.create_tensorflow_op(use_cuda=False, backend='torch_native')
+    rng = np.random.default_rng(4)
+    dt = np.float16 if builder is W.stencil_27pt else np.float32
+    u = rng.uniform(-1, 1, (7, 9, 12)).astype(dt)
+    d = rng.uniform(-1, 1, (7, 9, 12)).astype(dt)
+    uu = torch.from_numpy(u).requires_grad_(True)
+    (o,) = fn.apply(uu)
+    o.backward(torch.from_numpy(d))
+    tol = 1e-3 if dt == np.float16 else 1e-6
+    ref = OE.evaluate(op.forward_assignments, {'u': u}, boundary_handling=None)['out']
+    refb = OE.evaluate(op.backward_assignments, {'diffout': d}, boundary_handling=None)['diffu']
+    assert_close_rel(o.detach().numpy(), ref, tol, 'out')
+    assert_close_rel(uu.grad.numpy(), refb, tol, 'diffu')

@@ -791,3 +791,25 @@ def test_ws_residency_chunking_shapes_vs_oracle(shape):
     assert_close_rel(out, S.linear_stencil(u, taps), 1e-6, 'out')
     assert_close_rel(du, S.linear_stencil(d, S.flip(taps)), 1e-6, 'diffu')
     assert op.forward_ast_gpu.compile().last_variant[1].WS
+
+
+@pytest.mark.parametrize('bmin', [0, 1 << 30])
+@pytest.mark.parametrize('builder,shape', [(W.asym_7pt, (20, 33, 70)), (W.stencil_27pt, (9, 24, 80)),
+                                           (W.laplace_5pt, (40, 70))])
+def test_interior_only_border_allocation_gpu(monkeypatch, bmin, builder, shape):
+    """boundary_handling=None: torch.empty outputs with zeroed border slabs (or one memset) on the GPU;
+    uninitialised memory poisoned with NaN."""
+    from pystencils_autodiff_amd.backends import _torch_native as TN
+    monkeypatch.setattr(TN, 'BORDER_KERNEL', bmin == 0)
+    empty = torch.empty
+    monkeypatch.setattr(torch, 'empty', lambda *a, **k: empty(*a, **k).fill_(float('nan')))
+    op, fn = _op(builder(), None)
+    g = np.random.default_rng(6)
+    dt = np.float16 if builder is W.stencil_27pt else np.float32
+    u = g.uniform(-1, 1, shape).astype(dt)
+    d = g.uniform(-1, 1, shape).astype(dt)
+    (out,), (du,) = _run(fn, [u], [d])
+    tol = 1e-3 if dt == np.float16 else 1e-6
+    assert_close_rel(out, OE.evaluate(op.forward_assignments, {'u': u}, boundary_handling=None)['out'], tol, 'out')
+    assert_close_rel(du, OE.evaluate(op.backward_assignments, {'diffout': d}, boundary_handling=None)['diffu'],
+                     tol, 'diffu')
