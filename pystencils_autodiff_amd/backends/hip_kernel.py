@@ -534,10 +534,11 @@ def zero_border(t, bounds, ncomp=1, stream=None):
     if not t.is_contiguous() or t.numel() != Z * Y * L:
         raise ValueError('zero_border needs a contiguous tensor of the kernel shape')
     device = t.device.index
-    key = (t.element_size(), device)
+    idx32 = Z * Y * L + 256 * 256 * 64 < 2 ** 31
+    key = (t.element_size(), idx32, device)
     fn = _zero_border_fns.get(key)
     if fn is None:
-        src, name = emit_zero_border(t.element_size())
+        src, name = emit_zero_border(t.element_size(), idx32)
         fn = _zero_border_fns[key] = rt.load_function(rt.compile_hip(src), name, device)
     if stream is None:
         stream = torch._C._cuda_getCurrentRawStream(device)
