@@ -124,13 +124,18 @@ def _allocator(kernel, field_name, read_names=()):
             for n in (f.index_shape if f.index_dimensions else ()):
                 ncomp *= int(n)
 
-    def alloc(shape, dtype, device):
+    def alloc(shape, dtype, device, pending=None):
         t = torch.empty(shape, dtype=dtype, device=device)
         if t.is_cuda:
             if not BORDER_KERNEL:
                 return t.zero_()
             from .hip_kernel import zero_border
-            zero_border(t, ir.iteration_bounds(tuple(shape[:sdim])), ncomp)
+            bounds = ir.iteration_bounds(tuple(shape[:sdim]))
+            # the x ends of the interior rows are left to the kernel's x_border stores (or, if its launch
+            # cannot, to a second fill after it: ``pending``)
+            zero_border(t, bounds, ncomp, x=pending is None)
+            if pending is not None:
+                pending.append(lambda: zero_border(t, bounds, ncomp, zy=False))
             return t
         if t.numel() < BORDER_ZERO_MIN:
             return t.zero_()
@@ -141,7 +146,22 @@ def _allocator(kernel, field_name, read_names=()):
             if hi < n:
                 t.narrow(d, hi, n - hi).zero_()
         return t
+    alloc.border = True
     return alloc
+
+
+def _border_kw(alloc, pending):
+    return {'pending': pending} if getattr(alloc, 'border', False) else {}
+
+
+def _launch(call, kwargs, pending):
+    """Launch; when outputs have a zeroed border (``_allocator``), ask the kernel to store the x ends of
+    its rows too (``x_border``) and fill them separately only if its schedule cannot."""
+    if not pending:
+        call(**kwargs)
+    elif not call(x_border=True, **kwargs):
+        for fill in pending:
+            fill()
 
 
 def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
@@ -234,14 +254,15 @@ def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
                 raise TypeError(f"{op_name}: scalar parameter '{name}' missing: set {op_name}.class_kwargs['{name}']")
             kwargs[name] = class_kwargs[name]
         outputs = []
+        pending = []
         for name, dtype, fixed, alloc, sdim, ishape in fwd_out:
             # variable-size outputs: the first input's spatial extent plus the output's own index shape (the
             # reference takes the first input's whole shape, _torch_native.py:66-72)
             t = alloc(fixed if fixed is not None else tuple(first.shape[:sdim]) + ishape, dtype=dtype,
-                      device=first.device)
+                      device=first.device, **_border_kw(alloc, pending))
             kwargs[name] = t
             outputs.append(t)
-        fwd_call(**kwargs)
+        _launch(fwd_call, kwargs, pending)
         ctx.saved_names = [n for n in saved_fwd if n in kwargs]
         ctx.save_for_backward(*[kwargs[n] for n in ctx.saved_names])
         ctx.scalars = dict(class_kwargs)
@@ -270,12 +291,13 @@ def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
                 kwargs[aname] = g
             like = g if like is None else like
         result = {}
+        pending = []
         for name, dtype, fixed, alloc, sdim, ishape in bwd_out:
             t = alloc(fixed if fixed is not None else tuple(like.shape[:sdim]) + ishape, dtype=dtype,
-                      device=like.device)
+                      device=like.device, **_border_kw(alloc, pending))
             result[name] = t
             kwargs[name] = t
-        bwd_call(**kwargs)
+        _launch(bwd_call, kwargs, pending)
         return tuple(result.get(a) if a is not None else None for a in in_adj[:ctx.n_inputs]) + \
             (None,) * max(0, ctx.n_inputs - len(in_adj))
 

@@ -211,10 +211,11 @@ class HipStencilKernel:
                             tuple(int(x) for x in f.shape) if f.has_fixed_shape else None) for f in self.ir.fields]
         return self._specs
 
-    def __call__(self, halos=None, stream=None, force_schedule=None, z_range=None, **kwargs):
+    def __call__(self, halos=None, stream=None, force_schedule=None, z_range=None, x_border=False, **kwargs):
         """Launch on the field tensors / scalars given by name.
 
-        ``halos`` = ``{field: (lo_planes, hi_planes)}``: tensors holding the RZ planes just
+        ``x_border=True`` asks the zsum schedule to also store zeros at x outside the iteration bounds of
+        the rows it writes (returns True if the launch did). ``halos`` = ``{field: (lo_planes, hi_planes)}``: tensors holding the RZ planes just
         below plane 0 / above plane Z-1 of a stencil field (``None`` = zeros); ``z_range``
         restricts the written planes of axis 0 — ``(lo, hi)``, or two disjoint ranges of equal
         length ``((lo0, hi0), (lo1, hi1))`` written by ONE launch (the two slab faces; both:
@@ -264,18 +265,19 @@ class HipStencilKernel:
         contiguous = all(t.is_contiguous() for t in tensors)
         strides = None if contiguous else tuple(tuple(t.stride()) for t in tensors)
         align = tuple(p % 32 == 0 for p in ptrs + hptrs)
-        key = (force_schedule, shape, strides, align, tuple(h is not None for h in halo_list),
+        key = (force_schedule, bool(x_border), shape, strides, align, tuple(h is not None for h in halo_list),
                _zkey(z_range), device)
         plan = self._plans.get(key)
         if plan is None:
-            plan = self._make_plan(tensors, halo_list, shape, device, contiguous, force_schedule, z_range)
+            plan = self._make_plan(tensors, halo_list, shape, device, contiguous, force_schedule, z_range, x_border)
             self._plans[key] = plan
         self.last_variant = plan.variant
         if plan.grid == 0:
-            return
+            return plan.xb
         rt.launch(plan.fn, (plan.grid,), (plan.block,), plan.pack(ptrs, hptrs, scalars), stream)
+        return plan.xb
 
-    def _make_plan(self, tensors, halo_list, shape, device, contiguous, force_schedule, z_range):
+    def _make_plan(self, tensors, halo_list, shape, device, contiguous, force_schedule, z_range, x_border=False):
         torch = _torch()
         ir = self.ir
         sched = force_schedule or self.schedule()
@@ -287,7 +289,7 @@ class HipStencilKernel:
             if sched == 'pointwise':
                 return self._plan_pointwise(tensors, shape, device)
             if sched == 'march':
-                return self._plan_march(tensors, halo_list, shape, device, z_range)
+                return self._plan_march(tensors, halo_list, shape, device, z_range, x_border)
             return self._plan_generic(tensors, shape, device)
 
     def _scalar_kind(self):
@@ -395,7 +397,7 @@ class HipStencilKernel:
             Y = 1
             (zlo, zhi), (xlo, xhi) = bounds
             ylo, yhi = 0, 1
-        ntx = max(1, math.ceil(xhi / cfg.TX))
+        ntx = max(1, math.ceil((X if cfg.XB else xhi) / cfg.TX))
         nty = max(1, math.ceil(yhi / cfg.TY))
         nt = ntx * nty
         nz = max(0, zhi - zlo)
@@ -423,7 +425,7 @@ class HipStencilKernel:
         return dict(Z=Z, Y=Y, X=X, zlo=zlo, zhi=zhi, ylo=ylo, yhi=yhi, xlo=xlo, xhi=xhi, zc=zc, zstep=zc,
                     ntx=ntx, nty=nty, grid=nt * nchunks)
 
-    def _plan_march(self, tensors, halo_list, shape, device, z_range):
+    def _plan_march(self, tensors, halo_list, shape, device, z_range, x_border=False):
         torch = _torch()
         ir = self.ir
         ve = self._vec_elems()
@@ -445,6 +447,10 @@ class HipStencilKernel:
         if ws and int(np.prod(shape[1:])) * cmax * max(ws['esize'], ws.get('ssize', 0)) >= 2 ** 31 - 1024:
             # planes beyond the loader's 32-bit buffer offsets: register-prefetch form of the same schedule
             cfg = MarchConfig(**{**cfg.__dict__, 'WS': False})
+        xlo, xhi = ir.iteration_bounds(shape)[-1]
+        if x_border and cfg.ZSUM and not cfg.PX and (xlo > 0 or xhi < shape[-1]) and \
+                not (ir.ndim == 2 and cfg.VIEW2D == 'zy'):
+            cfg = MarchConfig(**{**cfg.__dict__, 'XB': True})
         variant = ('march', cfg)
         fn = self.function(variant, device)
         ws = ws_geometry(ir, cfg)
@@ -466,7 +472,7 @@ class HipStencilKernel:
                                           'nty')]
         kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics) + \
             [self._scalar_kind()] * len(ir.scalars)
-        return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics,
+        return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics, xb=cfg.XB,
                      block=ws['block'] if ws else cfg.NT)
 
 
@@ -486,12 +492,13 @@ class _Plan:
 
     _CODES = {'ptr': ('Q', 8), 'i32': ('i', 4), 'u32': ('I', 4), 'i64': ('q', 8), 'f32': ('f', 4), 'f64': ('d', 8)}
 
-    def __init__(self, variant, fn, grid, kinds, n_ptr, n_halo, statics, block=256):
+    def __init__(self, variant, fn, grid, kinds, n_ptr, n_halo, statics, block=256, xb=False):
         import struct
         self.variant = variant
         self.fn = fn
         self.grid = grid
         self.block = block
+        self.xb = xb                     # the launch also zeroes x outside the iteration bounds
         fmt, off = '<', 0
         for k in kinds:
             c, size = self._CODES[k]
@@ -511,16 +518,21 @@ class _Plan:
 _zero_border_fns = {}
 
 
-def zero_border(t, bounds, ncomp=1, stream=None):
+def zero_border(t, bounds, ncomp=1, stream=None, x=True, zy=True):
     """Zero, in one launch on the current stream, every cell of the contiguous GPU tensor ``t`` outside the
     per-axis ``[lo, hi)`` ``bounds`` of its spatial axes (components, if any, last) — the border an
-    interior-only kernel leaves to the reference's ``torch.zeros`` allocation."""
+    interior-only kernel leaves to the reference's ``torch.zeros`` allocation. ``x=False`` leaves the x
+    ends of the rows (written by an ``x_border`` launch), ``zy=False`` does only those."""
     import struct
     torch = _torch()
     from .hip_emitter import emit_zero_border
     nd = len(bounds)
     shape = [int(s) for s in t.shape[:nd]]
     bounds = [(int(a), int(b)) for a, b in bounds]
+    if not x:
+        bounds[-1] = (0, shape[-1])
+    if not zy:
+        bounds[:-1] = [(0, n) for n in shape[:-1]]
     while len(shape) < 3:
         shape.insert(0, 1)
         bounds.insert(0, (0, 1))

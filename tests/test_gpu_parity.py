@@ -795,7 +795,8 @@ def test_ws_residency_chunking_shapes_vs_oracle(shape):
 
 @pytest.mark.parametrize('bmin', [0, 1 << 30])
 @pytest.mark.parametrize('builder,shape', [(W.asym_7pt, (20, 33, 70)), (W.stencil_27pt, (9, 24, 80)),
-                                           (W.laplace_5pt, (40, 70))])
+                                           (W.laplace_5pt, (40, 70)), (W.asym_7pt, (6, 9, 300)),
+                                           (W.vector_laplace_7pt, (7, 10, 40, 3))])
 def test_interior_only_border_allocation_gpu(monkeypatch, bmin, builder, shape):
     """boundary_handling=None: torch.empty outputs with zeroed border slabs (or one memset) on the GPU;
     uninitialised memory poisoned with NaN."""
@@ -813,3 +814,6 @@ def test_interior_only_border_allocation_gpu(monkeypatch, bmin, builder, shape):
     assert_close_rel(out, OE.evaluate(op.forward_assignments, {'u': u}, boundary_handling=None)['out'], tol, 'out')
     assert_close_rel(du, OE.evaluate(op.backward_assignments, {'diffout': d}, boundary_handling=None)['diffu'],
                      tol, 'diffu')
+    if bmin == 0:
+        v = op.forward_ast_gpu.compile().last_variant[1]
+        assert v.XB or not v.ZSUM              # zsum launches store the x ends themselves
