@@ -124,6 +124,32 @@ def run_slab(name, builder, shape, dtype, full_cells, steps=20, warmup=3):
     sys.stdout.flush()
 
 
+def run_cpu(name, builder, shape, bh, nin, steps=2000):
+    """BASELINE config 1 as stated: the op on the CPU backend (use_cuda=False, the C kernels), host
+    wall time per forward + backward."""
+    import torch
+
+    import pystencils_autodiff_amd as pa
+    op = pa.AutoDiffOp(builder(), boundary_handling=bh)
+    fn = op.create_tensorflow_op(use_cuda=False, backend='torch_native')
+    g = torch.Generator().manual_seed(0)
+    ins = [(torch.rand(shape, generator=g) + 0.5).requires_grad_(True) for _ in range(nin)]
+    outs = fn.apply(*ins)
+    grads = [torch.rand(o.shape, generator=g) * 2 - 1 for o in outs]
+    for _ in range(50):
+        torch.autograd.backward(list(fn.apply(*ins)), grads)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        torch.autograd.backward(list(fn.apply(*ins)), grads)
+    el = (time.perf_counter() - t0) / steps
+    cells = 1
+    for s in shape:
+        cells *= s
+    print(json.dumps({'config': name, 'shape': list(shape), 'backend': 'cpu (C kernels, use_cuda=False)',
+                      'us_per_step': round(el * 1e6, 2), 'mcells_per_s': round(cells / el / 1e6, 2)}))
+    sys.stdout.flush()
+
+
 def main():
     import torch
 
@@ -141,6 +167,8 @@ def main():
         ('veclaplace7_f32_384^3x3', lambda: W.vector_laplace_7pt(), (384, 384, 384, 3), torch.float32, 'zeros', 1,
          24, 24),
     ]
+    if not only or 'readme_op_f32_20x30_cpu' in only:
+        run_cpu('readme_op_f32_20x30_cpu', W.readme_op, (20, 30), None, 2)
     for name, b, shape, dt, bh, nin, bf, bb in cfgs:
         if only and name not in only:
             continue
