@@ -246,3 +246,23 @@ def test_quantized_chunk_model():
     assert q(128, 256, 256, 32, 128, 1, 256) == 128
     assert q(768, 144, 256, 32, 128, 1, 256) == 110
     assert q(5, 7, 256, 32, 128, 1, 256) == 5
+
+
+def test_rccl_entry_points_report_errors_without_gpu():
+    """The RCCL halo entry points fail with a described code (never abort) when librccl is missing."""
+    import ctypes
+    from pystencils_autodiff_amd.backends import hip_runtime as rt
+    L = rt.lib()
+    rc = L.psad_rccl_open(b'/nonexistent/librccl.so')
+    assert rc == 20100
+    assert b'RCCL' in L.psad_error_string(rc)
+    uid = ctypes.create_string_buffer(128)
+    # still not opened (the failed open left no handle): every call reports the same code
+    assert L.psad_rccl_unique_id(uid) in (0, 20100)
+    if L.psad_rccl_unique_id(uid) == 20100:
+        comm = ctypes.c_void_p()
+        assert L.psad_rccl_comm_init(uid, 1, 0, ctypes.byref(comm)) == 20100
+        vp = ctypes.c_void_p
+        z = (vp * 1)(0)
+        n = (ctypes.c_size_t * 1)(0)
+        assert L.psad_halo_exchange(None, 1, z, z, z, z, n, -1, -1, None) == 20100
