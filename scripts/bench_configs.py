@@ -14,6 +14,33 @@ sys.path.insert(0, ROOT)
 PEAK = 8000.0
 
 
+def graph_step(fn, ins, grads, steps):
+    """Seconds per step of the same apply + backward captured once in a HIP graph (torch.cuda.graph on
+    static inputs / gradients) and replayed: what a stepped solver with fixed shapes pays once the
+    host-side autograd / launch overhead is gone."""
+    import torch
+    static = [t.detach().clone().requires_grad_(True) for t in ins]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            torch.autograd.backward(list(fn.apply(*static)), grads)
+            for t in static:
+                t.grad = None
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        torch.autograd.backward(list(fn.apply(*static)), grads)
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps * 10):
+        graph.replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / (steps * 10)
+
+
 def run(name, builder, shape, dtype, bh, nin, steps=20, warmup=3, bytes_fwd=None, bytes_bwd=None):
     import torch
 
@@ -65,12 +92,15 @@ def run(name, builder, shape, dtype, bh, nin, steps=20, warmup=3, bytes_fwd=None
     cells = 1
     for s in shape[:3]:
         cells *= s
+    el_graph = graph_step(fn, ins, grads, steps) if cells <= 1 << 26 else None
     f_ms = sorted(a.elapsed_time(b) for a, b, _ in ev)[len(ev) // 2]
     b_ms = sorted(b.elapsed_time(c) for _, b, c in ev)[len(ev) // 2]
     res = {'config': name, 'shape': list(shape), 'dtype': str(dtype).replace('torch.', ''),
            'mcells_per_s': round(cells * steps / el / 1e6, 1), 'ms_per_step': round(el / steps * 1e3, 4),
            'mcells_per_s_autograd_1thread': round(cells * steps / el_st / 1e6, 1),
            'ms_per_step_autograd_1thread': round(el_st / steps * 1e3, 4),
+           **({'mcells_per_s_hip_graph': round(cells / el_graph / 1e6, 1),
+               'ms_per_step_hip_graph': round(el_graph * 1e3, 4)} if el_graph else {}),
            'fwd_ms': round(f_ms, 4), 'bwd_ms': round(b_ms, 4),
            'fwd_schedule': op.forward_ast_gpu.compile().last_variant[0],
            'bwd_schedule': op.backward_ast_gpu.compile().last_variant[0]}
