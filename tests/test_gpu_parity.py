@@ -817,3 +817,38 @@ def test_interior_only_border_allocation_gpu(monkeypatch, bmin, builder, shape):
     if bmin == 0:
         v = op.forward_ast_gpu.compile().last_variant[1]
         assert v.XB or not v.ZSUM              # zsum launches store the x ends themselves
+
+
+@pytest.mark.parametrize('builder,n,tol', [(W.diffusion_7pt, 1024, 1e-6), (W.stencil_27pt, 768, 1e-3)])
+def test_full_size_properties(builder, n, tol):
+    """BASELINE full sizes (1024³ fp32 7-point, 768³ fp16 27-point) through the op: sampled planes (both
+    domain faces, the middle, chunk edges) vs the oracle evaluated on the 3-plane neighbourhood,
+    the adjoint dot-product identity <A u, d> = <u, Aᵀ d>, and linearity A(u + 2v) = Au + 2Av."""
+    op, fn = _op(builder())
+    dt = torch.float16 if builder is W.stencil_27pt else torch.float32
+    taps = S.taps_27pt() if builder is W.stencil_27pt else S.taps_diffusion_7pt()
+    g = torch.Generator(device='cuda').manual_seed(7)
+    u = torch.rand((n, n, n), generator=g, device='cuda').to(dt).requires_grad_(True)
+    d = (torch.rand((n, n, n), generator=g, device='cuda') * 2 - 1).to(dt)
+    (out,) = fn.apply(u)
+    out.backward(d)
+    torch.cuda.synchronize()
+    for z in (0, 1, n // 2, 127, 128, n - 2, n - 1):
+        lo, hi = max(0, z - 1), min(n, z + 2)
+        uu = u.detach()[lo:hi].cpu().numpy()
+        dd = d[lo:hi].cpu().numpy()
+        ref_o = S.linear_stencil(uu, taps)[z - lo]
+        ref_g = S.linear_stencil(dd, S.flip(taps))[z - lo]
+        assert_close_rel(out.detach()[z].cpu().numpy(), ref_o, tol, f'out plane {z}')
+        assert_close_rel(u.grad[z].cpu().numpy(), ref_g, tol, f'diffu plane {z}')
+    lhs = torch.sum(out.detach().double() * d.double()).item()
+    rhs = torch.sum(u.detach().double() * u.grad.double()).item()
+    assert abs(lhs - rhs) <= (1e-5 if dt == torch.float32 else 2e-3) * max(abs(lhs), 1.0), (lhs, rhs)
+    if dt == torch.float32:
+        v = torch.rand((n, n, n), generator=g, device='cuda')
+        with torch.no_grad():
+            (a1,) = fn.apply(u.detach())
+            (a2,) = fn.apply(v)
+            (a3,) = fn.apply(u.detach() + 2 * v)
+            err = (a3 - (a1 + 2 * a2)).abs().max().item()
+        assert err <= 4e-6 * a3.abs().max().item(), err
