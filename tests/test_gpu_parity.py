@@ -852,3 +852,29 @@ def test_full_size_properties(builder, n, tol):
             (a3,) = fn.apply(u.detach() + 2 * v)
             err = (a3 - (a1 + 2 * a2)).abs().max().item()
         assert err <= 4e-6 * a3.abs().max().item(), err
+
+
+def test_full_size_2d_and_readme_op():
+    """BASELINE config 2 at full size (4096² 5-point, every cell vs the oracle) and the README op at
+    16384² (sampled rows vs the closed-form forward / adjoint)."""
+    op, fn = _op(W.laplace_5pt())
+    g = np.random.default_rng(3)
+    u = g.uniform(0, 1, (4096, 4096)).astype(np.float32)
+    d = g.uniform(-1, 1, (4096, 4096)).astype(np.float32)
+    (out,), (du,) = _run(fn, [u], [d])
+    assert_close_rel(out, S.linear_stencil(u, S.taps_laplace_5pt()), 1e-6, 'laplace 4096² out')
+    assert_close_rel(du, S.linear_stencil(d, S.flip(S.taps_laplace_5pt())), 1e-6, 'laplace 4096² diffu')
+    op, fn = _op(W.readme_op(shape=None), None)
+    n = 16384
+    gt = torch.Generator(device='cuda').manual_seed(5)
+    x = (torch.rand((n, n), generator=gt, device='cuda') + 0.5).requires_grad_(True)
+    y = (torch.rand((n, n), generator=gt, device='cuda') + 0.5).requires_grad_(True)
+    dz = torch.rand((n, n), generator=gt, device='cuda') * 2 - 1
+    (z,) = fn.apply(x, y)
+    z.backward(dz)
+    for r in (0, 1, n // 2, n - 1):
+        xr, yr, dr = (t.detach()[r].cpu().numpy() for t in (x, y, dz))
+        assert_close_rel(z.detach()[r].cpu().numpy(), S.readme_forward(xr, yr), 1e-6, f'z row {r}')
+        dx_ref, dy_ref = S.readme_backward(xr, yr, dr)
+        assert_close_rel(x.grad[r].cpu().numpy(), dx_ref, 1e-6, f'diffx row {r}')
+        assert_close_rel(y.grad[r].cpu().numpy(), dy_ref, 1e-6, f'diffy row {r}')
