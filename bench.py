@@ -124,6 +124,10 @@ def main():
         # RCCL halo exchange inside the forward and the backward (zslab.py)
         zop = ZSlabOp(op, use_cuda=True)
         fn = zop.autograd_function()
+        # the backward then runs in this thread: torch's autograd device thread doubles the host cost of
+        # every HIP / RCCL call of a slab sweep (scripts/probes/slab_step.py ... sweeps: 95 vs 52 us per
+        # sweep), which at 8 ranks is what the GPU would wait on; same work, same autograd graph
+        torch.autograd.set_multithreading_enabled(False)
     uu = u.requires_grad_(True)
 
     def step(record):
@@ -210,7 +214,8 @@ def main():
                                    f'{n}^3 forward + TF-MAD adjoint per step',
                        'cells': cells_total, 'decomposition': f'z-slab x{world}' if world > 1 else 'single GPU',
                        'path': ('AutoDiffOp.create_tensorflow_op(backend=torch_native) apply+backward' if world == 1
-                                else 'ZSlabOp(AutoDiffOp).autograd_function() apply+backward, RCCL halo exchange')},
+                                else 'ZSlabOp(AutoDiffOp).autograd_function() apply+backward, RCCL halo exchange, '
+                                     'autograd engine single-threaded (set_multithreading_enabled(False))')},
             'fwd_ms': round(fwd_ms, 4),
             'bwd_ms': round(bwd_ms, 4),
             'hbm_roofline_frac_step': round(2 * BYTES_PER_CELL_SWEEP * cells_total / (ms_per_step * 1e-3) / 1e9

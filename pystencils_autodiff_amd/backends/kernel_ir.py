@@ -23,10 +23,10 @@ touches (``function_name``, ``fields_accessed``, ``fields_read``,
 schedule the HIP emitter prints (``hip_emitter.py``).
 """
 import hashlib
-from dataclasses import dataclass, field as dc_field
-from typing import Dict, List, Tuple
-
 import itertools
+from dataclasses import dataclass, field as dc_field
+from functools import cached_property
+from typing import Dict, List, Tuple
 
 import numpy as np
 import sympy as sp
@@ -75,21 +75,21 @@ class KernelIR:
     compute_dtype: np.dtype
     symbol_names: Dict[sp.Symbol, str] = dc_field(default_factory=dict)
 
-    @property
+    @cached_property
     def pointwise(self):
         return all(all(o == 0 for o in r.offsets) for r in self.reads) and \
             all(all(o == 0 for o in s[1]) for s in self.stores)
 
-    @property
+    @cached_property
     def has_index_dims(self):
         return any(f.index_dimensions > 0 for f in self.fields)
 
-    @property
+    @cached_property
     def stencil_fields(self):
         """Read fields with at least one non-zero offset (they need halo data)."""
         return sorted({r.field for r in self.reads if any(o != 0 for o in r.offsets)}, key=lambda f: f.name)
 
-    @property
+    @cached_property
     def point_fields(self):
         st = set(self.stencil_fields)
         return sorted({r.field for r in self.reads if r.field not in st}, key=lambda f: f.name)

@@ -71,17 +71,27 @@ class RcclHalo:
             rt._check(L.psad_rccl_comm_init(obj[0], self.world, self.rank, ctypes.byref(comm)), 'ncclCommInitRank')
             self.comm = comm
             self.stream = torch.cuda.Stream(device=self.device)
+            # reused stream-order events (Stream.wait_stream would create two per sweep)
+            self.ev_faces = torch.cuda.Event()
+            self.ev_halos = torch.cuda.Event()
+        self._arrays = {}
+        self._exchange = L.psad_halo_exchange
+        self._stream_handle = self.stream.cuda_stream
 
     def exchange(self, planes, peer_lo, peer_hi):
         """``planes`` = [(send_lo, recv_lo, send_hi, recv_hi, nbytes)] (device pointers, 0 for an
         absent side); enqueued on :attr:`stream`, which the caller orders against its own."""
         n = len(planes)
-        vp = ctypes.c_void_p
-        cols = list(zip(*planes)) if n else [()] * 5
-        arrs = [(vp * n)(*cols[i]) for i in range(4)]
-        sizes = (ctypes.c_size_t * n)(*cols[4])
-        self._rt._check(self._rt.lib().psad_halo_exchange(self.comm, n, *arrs, sizes, peer_lo, peer_hi,
-                                                          self.stream.cuda_stream), 'RCCL halo exchange')
+        bufs = self._arrays.get(n)
+        if bufs is None:           # argument arrays reused across sweeps (ctypes construction is not free)
+            bufs = self._arrays[n] = ([(ctypes.c_void_p * n)() for _ in range(4)], (ctypes.c_size_t * n)())
+        arrs, sizes = bufs
+        for i, (a, b, c, d, nb) in enumerate(planes):
+            arrs[0][i], arrs[1][i], arrs[2][i], arrs[3][i], sizes[i] = a, b, c, d, nb
+        rc = self._exchange(self.comm, n, arrs[0], arrs[1], arrs[2], arrs[3], sizes, peer_lo, peer_hi,
+                            self._stream_handle)
+        if rc:
+            self._rt._check(rc, 'RCCL halo exchange')
 
     def close(self):
         if self.comm:
@@ -158,6 +168,7 @@ class ZSlabOp:
                 raise ValueError("z-slab decomposition supports boundary_handling='zeros'")
         self._bufs = {}
         self._halo = None
+        self._meta = {}
 
     def _rccl(self, device):
         """The RCCL exchange path (GPU, ``nccl`` process group, ``PSAD_HALO`` not ``torch``)."""
@@ -184,10 +195,13 @@ class ZSlabOp:
         return self._sweep('backward', kwargs)
 
     def _sweep(self, which, kwargs):
-        k = self.kernels[which]
+        meta = self._meta.get(which)
+        if meta is None:
+            k = self.kernels[which]
+            meta = self._meta[which] = (k, k.ir.stencil_fields,
+                                        max([self._radius(k, f) for f in k.ir.stencil_fields] + [0]))
+        k, stencil, rz = meta
         ir = k.ir
-        stencil = ir.stencil_fields
-        rz = max([self._radius(k, f) for f in stencil] + [0])
         ref = kwargs[ir.fields_written[0].name]
         split = rz > 0 and dist.is_initialized() and dist.get_world_size(self.group) > 1
         halo = None
@@ -250,7 +264,8 @@ class ZSlabOp:
         if halo.loopback:
             peer_lo = peer_hi = 0
         cur = torch.cuda.current_stream(halo.device)
-        halo.stream.wait_stream(cur)                  # the faces are final; the last sweep's reads are done
+        halo.ev_faces.record(cur)
+        halo.stream.wait_event(halo.ev_faces)         # the faces are final; the last sweep's reads are done
         planes, halos = [], {}
         for f in stencil:
             t = kwargs[f.name]
@@ -282,7 +297,8 @@ class ZSlabOp:
         zl = kwargs[k.ir.fields_written[0].name].shape[0]
         if zl > 2 * rz:
             compiled(z_range=(rz, zl - rz), **kwargs)  # interior overlaps the exchange
-        cur.wait_stream(halo.stream)
+        halo.ev_halos.record(halo.stream)
+        cur.wait_event(halo.ev_halos)
         if zl > 2 * rz:
             compiled(halos=halos, z_range=((0, rz), (zl - rz, zl)), **kwargs)
         else:

@@ -32,9 +32,12 @@ def timed(fn, u, d, steps=50):
 
 def main():
     zl = int(sys.argv[1]) if len(sys.argv) > 1 else 128
-    op = pa.AutoDiffOp(W.diffusion_7pt(), boundary_handling='zeros')
-    u = torch.rand((zl, 1024, 1024), device='cuda')
-    d = torch.rand_like(u) * 2 - 1
+    wl = sys.argv[2] if len(sys.argv) > 2 else 'diffusion7'
+    n = 768 if wl == 'stencil27' else 1024
+    op = pa.AutoDiffOp(W.stencil_27pt() if wl == 'stencil27' else W.diffusion_7pt(), boundary_handling='zeros')
+    dt = torch.float16 if wl == 'stencil27' else torch.float32
+    u = torch.rand((zl, n, n), device='cuda').to(dt)
+    d = (torch.rand_like(u, dtype=torch.float32) * 2 - 1).to(dt)
     plain = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
     zop = ZSlabOp(op, use_cuda=True)
     zop._halo = RcclHalo(loopback=True)
@@ -42,14 +45,103 @@ def main():
     for name, fn in (('plain op', plain), ('zslab + RCCL loopback', zfn), ('plain op', plain),
                      ('zslab + RCCL loopback', zfn)):
         wall, host = timed(fn, u, d)
-        print(f'{name:24s} {zl}x1024^2: {wall:.4f} ms/step wall, {host:.4f} ms/step host enqueue, '
-              f'implied N=8 1024^3 rate {1024**3 / (wall * 1e-3) / 1e6:,.0f} Mcells/s' if zl == 128 else
-              f'{name:24s} {zl}x1024^2: {wall:.4f} ms/step wall, {host:.4f} ms/step host enqueue')
+        print(f'{name:24s} {wl} {zl}x{n}^2: {wall:.4f} ms/step wall, {host:.4f} ms/step host enqueue, '
+              f'implied N={n // zl} {n}^3 rate {n**3 / (wall * 1e-3) / 1e6:,.0f} Mcells/s')
     torch.autograd.set_multithreading_enabled(False)
     wall, host = timed(zfn, u, d)
-    print(f'zslab, autograd 1 thread  : {wall:.4f} ms/step wall, {host:.4f} ms/step host enqueue')
+    print(f'zslab, autograd 1 thread  : {wall:.4f} ms/step wall, {host:.4f} ms/step host enqueue, '
+          f'implied N={n // zl} {n}^3 rate {n**3 / (wall * 1e-3) / 1e6:,.0f} Mcells/s')
+    zop.close()
+
+
+def profile_host(zl=96, wl='stencil27', steps=300):
+    """cProfile of the zslab step's host side (autograd in the calling thread so all of it is visible)."""
+    import cProfile
+    import pstats
+    n = 768 if wl == 'stencil27' else 1024
+    op = pa.AutoDiffOp(W.stencil_27pt() if wl == 'stencil27' else W.diffusion_7pt(), boundary_handling='zeros')
+    dt = torch.float16 if wl == 'stencil27' else torch.float32
+    u = torch.rand((zl, n, n), device='cuda').to(dt).requires_grad_(True)
+    d = (torch.rand((zl, n, n), device='cuda') * 2 - 1).to(dt)
+    zop = ZSlabOp(op, use_cuda=True)
+    zop._halo = RcclHalo(loopback=True)
+    fn = zop.autograd_function()
+    torch.autograd.set_multithreading_enabled(False)
+    for _ in range(10):
+        (o,) = fn.apply(u)
+        o.backward(d)
+        u.grad = None
+    torch.cuda.synchronize()
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(steps):
+        (o,) = fn.apply(u)
+        o.backward(d)
+        u.grad = None
+    torch.cuda.synchronize()
+    pr.disable()
+    pstats.Stats(pr, stream=sys.stdout).sort_stats('tottime').print_stats(22)
+    zop.close()
+
+
+def time_sweeps(zl=96, wl='stencil27', steps=300):
+    """Host time inside ZSlabOp._sweep per forward / backward sweep, autograd multi- vs single-threaded."""
+    import collections
+    n = 768 if wl == 'stencil27' else 1024
+    op = pa.AutoDiffOp(W.stencil_27pt() if wl == 'stencil27' else W.diffusion_7pt(), boundary_handling='zeros')
+    dt = torch.float16 if wl == 'stencil27' else torch.float32
+    u = torch.rand((zl, n, n), device='cuda').to(dt).requires_grad_(True)
+    d = (torch.rand((zl, n, n), device='cuda') * 2 - 1).to(dt)
+    zop = ZSlabOp(op, use_cuda=True)
+    zop._halo = RcclHalo(loopback=True)
+    fn = zop.autograd_function()
+    acc = collections.defaultdict(float)
+    orig = zop._sweep
+
+    def timed(which, kwargs):
+        t = time.perf_counter()
+        orig(which, kwargs)
+        acc[which] += time.perf_counter() - t
+    zop._sweep = timed
+    ex = zop._halo.exchange
+
+    def timed_ex(*a):
+        t = time.perf_counter()
+        ex(*a)
+        acc['exchange'] += time.perf_counter() - t
+    zop._halo.exchange = timed_ex
+    for mt in (True, False):
+        torch.autograd.set_multithreading_enabled(mt)
+        for _ in range(10):
+            (o,) = fn.apply(u)
+            o.backward(d)
+            u.grad = None
+        torch.cuda.synchronize()
+        acc.clear()
+        t0 = time.perf_counter()
+        ta = tb = 0.0
+        for _ in range(steps):
+            t1 = time.perf_counter()
+            (o,) = fn.apply(u)
+            t2 = time.perf_counter()
+            o.backward(d)
+            t3 = time.perf_counter()
+            ta += t2 - t1
+            tb += t3 - t2
+            u.grad = None
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / steps * 1e6
+        print(f'multithreaded={mt}: wall {wall:.1f} us/step; apply {ta / steps * 1e6:.1f} us, backward() '
+              f'{tb / steps * 1e6:.1f} us; inside _sweep: fwd {acc["forward"] / steps * 1e6:.1f} us, '
+              f'bwd {acc["backward"] / steps * 1e6:.1f} us; exchange calls {acc["exchange"] / steps * 1e6:.1f} us')
+    torch.autograd.set_multithreading_enabled(True)
     zop.close()
 
 
 if __name__ == '__main__':
-    main()
+    if len(sys.argv) > 3 and sys.argv[3] == 'profile':
+        profile_host(int(sys.argv[1]), sys.argv[2])
+    elif len(sys.argv) > 3 and sys.argv[3] == 'sweeps':
+        time_sweeps(int(sys.argv[1]), sys.argv[2])
+    else:
+        main()

@@ -38,6 +38,7 @@ class _GlooHalo:
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
         self.device = torch.device('cuda', torch.cuda.current_device())
         self.stream = torch.cuda.Stream()
+        self.ev_faces, self.ev_halos = torch.cuda.Event(), torch.cuda.Event()
 
     def exchange(self, planes, peer_lo, peer_hi):
         from pystencils_autodiff_amd.backends import hip_runtime as rt
