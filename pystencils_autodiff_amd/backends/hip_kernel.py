@@ -223,6 +223,21 @@ class HipStencilKernel:
         The first call for a given (shape, alignment, halo layout, z range) builds a launch plan
         (variant, function handle, grid, argument layout); later calls only re-pack pointers.
         """
+        prep = self.prepare(halos=halos, force_schedule=force_schedule, z_range=z_range, x_border=x_border,
+                            **kwargs)
+        if prep is None:
+            return None
+        fn, grid, block, packed, xb, device = prep
+        if grid == 0:
+            return xb
+        if stream is None:
+            stream = _torch()._C._cuda_getCurrentRawStream(device)
+        rt.launch(fn, (grid,), (block,), packed, stream)
+        return xb
+
+    def prepare(self, halos=None, force_schedule=None, z_range=None, x_border=False, **kwargs):
+        """Everything of a launch but the launch: ``(function, grid, block, packed args, x_border done,
+        device)``, or None for an empty domain (arguments as for ``__call__``)."""
         torch = _torch()
         ir = self.ir
         tensors = []
@@ -251,10 +266,8 @@ class HipStencilKernel:
                 raise ValueError(f"{self.name}: field '{name}' has spatial shape {tuple(t.shape[:ir.ndim])}, "
                                  f"expected {shape}")
         if any(n == 0 for n in shape):
-            return
+            return None
         device = ref.device.index
-        if stream is None:
-            stream = torch._C._cuda_getCurrentRawStream(device)
         halo_list = []
         if halos:
             for f in ir.stencil_fields:
@@ -273,9 +286,8 @@ class HipStencilKernel:
             self._plans[key] = plan
         self.last_variant = plan.variant
         if plan.grid == 0:
-            return plan.xb
-        rt.launch(plan.fn, (plan.grid,), (plan.block,), plan.pack(ptrs, hptrs, scalars), stream)
-        return plan.xb
+            return plan.fn, 0, plan.block, b'', plan.xb, device
+        return plan.fn, plan.grid, plan.block, plan.pack(ptrs, hptrs, scalars), plan.xb, device
 
     def _make_plan(self, tensors, halo_list, shape, device, contiguous, force_schedule, z_range, x_border=False):
         torch = _torch()
