@@ -273,17 +273,18 @@ class ZSlabOp:
                 raise ValueError(f"slab of {t.shape[0]} planes is thinner than the stencil radius {rz}")
             if not t.is_contiguous():
                 raise ValueError(f"slab of '{f.name}' must be contiguous for the RCCL face exchange")
-            key = ('rccl', f.name, t.dtype, tuple(t.shape[1:]), t.device)
+            key = ('rccl', f.name, t.dtype, t.shape, t.device)
             bufs = self._bufs.get(key)
             if bufs is None:
                 shape = (rz,) + tuple(t.shape[1:])
+                plane = t[0].numel() * t.element_size()
                 bufs = (torch.empty(shape, dtype=t.dtype, device=t.device) if peer_lo >= 0 else None,
-                        torch.empty(shape, dtype=t.dtype, device=t.device) if peer_hi >= 0 else None)
+                        torch.empty(shape, dtype=t.dtype, device=t.device) if peer_hi >= 0 else None,
+                        rz * plane, (t.shape[0] - rz) * plane)
                 self._bufs[key] = bufs
-            lo, hi = bufs
-            nbytes = rz * t[0].numel() * t.element_size()
+            lo, hi, nbytes, last_off = bufs
             first = t.data_ptr()
-            last = first + (t.shape[0] - rz) * t[0].numel() * t.element_size()
+            last = first + last_off
             if halo.loopback:
                 # RCCL pairs a peer's sends and receives in issue order: swap the faces so that, as
                 # with real neighbours, the lower halo receives the far (upper) face — periodic z
