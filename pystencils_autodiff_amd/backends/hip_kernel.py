@@ -421,9 +421,15 @@ class HipStencilKernel:
             min(nz, max(cfg.ZMIN, min(cfg.ZMAX, math.ceil(nz * nt / target))))
         explicit = self.kernel.tuning.get('ZC') or os.environ.get('PSAD_MARCH_ZC') or cfg.ZCT or \
             'BLOCKS' in self.kernel.tuning or os.environ.get('PSAD_MARCH_BLOCKS')
-        if slots and cfg.WS and nz and not explicit:
+        cus = _torch().cuda.get_device_properties(_torch().cuda.current_device()).multi_processor_count \
+            if slots else 0
+        # measured on the default WS tiles (one workgroup per CU, or the half-width tiles it picks for
+        # x extents that pad less); with user tile / depth overrides that allow several partially filled
+        # workgroups per CU it can pick an unbalanced grid (512³ D=3: 0.249 vs 0.188 ms), so those keep
+        # the block-count target
+        overridden = any(k in self.kernel.tuning for k in ('CX', 'NR', 'D', 'WX', 'NW'))
+        if slots and cfg.WS and nz and not explicit and (slots <= cus or not overridden):
             ws = ws_geometry(ir, cfg)
-            cus = _torch().cuda.get_device_properties(_torch().cuda.current_device()).multi_processor_count
             # workgroups that saturate HBM: ~64 KiB in flight per CU (one 256×16 fp32 ring of 4 planes)
             wsat = max(cus, math.ceil(cus * 65536 / (ws['D'] * ws['per_plane'] * 1024)))
             zc = self.quantized_chunk(nz, nt, slots, cfg.ZMIN, cfg.ZMAX, march_geometry(ir, cfg)['RZ'], wsat)
