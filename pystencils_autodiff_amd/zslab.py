@@ -318,6 +318,7 @@ class ZSlabOp:
         fwd_names = {f.name for f in fk.ir.fields}
         bwd_names = {f.name for f in bk.ir.fields}
         bwd_outputs = [f.name for f in op.backward_output_fields]
+        bwd_read = {r.field.name for r in bk.ir.reads}        # accumulated adjoints start from zeros
         prefix = 'diff'
 
         def tdtype(f):
@@ -349,8 +350,7 @@ class ZSlabOp:
                         kw[prefix + f.name] = (g if g is not None else torch.zeros_like(like)).contiguous()
                 res = {}
                 for name in bwd_outputs:
-                    accum = any(r.field.name == name for r in bk.ir.reads)
-                    res[name] = (torch.zeros_like if accum else torch.empty_like)(like)
+                    res[name] = (torch.zeros_like if name in bwd_read else torch.empty_like)(like)
                     kw[name] = res[name]
                 zop.bwd(**kw)
                 return tuple(res.get(prefix + f.name) for f in fwd_inputs[:ctx.n_inputs])
