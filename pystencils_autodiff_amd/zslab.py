@@ -33,7 +33,7 @@ import os
 import torch
 import torch.distributed as dist
 
-__all__ = ['slab_bounds', 'ZSlabOp', 'exchange_halos', 'RcclHalo']
+__all__ = ['slab_bounds', 'ZSlabOp', 'exchange_halos', 'RcclHalo', 'RcclUnavailable']
 
 
 def rccl_library_path():
@@ -41,6 +41,11 @@ def rccl_library_path():
     cands = sorted(glob.glob(os.path.join(os.path.dirname(torch.__file__), 'lib', 'librccl.so*')))
     cands += sorted(glob.glob('/opt/rocm/lib/librccl.so*'))
     return os.environ.get('PSAD_RCCL_LIBRARY') or (cands[0] if cands else 'librccl.so.1')
+
+
+class RcclUnavailable(RuntimeError):
+    """Raised on every rank alike when the C-ABI RCCL communicator cannot be set up; the sweep then
+    uses ``torch.distributed.batch_isend_irecv`` on the same ``nccl`` (= RCCL) process group."""
 
 
 class RcclHalo:
@@ -54,10 +59,24 @@ class RcclHalo:
         from .backends import hip_runtime as rt
         self._rt = rt
         L = rt.lib()
-        rt._check(L.psad_rccl_open(rccl_library_path().encode()), 'opening librccl')
+        opened = L.psad_rccl_open(rccl_library_path().encode())
         self.loopback = loopback
         self.rank = 0 if loopback else dist.get_rank(group)
         self.world = 1 if loopback else dist.get_world_size(group)
+        if not loopback:
+            # every rank agrees before the collective setup below: a rank that could not open librccl
+            # must not leave the others waiting in the unique-id broadcast
+            if dist.get_backend(group) == 'gloo':
+                dev = torch.device('cpu')
+            else:
+                dev = torch.device('cuda', torch.cuda.current_device()) if device is None else device
+            flag = torch.tensor([0 if opened == 0 else 1], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+            if int(flag.item()):
+                raise RcclUnavailable('librccl could not be opened on at least one rank'
+                                      + (f' ({rt.lib().psad_rccl_error_string(opened).decode()})' if opened else ''))
+        else:
+            rt._check(opened, 'opening librccl')
         uid = ctypes.create_string_buffer(128)
         if self.rank == 0:
             rt._check(L.psad_rccl_unique_id(uid), 'ncclGetUniqueId')
@@ -168,6 +187,7 @@ class ZSlabOp:
                 raise ValueError("z-slab decomposition supports boundary_handling='zeros'")
         self._bufs = {}
         self._halo = None
+        self._no_rccl = False
         self._meta = {}
 
     def _rccl(self, device):
@@ -176,7 +196,16 @@ class ZSlabOp:
                 and os.environ.get('PSAD_HALO', 'rccl') == 'rccl'):
             return None
         if self._halo is None:
-            self._halo = RcclHalo(self.group, device)
+            if self._no_rccl:
+                return None
+            try:
+                self._halo = RcclHalo(self.group, device)
+            except RcclUnavailable as exc:
+                import sys
+                print(f'zslab: {exc}; halo exchange falls back to torch.distributed.batch_isend_irecv',
+                      file=sys.stderr)
+                self._no_rccl = True
+                return None
         return self._halo
 
     def close(self):

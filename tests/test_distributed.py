@@ -244,3 +244,34 @@ def test_zslab_rccl_sweep_emulated_ranks(world, shape, builder_name, tmp_path, m
     tol = 1e-3 if builder_name == 'stencil_27pt' else 1e-6
     assert_close_rel(out, ref_out, tol, 'out')
     assert_close_rel(du, ref_du, tol, 'diffu')
+
+
+def _rccl_agreement_worker(rank, world, port, result_dir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    if rank == 1:   # this rank cannot open librccl; rank 0 can
+        os.environ['PSAD_RCCL_LIBRARY'] = '/nonexistent/librccl.so'
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from pystencils_autodiff_amd.zslab import RcclHalo, RcclUnavailable
+        try:
+            RcclHalo()
+            outcome = 'constructed'
+        except RcclUnavailable:
+            outcome = 'unavailable'
+        with open(os.path.join(result_dir, f'rccl_{rank}.txt'), 'w') as fh:
+            fh.write(outcome)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_open_failure_is_agreed_by_every_rank(tmp_path):
+    """A rank that cannot open librccl makes EVERY rank raise RcclUnavailable before the unique-id
+    broadcast (none is left waiting in a collective); ZSlabOp then uses batch_isend_irecv."""
+    pytest.importorskip('pystencils_autodiff_amd.backends.hip_runtime')
+    from pystencils_autodiff_amd.backends import hip_runtime as rt
+    try:
+        rt.lib()
+    except Exception as exc:  # noqa: BLE001
+        pytest.skip(f'libpsad_hip.so not built: {exc}')
+    mp.spawn(_rccl_agreement_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    assert [open(tmp_path / f'rccl_{r}.txt').read() for r in range(2)] == ['unavailable', 'unavailable']
