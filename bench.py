@@ -128,6 +128,18 @@ def main():
         # every HIP / RCCL call of a slab sweep (scripts/probes/slab_step.py ... sweeps: 95 vs 52 us per
         # sweep), which at 8 ranks is what the GPU would wait on; same work, same autograd graph
         torch.autograd.set_multithreading_enabled(False)
+        zop.connect(u.device)       # setup, not a step: the RCCL communicator exists before warmup
+    # setup, not a step: the 1024^3 kernel variants compiled (hiprtc) and loaded, and the output and
+    # gradient blocks reserved in torch's caching allocator, before warmup
+    scratch = [torch.empty_like(u), torch.empty_like(u)]
+    fwd_k.prepare(u=u, out=scratch[0])
+    bwd_k.prepare(diffout=d, diffu=scratch[1])
+    del scratch
+    # and a first backward with an explicit gradient (its lazy imports in autograd._make_grads cost ~40 ms)
+    # run on a 1-element tensor (scripts/probes/first_step.py)
+    probe = torch.zeros(1, device=u.device, requires_grad=True)
+    (probe * 2).backward(torch.ones_like(probe))
+    del probe
     uu = u.requires_grad_(True)
 
     def step(record):

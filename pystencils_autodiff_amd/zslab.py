@@ -208,6 +208,12 @@ class ZSlabOp:
                 return None
         return self._halo
 
+    def connect(self, device=None):
+        """Create the RCCL halo communicator now (collective: every rank calls it) instead of in the
+        first sweep — setup kept out of a timed loop. A no-op off the ``nccl`` process group."""
+        if dist.is_initialized() and dist.get_world_size(self.group) > 1:
+            self._rccl(device if device is not None else torch.device('cuda', torch.cuda.current_device()))
+
     def close(self):
         """Destroy the halo communicator (collective, before ``destroy_process_group``)."""
         if self._halo is not None:
