@@ -129,6 +129,7 @@ def main():
         # sweep), which at 8 ranks is what the GPU would wait on; same work, same autograd graph
         torch.autograd.set_multithreading_enabled(False)
         zop.connect(u.device)       # setup, not a step: the RCCL communicator exists before warmup
+        zop.warm_exchange(u=u, diffout=d)   # and RCCL's peer connections (set up on first use)
     # setup, not a step: the 1024^3 kernel variants compiled (hiprtc) and loaded, and the output and
     # gradient blocks reserved in torch's caching allocator, before warmup
     scratch = [torch.empty_like(u), torch.empty_like(u)]

@@ -290,25 +290,23 @@ class ZSlabOp:
             if rz:
                 t.copy_(ghosted[name][rz:rz + zl])
 
-    def _sweep_rccl(self, k, halo, stencil, rz, kwargs):
-        """Faces out on the halo stream (one RCCL group for every stencil field) while the interior
-        planes run on the caller's stream; then the two face ranges in one launch."""
-        rank, world = halo.rank, halo.world
-        peer_lo = rank - 1 if rank > 0 else -1
-        peer_hi = rank + 1 if rank < world - 1 else -1
+    @staticmethod
+    def _peers(halo):
         if halo.loopback:
-            peer_lo = peer_hi = 0
-        cur = torch.cuda.current_stream(halo.device)
-        halo.ev_faces.record(cur)
-        halo.stream.wait_event(halo.ev_faces)         # the faces are final; the last sweep's reads are done
+            return 0, 0
+        return (halo.rank - 1 if halo.rank > 0 else -1), (halo.rank + 1 if halo.rank < halo.world - 1 else -1)
+
+    def _face_planes(self, halo, named, rz):
+        """Send / receive pointers of the RZ boundary planes of each ``(name, slab)`` and the receive
+        buffers (cached per field, dtype, shape, device) as ``{name: (lo, hi)}`` halos."""
+        peer_lo, peer_hi = self._peers(halo)
         planes, halos = [], {}
-        for f in stencil:
-            t = kwargs[f.name]
+        for name, t in named:
             if t.shape[0] < rz:
                 raise ValueError(f"slab of {t.shape[0]} planes is thinner than the stencil radius {rz}")
             if not t.is_contiguous():
-                raise ValueError(f"slab of '{f.name}' must be contiguous for the RCCL face exchange")
-            key = ('rccl', f.name, t.dtype, t.shape, t.device)
+                raise ValueError(f"slab of '{name}' must be contiguous for the RCCL face exchange")
+            key = ('rccl', name, t.dtype, t.shape, t.device)
             bufs = self._bufs.get(key)
             if bufs is None:
                 shape = (rz,) + tuple(t.shape[1:])
@@ -327,7 +325,38 @@ class ZSlabOp:
             planes.append((first, lo.data_ptr() if lo is not None else 0, last,
                            hi.data_ptr() if hi is not None else 0, nbytes))
             t.record_stream(halo.stream)
-            halos[f.name] = (lo, hi)
+            halos[name] = (lo, hi)
+        return planes, halos
+
+    def warm_exchange(self, **slabs):
+        """One face exchange of the given slabs (``name=tensor``, stencil field names) with no compute:
+        RCCL sets up its peer connections on first use, so this keeps that out of a timed loop and
+        leaves the receive buffers allocated. Collective; a no-op without an RCCL communicator."""
+        halo = self._halo
+        if halo is None or not slabs:
+            return
+        cur = torch.cuda.current_stream(halo.device)
+        halo.ev_faces.record(cur)
+        halo.stream.wait_event(halo.ev_faces)
+        for which in ('forward', 'backward'):      # each with its own kernel's radius, as its sweep does
+            k = self.kernels.get(which)
+            if k is None:
+                continue
+            named = [(f.name, slabs[f.name]) for f in k.ir.stencil_fields if f.name in slabs]
+            rz = max([self._radius(k, f) for f in k.ir.stencil_fields] + [0])
+            if named and rz:
+                planes, _ = self._face_planes(halo, named, rz)
+                halo.exchange(planes, *self._peers(halo))
+        halo.stream.synchronize()
+
+    def _sweep_rccl(self, k, halo, stencil, rz, kwargs):
+        """Faces out on the halo stream (one RCCL group for every stencil field) while the interior
+        planes run on the caller's stream; then the two face ranges in one launch."""
+        peer_lo, peer_hi = self._peers(halo)
+        cur = torch.cuda.current_stream(halo.device)
+        halo.ev_faces.record(cur)
+        halo.stream.wait_event(halo.ev_faces)         # the faces are final; the last sweep's reads are done
+        planes, halos = self._face_planes(halo, [(f.name, kwargs[f.name]) for f in stencil], rz)
         halo.exchange(planes, peer_lo, peer_hi)
         compiled = k.compile()
         zl = kwargs[k.ir.fields_written[0].name].shape[0]

@@ -218,6 +218,7 @@ def test_zslab_rccl_loopback_sweep(builder_name, shape):
     try:
         tu, td = torch.from_numpy(u).cuda(), torch.from_numpy(d).cuda()
         out, du = torch.empty_like(tu), torch.empty_like(td)
+        z.warm_exchange(u=tu, diffout=td)      # setup exchange: the sweeps reuse its receive buffers
         for which, kw in (('forward', dict(u=tu, out=out)), ('backward', dict(diffout=td, diffu=du))):
             k = z.kernels[which]
             z._sweep_rccl(k, z._halo, k.ir.stencil_fields, 1, kw)
