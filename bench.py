@@ -34,34 +34,59 @@ def parse():
     return p.parse_args()
 
 
+def cpu_model():
+    try:
+        with open('/proc/cpuinfo') as fh:
+            for line in fh:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or 'unknown'
+
+
 def cpu_baseline(budget_s):
-    """The oracle's C restatement of the reference CPU kernel (OpenMP), bounded 1024²×64 sample."""
+    """The oracle's C restatement of the reference CPU kernel on bounded slabs of the workload: first with
+    ONE thread — the reference's default (``create_kernel`` without ``cpu_openmp``, ``_autodiff.py:487-489``),
+    reported as ``value`` — then with OpenMP over this process's cores (``cpu_openmp=True``)."""
     import numpy as np
     from oracle import cref
     build_dir = os.path.join(ROOT, 'oracle', 'build_native')
     lib = cref.load(build_dir=build_dir, march='native')
-    threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or len(os.sched_getaffinity(0))
-    os.environ.setdefault('OMP_NUM_THREADS', str(threads))
-    shape = (64, 1024, 1024)
-    rng = np.random.default_rng(0)
-    u = rng.uniform(0, 1, shape).astype(np.float32)
-    d = rng.uniform(-1, 1, shape).astype(np.float32)
-    out = np.empty_like(u)
-    du = np.empty_like(u)
-    lib.diffusion7_f32(u, 0.1, out)          # warm-up (first touch, thread pool)
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        lib.diffusion7_f32(u, 0.1, out)      # forward sweep
-        lib.diffusion7_f32(d, 0.1, du)       # adjoint sweep (same symmetric stencil on diffout)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or reps >= 5000:
-            break
-    cells = reps * u.size
-    return {'value': round(cells / el / 1e6, 2), 'unit': 'Mcells/s', 'cores': threads, 'kind': 'port',
-            'sample': f'{reps} fwd+bwd sweeps of a 64x1024x1024 fp32 slab of the 1024^3 workload, '
-                      f'oracle/stencil_ref.c (pystencils CPU loop nest restated), gcc -O3 -march=native -fopenmp, '
-                      f'{threads} OpenMP threads, {el:.1f} s'}
+    affinity = len(os.sched_getaffinity(0))
+    mt = int(os.environ.get('OMP_NUM_THREADS', '0')) or affinity
+
+    def run(threads, planes, budget):
+        got = lib.set_threads(threads)
+        shape = (planes, 1024, 1024)
+        rng = np.random.default_rng(0)
+        u = rng.uniform(0, 1, shape).astype(np.float32)
+        d = rng.uniform(-1, 1, shape).astype(np.float32)
+        out, du = np.empty_like(u), np.empty_like(u)
+        lib.diffusion7_f32(u, 0.1, out)          # warm-up (first touch, thread pool)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            lib.diffusion7_f32(u, 0.1, out)      # forward sweep
+            lib.diffusion7_f32(d, 0.1, du)       # adjoint sweep (same symmetric stencil on diffout)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget or reps >= 5000:
+                break
+        return got, reps, el, round(reps * u.size / el / 1e6, 2)
+
+    t1, reps1, el1, v1 = run(1, 16, budget_s / 2)
+    tm, repsm, elm, vm = run(mt, 64, budget_s / 2)
+    model = cpu_model()
+    return {'value': v1, 'unit': 'Mcells/s', 'cores': t1, 'kind': 'port',
+            'sample': f'{reps1} fwd+bwd sweeps of a 16x1024x1024 fp32 slab of the 1024^3 workload in {el1:.1f} s, '
+                      f'1 thread (the reference default: no cpu_openmp); oracle/stencil_ref.c (pystencils CPU '
+                      f'loop nest restated), gcc -O3 -march=native -fopenmp; host CPU {model}',
+            'threads_1': {'value': v1, 'threads': t1, 'sweeps': reps1, 'seconds': round(el1, 2),
+                          'sample': '16x1024x1024 fp32'},
+            'threads_mt': {'value': vm, 'threads': tm, 'sweeps': repsm, 'seconds': round(elm, 2),
+                           'sample': '64x1024x1024 fp32', 'cpu_openmp': True},
+            'cpu_model': model, 'cpus_available': affinity}
 
 
 def load_traffic(workload, kernel):

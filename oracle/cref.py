@@ -24,11 +24,17 @@ class OracleLib:
         L.oracle_stencil27_f16.argtypes = [vp, vp, i64, i64, i64, vp]
         L.oracle_readme_fwd_f32.argtypes = [vp, vp, vp, i64]
         L.oracle_readme_bwd_f32.argtypes = [vp, vp, vp, vp, vp, i64]
+        L.oracle_set_threads.argtypes = [ctypes.c_int]
+        L.oracle_set_threads.restype = ctypes.c_int
         for name in ('oracle_diffusion7_f32', 'oracle_linear3d_f64', 'oracle_stencil27_f16',
                      'oracle_readme_fwd_f32', 'oracle_readme_bwd_f32'):
             getattr(L, name).restype = None
         self.lib = L
         self.path = path
+
+    def set_threads(self, n):
+        """OpenMP threads of the loops (1 = the reference's default, no cpu_openmp); returns the count."""
+        return self.lib.oracle_set_threads(int(n))
 
     def diffusion7_f32(self, u, alpha, out=None):
         u = np.ascontiguousarray(u, dtype=np.float32)

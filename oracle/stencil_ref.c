@@ -11,6 +11,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 typedef long long i64;
@@ -52,7 +53,16 @@ void oracle_linear3d_f64(const double* restrict u, double* restrict out, i64 Z, 
             }
 }
 
+#ifdef __F16C__
+#include <immintrin.h>
+#endif
+
+/* IEEE binary16 -> binary32: the hardware conversion (F16C, in every x86-64-v3 host) when compiled for
+ * it, else the bit-level restatement. */
 static inline float h2f(uint16_t h) {
+#ifdef __F16C__
+    return _cvtsh_ss(h);
+#else
     uint32_t s = (uint32_t)(h >> 15) << 31, e = (h >> 10) & 0x1f, m = h & 0x3ff, u;
     if (e == 0) {
         if (m == 0) u = s;
@@ -62,26 +72,64 @@ static inline float h2f(uint16_t h) {
     float f;
     memcpy(&f, &u, 4);
     return f;
+#endif
 }
 
-/* 27-point stencil, float16 storage, float32 arithmetic, float32 result (rounded by the caller). */
+/* One row of binary16 values -> binary32, eight at a time with F16C. */
+static void h2f_row(const uint16_t* restrict src, float* restrict dst, i64 n) {
+    i64 i = 0;
+#ifdef __F16C__
+    for (; i + 8 <= n; i += 8)
+        _mm256_storeu_ps(dst + i, _mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(src + i))));
+#endif
+    for (; i < n; ++i) dst[i] = h2f(src[i]);
+}
+
+/* 27-point stencil, float16 storage, float32 arithmetic, float32 result (rounded by the caller).
+ * Per output row the nine input rows (dz, dy) are converted once into zero-padded float32 rows (the
+ * 'zeros' boundary), then the 27 taps run as a vectorisable float loop; the taps are summed in the same
+ * (dz, dy, dx) order as the per-tap restatement, so the results are identical. */
 void oracle_stencil27_f16(const uint16_t* restrict u, float* restrict out, i64 Z, i64 Y, i64 X,
                           const float* restrict w /* 27, C order over (dz,dy,dx) in {-1,0,1}^3 */) {
-#pragma omp parallel for schedule(static)
-    for (i64 z = 0; z < Z; ++z)
-        for (i64 y = 0; y < Y; ++y)
-            for (i64 x = 0; x < X; ++x) {
-                float acc = 0.0f;
-                int k = 0;
-                for (int dz = -1; dz <= 1; ++dz)
-                    for (int dy = -1; dy <= 1; ++dy)
-                        for (int dx = -1; dx <= 1; ++dx, ++k) {
-                            const i64 zz = z + dz, yy = y + dy, xx = x + dx;
-                            const float v = (IN(zz, Z) && IN(yy, Y) && IN(xx, X)) ? h2f(u[(zz * Y + yy) * X + xx]) : 0.0f;
-                            acc += w[k] * v;
-                        }
-                out[(z * Y + y) * X + x] = acc;
+#pragma omp parallel
+    {
+        float* rows = (float*)malloc(sizeof(float) * 9 * (size_t)(X + 2));
+#pragma omp for schedule(static)
+        for (i64 z = 0; z < Z; ++z)
+            for (i64 y = 0; y < Y; ++y) {
+                for (int r = 0; r < 9; ++r) {
+                    const i64 zz = z + r / 3 - 1, yy = y + r % 3 - 1;
+                    float* row = rows + r * (X + 2);
+                    row[0] = row[X + 1] = 0.0f;
+                    if (IN(zz, Z) && IN(yy, Y)) h2f_row(u + (zz * Y + yy) * X, row + 1, X);
+                    else memset(row + 1, 0, sizeof(float) * (size_t)X);
+                }
+                float* restrict o = out + (z * Y + y) * X;
+                for (i64 x = 0; x < X; ++x) o[x] = 0.0f;
+                for (int k = 0; k < 27; ++k) {        /* tap-major: each cell still sums k = 0..26 in order */
+                    const float wk = w[k];
+                    const float* restrict row = rows + (k / 3) * (X + 2) + k % 3;
+                    for (i64 x = 0; x < X; ++x) o[x] += wk * row[x];
+                }
             }
+        free(rows);
+    }
+}
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* Thread count of the OpenMP loops above (1 = the reference's default CPU kernel, cpu_openmp off,
+ * _autodiff.py:487-489); returns the count in effect. */
+int oracle_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+    return omp_get_max_threads();
+#else
+    (void)n;
+    return 1;
+#endif
 }
 
 /* README op z = x*log(x*y) and its adjoint, float32. */

@@ -251,6 +251,7 @@ class AutoDiffOp:
         self._time_constant_fields = time_constant_fields
         self._kwargs = kwargs
         self.op_name = op_name
+        self._diff_fields_prefix = diff_fields_prefix
         self._do_common_subexpression_elimination = do_common_subexpression_elimination
         self._boundary_handling = boundary_handling
         self._diff_mode = diff_mode
@@ -372,6 +373,17 @@ class AutoDiffOp:
     @property
     def constant_fields(self):
         return self._constant_fields
+
+    @property
+    def diff_fields_prefix(self):
+        return self._diff_fields_prefix
+
+    def adjoint_name(self, field):
+        """Name of the adjoint of a forward field: the field map the adjoint derivation built
+        (``_autodiff.py:81-84``), else ``<diff_fields_prefix><name>`` (user-given backward assignments)."""
+        fmap = self._backward_field_map or {}
+        a = fmap.get(field)
+        return a.name if a is not None else self._diff_fields_prefix + field.name
 
     @property
     def time_constant_fields(self):

@@ -186,7 +186,7 @@ def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
     bwd_outputs = list(autodiff_obj.backward_output_fields) if backward_kernel else []
     bwd_inputs = list(autodiff_obj.backward_input_fields) if backward_kernel else []
     # adjoint of output i <-> grad_outputs[i]; match by name like the reference's prefixing
-    prefix = 'diff'
+    prefix = getattr(autodiff_obj, 'diff_fields_prefix', 'diff')
     field_map = getattr(autodiff_obj, '_backward_field_map', None) or {}
     adj_of = {}
     for f in fwd_outputs + fwd_inputs:

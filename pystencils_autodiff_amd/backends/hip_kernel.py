@@ -211,7 +211,8 @@ class HipStencilKernel:
                             tuple(int(x) for x in f.shape) if f.has_fixed_shape else None) for f in self.ir.fields]
         return self._specs
 
-    def __call__(self, halos=None, stream=None, force_schedule=None, z_range=None, x_border=False, **kwargs):
+    def __call__(self, halos=None, stream=None, force_schedule=None, z_range=None, x_border=False, z_limits=None,
+                 **kwargs):
         """Launch on the field tensors / scalars given by name.
 
         ``x_border=True`` asks the zsum schedule to also store zeros at x outside the iteration bounds of
@@ -219,12 +220,14 @@ class HipStencilKernel:
         below plane 0 / above plane Z-1 of a stencil field (``None`` = zeros); ``z_range``
         restricts the written planes of axis 0 — ``(lo, hi)``, or two disjoint ranges of equal
         length ``((lo0, hi0), (lo1, hi1))`` written by ONE launch (the two slab faces; both:
-        z-slab decomposition, ``zslab.py``).
+        z-slab decomposition, ``zslab.py``). ``z_limits=(lo, hi)`` replaces the kernel's own axis-0
+        iteration bounds (an interior-only kernel on a z-slab: the GLOBAL domain's interior, in local
+        plane numbers).
         The first call for a given (shape, alignment, halo layout, z range) builds a launch plan
         (variant, function handle, grid, argument layout); later calls only re-pack pointers.
         """
         prep = self.prepare(halos=halos, force_schedule=force_schedule, z_range=z_range, x_border=x_border,
-                            **kwargs)
+                            z_limits=z_limits, **kwargs)
         if prep is None:
             return None
         fn, grid, block, packed, xb, device = prep
@@ -235,7 +238,7 @@ class HipStencilKernel:
         rt.launch(fn, (grid,), (block,), packed, stream)
         return xb
 
-    def prepare(self, halos=None, force_schedule=None, z_range=None, x_border=False, **kwargs):
+    def prepare(self, halos=None, force_schedule=None, z_range=None, x_border=False, z_limits=None, **kwargs):
         """Everything of a launch but the launch: ``(function, grid, block, packed args, x_border done,
         device)``, or None for an empty domain (arguments as for ``__call__``)."""
         torch = _torch()
@@ -278,30 +281,36 @@ class HipStencilKernel:
         contiguous = all(t.is_contiguous() for t in tensors)
         strides = None if contiguous else tuple(tuple(t.stride()) for t in tensors)
         align = tuple(p % 32 == 0 for p in ptrs + hptrs)
-        key = (force_schedule, bool(x_border), shape, strides, align, tuple(h is not None for h in halo_list),
-               _zkey(z_range), device)
+        key = (force_schedule, bool(x_border), shape, strides, align,
+               tuple(h.numel() if h is not None else -1 for h in halo_list), _zkey(z_range),
+               tuple(z_limits) if z_limits is not None else None, device)
         plan = self._plans.get(key)
         if plan is None:
-            plan = self._make_plan(tensors, halo_list, shape, device, contiguous, force_schedule, z_range, x_border)
+            if z_limits is not None:
+                if not ir.ndim == 3 or not 0 <= int(z_limits[0]) <= int(z_limits[1]) <= shape[0]:
+                    raise ValueError(f'z_limits {z_limits} must lie in [0, {shape[0]}] of a 3-D kernel')
+            plan = self._make_plan(tensors, halo_list, shape, device, contiguous, force_schedule, z_range, x_border,
+                                   z_limits)
             self._plans[key] = plan
         self.last_variant = plan.variant
         if plan.grid == 0:
             return plan.fn, 0, plan.block, b'', plan.xb, device
         return plan.fn, plan.grid, plan.block, plan.pack(ptrs, hptrs, scalars), plan.xb, device
 
-    def _make_plan(self, tensors, halo_list, shape, device, contiguous, force_schedule, z_range, x_border=False):
+    def _make_plan(self, tensors, halo_list, shape, device, contiguous, force_schedule, z_range, x_border=False,
+                   z_limits=None):
         torch = _torch()
         ir = self.ir
         sched = force_schedule or self.schedule()
         if sched != 'generic' and not contiguous:
             sched = 'generic'
-        if (halo_list or z_range is not None) and sched != 'march':
+        if (halo_list or z_range is not None or z_limits is not None) and sched != 'march':
             raise ValueError('halo planes / z ranges are only supported by the march schedule')
         with torch.cuda.device(device):
             if sched == 'pointwise':
                 return self._plan_pointwise(tensors, shape, device)
             if sched == 'march':
-                return self._plan_march(tensors, halo_list, shape, device, z_range, x_border)
+                return self._plan_march(tensors, halo_list, shape, device, z_range, x_border, z_limits)
             return self._plan_generic(tensors, shape, device)
 
     def _scalar_kind(self):
@@ -375,11 +384,13 @@ class HipStencilKernel:
                 best = (t, zc)
         return best[1]
 
-    def march_launch_geometry(self, shape, cfg, z_range=None, slots=None):
+    def march_launch_geometry(self, shape, cfg, z_range=None, slots=None, z_limits=None):
         """(Z, Y, X), bounds and grid of the march schedule for a field shape; ``slots`` = resident
         workgroups (``_resident_slots``) switches the WS schedule to quantisation-aware chunks."""
         ir = self.ir
         bounds = ir.iteration_bounds(shape)
+        if z_limits is not None:
+            bounds[0] = (int(z_limits[0]), int(z_limits[1]))
         if z_range is not None and _is_pair(z_range):
             (a0, a1), (b0, b1) = [(int(a), int(b)) for a, b in z_range]
             lo, hi = bounds[0]
@@ -388,7 +399,7 @@ class HipStencilKernel:
             if not (lo <= a0 < a1 <= b0 < b1 <= hi) or a1 - a0 != b1 - b0:
                 raise ValueError(f'z_range pair {z_range} must be disjoint, ordered, of equal length '
                                  f'and inside [{lo}, {hi})')
-            geo = self.march_launch_geometry(shape, cfg, (a0, b1))
+            geo = self.march_launch_geometry(shape, cfg, (a0, b1), z_limits=z_limits)
             zc = a1 - a0
             geo.update(zlo=a0, zhi=b1, zc=zc, zstep=b0 - a0, grid=geo['ntx'] * geo['nty'] * 2)
             return geo
@@ -443,7 +454,7 @@ class HipStencilKernel:
         return dict(Z=Z, Y=Y, X=X, zlo=zlo, zhi=zhi, ylo=ylo, yhi=yhi, xlo=xlo, xhi=xhi, zc=zc, zstep=zc,
                     ntx=ntx, nty=nty, grid=nt * nchunks)
 
-    def _plan_march(self, tensors, halo_list, shape, device, z_range, x_border=False):
+    def _plan_march(self, tensors, halo_list, shape, device, z_range, x_border=False, z_limits=None):
         torch = _torch()
         ir = self.ir
         ve = self._vec_elems()
@@ -457,7 +468,7 @@ class HipStencilKernel:
             cfg = MarchConfig(**{**cfg.__dict__, 'VIEW2D': 'zy'})
         from .hip_emitter import ncomp
         if ir.has_index_dims and not cfg.ZSUM:
-            if halo_list or z_range is not None:
+            if halo_list or z_range is not None or z_limits is not None:
                 raise ValueError('vector-field kernels take halo planes / z ranges only in the zsum schedule')
             return self._plan_generic(tensors, shape, device)
         cmax = max([ncomp(f) for f in stencil] + [1])
@@ -473,7 +484,7 @@ class HipStencilKernel:
         fn = self.function(variant, device)
         ws = ws_geometry(ir, cfg)
         slots = self._resident_slots(fn, ws['block'], device) if ws else None
-        geo = self.march_launch_geometry(shape, cfg, z_range, slots=slots)
+        geo = self.march_launch_geometry(shape, cfg, z_range, slots=slots, z_limits=z_limits)
         grid = geo['grid'] if geo['yhi'] > geo['ylo'] and geo['xhi'] > geo['xlo'] else 0
         rz = march_geometry(ir, cfg)['RZ']
         plane = geo['Y'] * geo['X']

@@ -78,16 +78,22 @@ class RcclHalo:
         else:
             rt._check(opened, 'opening librccl')
         uid = ctypes.create_string_buffer(128)
+        status = 0
         if self.rank == 0:
-            rt._check(L.psad_rccl_unique_id(uid), 'ncclGetUniqueId')
-        obj = [uid.raw if self.rank == 0 else None]
+            status = L.psad_rccl_unique_id(uid)
+        # rank 0 sends (status, id): a failed ncclGetUniqueId makes every rank raise alike instead of
+        # leaving the others waiting for an id that never comes
+        obj = [(status, uid.raw) if self.rank == 0 else None]
         if not loopback:
             dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0,
                                        group=group)
+        status, uid_raw = obj[0]
+        if status:
+            raise RcclUnavailable(f'ncclGetUniqueId failed on rank 0 ({L.psad_error_string(status).decode()})')
         self.device = torch.device('cuda', torch.cuda.current_device()) if device is None else device
         with torch.cuda.device(self.device):
             comm = ctypes.c_void_p()
-            rt._check(L.psad_rccl_comm_init(obj[0], self.world, self.rank, ctypes.byref(comm)), 'ncclCommInitRank')
+            rt._check(L.psad_rccl_comm_init(uid_raw, self.world, self.rank, ctypes.byref(comm)), 'ncclCommInitRank')
             self.comm = comm
             self.stream = torch.cuda.Stream(device=self.device)
             # reused stream-order events (Stream.wait_stream would create two per sweep)
@@ -171,9 +177,15 @@ class ZSlabOp:
     ``fwd(**fields)`` / ``bwd(**fields)`` take the local slabs by field name (outputs
     preallocated, written in place) plus scalars, exchange the halos of every stencil field,
     and launch with interior / boundary overlap.
+
+    Both boundary modes of the reference (``_autodiff.py:479-542``): ``'zeros'`` (every cell written,
+    zero reads outside the global domain) and ``None`` (only the global interior ``[g, Z-g)`` of axis
+    0 — and ``[g, N-g)`` of the others — is written; the untouched border keeps what the caller
+    allocated). Interior-only slabs need their place in the global domain: ``z_offset`` / ``global_z``,
+    else gathered once from every rank's slab extent (collective, on the first sweep).
     """
 
-    def __init__(self, autodiff_op, use_cuda=True, group=None):
+    def __init__(self, autodiff_op, use_cuda=True, group=None, z_offset=None, global_z=None):
         self.op = autodiff_op
         self.use_cuda = use_cuda
         self.group = group
@@ -183,8 +195,8 @@ class ZSlabOp:
         for k in self.kernels.values():
             if k.ir.ndim != 3 and k.ir.ndim != 2:
                 raise ValueError('z-slab decomposition needs 2-D or 3-D fields')
-            if not k.ir.zeros:
-                raise ValueError("z-slab decomposition supports boundary_handling='zeros'")
+        self._span = {} if z_offset is None or global_z is None else None
+        self._fixed_span = None if self._span is not None else (int(z_offset), int(global_z))
         self._bufs = {}
         self._halo = None
         self._no_rccl = False
@@ -223,11 +235,62 @@ class ZSlabOp:
     def _radius(self, kernel, field):
         return max([abs(r.offsets[0]) for r in kernel.ir.reads if r.field.name == field.name] + [0])
 
+    def span(self, zl):
+        """``(z_offset, global_z)`` of a local slab of ``zl`` planes: given at construction, else the
+        slab extents of all ranks gathered once (collective), else the slab alone (no process group)."""
+        if self._fixed_span is not None:
+            return self._fixed_span
+        got = self._span.get(zl)
+        if got is None:
+            if dist.is_initialized() and dist.get_world_size(self.group) > 1:
+                sizes = [None] * dist.get_world_size(self.group)
+                dist.all_gather_object(sizes, int(zl), group=self.group)
+                r = dist.get_rank(self.group)
+                got = (sum(sizes[:r]), sum(sizes))
+            else:
+                got = (0, int(zl))
+            self._span[zl] = got
+        return got
+
+    def z_limits(self, kernel, zl):
+        """Local ``[lo, hi)`` of the planes this rank writes: all of them under ``'zeros'``, the part of
+        the global interior ``[g, Z-g)`` under ``boundary_handling=None``."""
+        ir = kernel.ir
+        if ir.zeros or ir.ghost_layers == 0:
+            return 0, zl
+        z0, Z = self.span(zl)
+        g = ir.ghost_layers
+        lo, hi = max(0, g - z0), min(zl, Z - g - z0)
+        return (lo, hi) if hi > lo else (0, 0)
+
     def fwd(self, **kwargs):
         return self._sweep('forward', kwargs)
 
     def bwd(self, **kwargs):
         return self._sweep('backward', kwargs)
+
+    @staticmethod
+    def _launches(zl, rz, lim):
+        """The interior range (no halo read) and the face ranges (read halos) of a split sweep,
+        restricted to the written planes ``lim``: ``(interior or None, [face ranges])``."""
+        lo, hi = lim
+
+        def clip(a, b):
+            a, b = max(a, lo), min(b, hi)
+            return (a, b) if b > a else None
+        if zl <= 2 * rz:
+            return None, [r for r in [clip(0, zl)] if r]
+        inner = clip(rz, zl - rz)
+        faces = [r for r in (clip(0, rz), clip(zl - rz, zl)) if r]
+        return inner, faces
+
+    @staticmethod
+    def _launch_faces(compiled, halos, faces, zlim, kwargs):
+        if len(faces) == 2 and faces[0][1] - faces[0][0] == faces[1][1] - faces[1][0]:
+            compiled(halos=halos, z_range=tuple(faces), z_limits=zlim, **kwargs)   # both faces in one launch
+        else:
+            for f in faces:
+                compiled(halos=halos, z_range=f, z_limits=zlim, **kwargs)
 
     def _sweep(self, which, kwargs):
         meta = self._meta.get(which)
@@ -238,6 +301,8 @@ class ZSlabOp:
         k, stencil, rz = meta
         ir = k.ir
         ref = kwargs[ir.fields_written[0].name]
+        zl = ref.shape[0]
+        zlim = self.z_limits(k, zl)
         split = rz > 0 and dist.is_initialized() and dist.get_world_size(self.group) > 1
         halo = None
         if rz > 0 and self._halo is not None:
@@ -245,50 +310,57 @@ class ZSlabOp:
         elif split:
             halo = self._rccl(ref.device)
         if halo is not None:
-            self._sweep_rccl(k, halo, stencil, rz, kwargs)
+            self._sweep_rccl(k, halo, stencil, rz, kwargs, zlim)
             return
         pending, halos = [], {}
         for f in stencil:
             t = kwargs[f.name]
-            bufs = self._bufs.get((which, f.name, t.dtype, tuple(t.shape[1:]), t.device))
-            works, lo, hi = exchange_halos(t, rz, self.group, bufs)
-            self._bufs[(which, f.name, t.dtype, tuple(t.shape[1:]), t.device)] = (lo, hi)
+            key = (which, f.name, rz, t.dtype, tuple(t.shape[1:]), t.device)
+            works, lo, hi = exchange_halos(t, rz, self.group, self._bufs.get(key))
+            self._bufs[key] = (lo, hi)
             pending += works
             halos[f.name] = (lo, hi)
-        zl = ref.shape[0]
+        kz = None if zlim == (0, zl) else zlim
         if self.use_cuda:
             compiled = k.compile()
             if split:
-                if zl > 2 * rz:
-                    compiled(z_range=(rz, zl - rz), **kwargs)          # interior overlaps the exchange
+                inner, faces = self._launches(zl, rz, zlim)
+                if inner:
+                    compiled(z_range=inner, z_limits=kz, **kwargs)   # interior overlaps the exchange
                 for w in pending:
                     w.wait()                                          # current stream waits on RCCL
-                if zl > 2 * rz:                                       # both faces in one launch
-                    compiled(halos=halos, z_range=((0, rz), (zl - rz, zl)), **kwargs)
-                else:
-                    compiled(halos=halos, z_range=(0, zl), **kwargs)
-            else:
-                compiled(halos=halos, **kwargs)
+                self._launch_faces(compiled, halos, faces, kz, kwargs)
+            elif zlim[1] > zlim[0]:
+                compiled(halos=halos, z_limits=kz, **kwargs)
             return
-        # CPU / gloo: evaluate a ghosted copy with the C kernel
+        # CPU / gloo: evaluate a ghosted copy with the C kernel; under boundary_handling=None the copy
+        # carries g >= rz planes per side so that its own interior covers every local plane
         for w in pending:
             w.wait()
+        pad = rz if (ir.zeros or ir.ghost_layers == 0) else max(rz, ir.ghost_layers)
         ghosted = dict(kwargs)
         outs = {f.name: kwargs[f.name] for f in ir.fields_written}
+        read_names = {r.field.name for r in ir.reads}
+
+        def zeros(n, t):
+            return torch.zeros((n,) + tuple(t.shape[1:]), dtype=t.dtype)
         for f in ir.fields:
             t = kwargs[f.name]
+            if not pad:
+                continue
             if f in stencil:
                 lo, hi = halos[f.name]
-                zeros = torch.zeros((rz,) + tuple(t.shape[1:]), dtype=t.dtype)
-                ghosted[f.name] = torch.cat([lo if lo is not None else zeros, t, hi if hi is not None else zeros])
-            elif rz:
-                pad = torch.zeros((rz,) + tuple(t.shape[1:]), dtype=t.dtype)
-                ghosted[f.name] = torch.cat([pad, t, pad]) if f not in ir.fields_written else \
-                    torch.zeros((zl + 2 * rz,) + tuple(t.shape[1:]), dtype=t.dtype)
+                ghosted[f.name] = torch.cat([zeros(pad - rz, t), lo if lo is not None else zeros(rz, t), t,
+                                             hi if hi is not None else zeros(rz, t), zeros(pad - rz, t)])
+            elif f.name in outs and f.name not in read_names:
+                ghosted[f.name] = zeros(zl + 2 * pad, t)
+            else:
+                ghosted[f.name] = torch.cat([zeros(pad, t), t, zeros(pad, t)])
         k.compile()(**ghosted)
+        a, b = zlim
         for name, t in outs.items():
-            if rz:
-                t.copy_(ghosted[name][rz:rz + zl])
+            if pad and b > a:
+                t[a:b].copy_(ghosted[name][pad + a:pad + b])
 
     @staticmethod
     def _peers(halo):
@@ -306,7 +378,7 @@ class ZSlabOp:
                 raise ValueError(f"slab of {t.shape[0]} planes is thinner than the stencil radius {rz}")
             if not t.is_contiguous():
                 raise ValueError(f"slab of '{name}' must be contiguous for the RCCL face exchange")
-            key = ('rccl', name, t.dtype, t.shape, t.device)
+            key = ('rccl', name, rz, t.dtype, t.shape, t.device)      # per radius: fwd and bwd may differ
             bufs = self._bufs.get(key)
             if bufs is None:
                 shape = (rz,) + tuple(t.shape[1:])
@@ -349,7 +421,7 @@ class ZSlabOp:
                 halo.exchange(planes, *self._peers(halo))
         halo.stream.synchronize()
 
-    def _sweep_rccl(self, k, halo, stencil, rz, kwargs):
+    def _sweep_rccl(self, k, halo, stencil, rz, kwargs, zlim=None):
         """Faces out on the halo stream (one RCCL group for every stencil field) while the interior
         planes run on the caller's stream; then the two face ranges in one launch."""
         peer_lo, peer_hi = self._peers(halo)
@@ -360,30 +432,50 @@ class ZSlabOp:
         halo.exchange(planes, peer_lo, peer_hi)
         compiled = k.compile()
         zl = kwargs[k.ir.fields_written[0].name].shape[0]
-        if zl > 2 * rz:
-            compiled(z_range=(rz, zl - rz), **kwargs)  # interior overlaps the exchange
+        zlim = (0, zl) if zlim is None else zlim
+        kz = None if zlim == (0, zl) else zlim
+        inner, faces = self._launches(zl, rz, zlim)
+        if inner:
+            compiled(z_range=inner, z_limits=kz, **kwargs)  # interior overlaps the exchange
         halo.ev_halos.record(halo.stream)
         cur.wait_event(halo.ev_halos)
-        if zl > 2 * rz:
-            compiled(halos=halos, z_range=((0, rz), (zl - rz, zl)), **kwargs)
-        else:
-            compiled(halos=halos, z_range=(0, zl), **kwargs)
+        self._launch_faces(compiled, halos, faces, kz, kwargs)
+
+    def _alloc(self, kernel, name, like, dtype, read):
+        """An output / gradient slab: zeros when the kernel accumulates into it or (CPU) leaves a border;
+        under ``boundary_handling=None`` on the GPU uninitialised plus one zero fill of the planes, rows
+        and columns the kernel does not write (the reference's ``torch.zeros`` values)."""
+        ir = kernel.ir
+        if read or (not ir.zeros and ir.ghost_layers and not like.is_cuda):
+            return torch.zeros_like(like, dtype=dtype)
+        t = torch.empty_like(like, dtype=dtype)
+        if not ir.zeros and ir.ghost_layers:
+            from .backends.hip_kernel import zero_border
+            bounds = ir.iteration_bounds(tuple(like.shape[:ir.ndim]))
+            bounds[0] = self.z_limits(kernel, like.shape[0])
+            ncomp = 1
+            for n in like.shape[ir.ndim:]:
+                ncomp *= int(n)
+            zero_border(t, bounds, ncomp)
+        return t
 
     def autograd_function(self):
         """A ``torch.autograd.Function`` over this rank's slabs with the drop-in op's contract:
         ``apply(*slabs)`` in ``forward_input_fields`` order returns the output slabs (tuple, in
         ``forward_output_fields`` order); ``backward`` exchanges the gradient halos and returns the
-        input gradients. Scalars come from ``class_kwargs``."""
+        input gradients. Scalars come from ``class_kwargs``. Adjoint names follow the op's field map
+        / ``diff_fields_prefix`` like the single-device op (``_torch_native.py:96-100``)."""
         op = self.op
         zop = self
         fwd_inputs = list(op.forward_input_fields)
         fwd_outputs = list(op.forward_output_fields)
         fk, bk = self.kernels['forward'], self.kernels['backward']
         fwd_names = {f.name for f in fk.ir.fields}
+        fwd_read = {r.field.name for r in fk.ir.reads}
         bwd_names = {f.name for f in bk.ir.fields}
         bwd_outputs = [f.name for f in op.backward_output_fields]
         bwd_read = {r.field.name for r in bk.ir.reads}        # accumulated adjoints start from zeros
-        prefix = 'diff'
+        adj = {f.name: op.adjoint_name(f) for f in fwd_inputs + fwd_outputs}
 
         def tdtype(f):
             return getattr(torch, f.dtype.numpy_dtype.name)
@@ -395,7 +487,7 @@ class ZSlabOp:
             def forward(ctx, *slabs):
                 kw = {f.name: t.contiguous() for f, t in zip(fwd_inputs, slabs) if f.name in fwd_names}
                 kw.update({s.name: ZSlabFunction.class_kwargs[s.name] for s in fk.ir.scalars})
-                outs = [torch.empty_like(slabs[0], dtype=tdtype(f)) for f in fwd_outputs]
+                outs = [zop._alloc(fk, f.name, slabs[0], tdtype(f), f.name in fwd_read) for f in fwd_outputs]
                 kw.update({f.name: t for f, t in zip(fwd_outputs, outs)})
                 zop.fwd(**kw)
                 saved = [n for n in [f.name for f in fwd_inputs + fwd_outputs] if n in bwd_names and n in kw]
@@ -410,14 +502,14 @@ class ZSlabOp:
                 kw.update({s.name: ZSlabFunction.class_kwargs[s.name] for s in bk.ir.scalars})
                 like = next(g for g in grads if g is not None)
                 for f, g in zip(fwd_outputs, grads):
-                    if prefix + f.name in bwd_names:
-                        kw[prefix + f.name] = (g if g is not None else torch.zeros_like(like)).contiguous()
+                    if adj[f.name] in bwd_names:
+                        kw[adj[f.name]] = (g if g is not None else torch.zeros_like(like)).contiguous()
                 res = {}
                 for name in bwd_outputs:
-                    res[name] = (torch.zeros_like if name in bwd_read else torch.empty_like)(like)
+                    res[name] = zop._alloc(bk, name, like, like.dtype, name in bwd_read)
                     kw[name] = res[name]
                 zop.bwd(**kw)
-                return tuple(res.get(prefix + f.name) for f in fwd_inputs[:ctx.n_inputs])
+                return tuple(res.get(adj[f.name]) for f in fwd_inputs[:ctx.n_inputs])
 
         ZSlabFunction.__name__ = f"{op.op_name}_zslab"
         return ZSlabFunction

@@ -72,7 +72,8 @@ class _GlooHalo:
         pass
 
 
-def _worker(rank, world, port, shape, builder_name, use_cuda, result_dir):
+def _worker(rank, world, port, shape, builder_name, use_cuda, result_dir, opts=None):
+    opts = opts or {}
     import sys
     sys.path.insert(0, ROOT)
     import pystencils_autodiff_amd as pa
@@ -81,7 +82,8 @@ def _worker(rank, world, port, shape, builder_name, use_cuda, result_dir):
     dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank, world_size=world)
     try:
         builder = getattr(W, builder_name)
-        op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
+        op = pa.AutoDiffOp(builder(), boundary_handling=opts.get('bh', 'zeros'),
+                           diff_fields_prefix=opts.get('prefix', 'diff'))
         rng = np.random.default_rng(0)
         dt = _dtype(builder_name)
         u = rng.uniform(0, 1, shape).astype(dt)
@@ -95,6 +97,9 @@ def _worker(rank, world, port, shape, builder_name, use_cuda, result_dir):
         z = ZSlabOp(op, use_cuda=use_cuda)
         if os.environ.get('PSAD_TEST_EMULATED_RCCL'):
             z._halo = _GlooHalo()
+            # the setup exchange bench.py runs before its timed loop: real peers, per-rank slab shapes
+            # (remainder planes) and receive buffers the sweeps below then reuse
+            z.warm_exchange(**{'u': ul, op.adjoint_name(op.forward_output_fields[0]): dl})
         if os.environ.get('PSAD_TEST_ZSLAB_AUTOGRAD'):
             fn = z.autograd_function()
             uu = ul.clone().requires_grad_(True)
@@ -103,8 +108,9 @@ def _worker(rank, world, port, shape, builder_name, use_cuda, result_dir):
             out.copy_(o.detach())
             du.copy_(uu.grad)
         else:
+            p = opts.get('prefix', 'diff')
             z.fwd(u=ul, out=out)
-            z.bwd(diffout=dl, diffu=du)
+            z.bwd(**{p + 'out': dl, p + 'u': du})
         if use_cuda:
             torch.cuda.synchronize()
         np.save(os.path.join(result_dir, f'out_{rank}.npy'), out.cpu().numpy())
@@ -113,9 +119,10 @@ def _worker(rank, world, port, shape, builder_name, use_cuda, result_dir):
         dist.destroy_process_group()
 
 
-def _run(world, shape, builder_name, use_cuda, tmp_path):
+def _run(world, shape, builder_name, use_cuda, tmp_path, **opts):
     port = _free_port()
-    mp.spawn(_worker, args=(world, port, shape, builder_name, use_cuda, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, port, shape, builder_name, use_cuda, str(tmp_path), opts), nprocs=world,
+             join=True)
     out = np.concatenate([np.load(tmp_path / f'out_{r}.npy') for r in range(world)])
     du = np.concatenate([np.load(tmp_path / f'du_{r}.npy') for r in range(world)])
     from oracle import stencils as S
@@ -125,22 +132,47 @@ def _run(world, shape, builder_name, use_cuda, tmp_path):
     dt = _dtype(builder_name)
     u = rng.uniform(0, 1, shape).astype(dt)
     d = rng.uniform(-1, 1, shape).astype(dt)
-    return out, du, S.linear_stencil(u, taps), S.linear_stencil(d, S.flip(taps))
+    ref_out, ref_du = S.linear_stencil(u, taps), S.linear_stencil(d, S.flip(taps))
+    if opts.get('bh', 'zeros') is None:
+        # interior-only kernels (_autodiff.py:485-486,518-519): interior cells read only in-domain
+        # neighbours, so they equal the 'zeros' values; the radius-1 border keeps torch.zeros
+        ref_out, ref_du = _interior(ref_out, 1), _interior(ref_du, 1)
+    return out, du, ref_out, ref_du
 
 
+def _interior(a, g):
+    b = np.zeros_like(a)
+    sl = tuple(slice(g, n - g) for n in a.shape)
+    b[sl] = a[sl]
+    return b
+
+
+@pytest.mark.parametrize('bh', ['zeros', None])
 @pytest.mark.parametrize('world,shape', [(2, (10, 9, 12)), (3, (13, 6, 7))])
 @pytest.mark.parametrize('builder_name', ['asym_7pt', 'diffusion_7pt'])
-def test_zslab_gloo_cpu(world, shape, builder_name, tmp_path):
+def test_zslab_gloo_cpu(world, shape, builder_name, bh, tmp_path):
     from tests.conftest import assert_close_rel
-    out, du, ref_out, ref_du = _run(world, shape, builder_name, False, tmp_path)
+    out, du, ref_out, ref_du = _run(world, shape, builder_name, False, tmp_path, bh=bh)
     assert_close_rel(out, ref_out, 1e-6, 'out')
     assert_close_rel(du, ref_du, 1e-6, 'diffu')
 
 
-def test_zslab_autograd_function_gloo_cpu(tmp_path, monkeypatch):
+@pytest.mark.parametrize('bh,prefix', [('zeros', 'diff'), ('zeros', 'grad'), (None, 'grad')])
+def test_zslab_autograd_function_gloo_cpu(tmp_path, monkeypatch, bh, prefix):
+    """The slab Function with the reference's own keyword surface: a non-default ``diff_fields_prefix``
+    (adjoint names from the op's field map, ``_autodiff.py:81-84``) and the default boundary (None)."""
     from tests.conftest import assert_close_rel
     monkeypatch.setenv('PSAD_TEST_ZSLAB_AUTOGRAD', '1')
-    out, du, ref_out, ref_du = _run(2, (11, 8, 9), 'asym_7pt', False, tmp_path)
+    out, du, ref_out, ref_du = _run(2, (11, 8, 9), 'asym_7pt', False, tmp_path, bh=bh, prefix=prefix)
+    assert_close_rel(out, ref_out, 1e-6, 'out')
+    assert_close_rel(du, ref_du, 1e-6, 'diffu')
+
+
+def test_zslab_none_mode_thin_edge_slabs(tmp_path):
+    """boundary_handling=None with 4 ranks on 6 planes: the edge ranks hold a single global-border plane
+    plus one interior plane, the inner ranks read both neighbours' faces."""
+    from tests.conftest import assert_close_rel
+    out, du, ref_out, ref_du = _run(4, (7, 6, 9), 'diffusion_7pt', False, tmp_path, bh=None)
     assert_close_rel(out, ref_out, 1e-6, 'out')
     assert_close_rel(du, ref_du, 1e-6, 'diffu')
 
@@ -156,11 +188,12 @@ def test_slab_bounds_cover_domain():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('bh', ['zeros', None])
 @pytest.mark.parametrize('world,shape', [(2, (24, 40, 64)), (3, (19, 33, 70))])
 @pytest.mark.parametrize('builder_name', ['asym_7pt', 'diffusion_7pt'])
-def test_zslab_gloo_gpu_halo_path(world, shape, builder_name, tmp_path):
+def test_zslab_gloo_gpu_halo_path(world, shape, builder_name, bh, tmp_path):
     from tests.conftest import assert_close_rel
-    out, du, ref_out, ref_du = _run(world, shape, builder_name, True, tmp_path)
+    out, du, ref_out, ref_du = _run(world, shape, builder_name, True, tmp_path, bh=bh)
     assert_close_rel(out, ref_out, 1e-6, 'out')
     assert_close_rel(du, ref_du, 1e-6, 'diffu')
 
@@ -235,13 +268,16 @@ def test_zslab_rccl_loopback_sweep(builder_name, shape):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('world,shape', [(2, (24, 40, 64)), (3, (19, 33, 70)), (3, (7, 9, 64))])
+@pytest.mark.parametrize('world,shape,bh', [(2, (24, 40, 64), 'zeros'), (3, (19, 33, 70), 'zeros'),
+                                            (3, (7, 9, 64), 'zeros'), (3, (19, 33, 70), None),
+                                            (3, (7, 9, 64), None)])
 @pytest.mark.parametrize('builder_name', ['asym_7pt', 'stencil_27pt'])
-def test_zslab_rccl_sweep_emulated_ranks(world, shape, builder_name, tmp_path, monkeypatch):
-    """ZSlabOp's RCCL sweep with 2-3 ranks on one GPU, the exchange carried by _GlooHalo."""
+def test_zslab_rccl_sweep_emulated_ranks(world, shape, builder_name, bh, tmp_path, monkeypatch):
+    """ZSlabOp's RCCL sweep with 2-3 ranks on one GPU, the exchange carried by _GlooHalo (after the
+    setup exchange bench.py runs, ``warm_exchange``), both boundary modes."""
     from tests.conftest import assert_close_rel
     monkeypatch.setenv('PSAD_TEST_EMULATED_RCCL', '1')
-    out, du, ref_out, ref_du = _run(world, shape, builder_name, True, tmp_path)
+    out, du, ref_out, ref_du = _run(world, shape, builder_name, True, tmp_path, bh=bh)
     tol = 1e-3 if builder_name == 'stencil_27pt' else 1e-6
     assert_close_rel(out, ref_out, tol, 'out')
     assert_close_rel(du, ref_du, tol, 'diffu')

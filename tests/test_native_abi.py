@@ -249,20 +249,28 @@ def test_quantized_chunk_model():
 
 
 def test_rccl_entry_points_report_errors_without_gpu():
-    """The RCCL halo entry points fail with a described code (never abort) when librccl is missing."""
-    import ctypes
-    from pystencils_autodiff_amd.backends import hip_runtime as rt
-    L = rt.lib()
-    rc = L.psad_rccl_open(b'/nonexistent/librccl.so')
-    assert rc == 20100
-    assert b'RCCL' in L.psad_error_string(rc)
-    uid = ctypes.create_string_buffer(128)
-    # still not opened (the failed open left no handle): every call reports the same code
-    assert L.psad_rccl_unique_id(uid) in (0, 20100)
-    if L.psad_rccl_unique_id(uid) == 20100:
-        comm = ctypes.c_void_p()
-        assert L.psad_rccl_comm_init(uid, 1, 0, ctypes.byref(comm)) == 20100
-        vp = ctypes.c_void_p
-        z = (vp * 1)(0)
-        n = (ctypes.c_size_t * 1)(0)
-        assert L.psad_halo_exchange(None, 1, z, z, z, z, n, -1, -1, None) == 20100
+    """The RCCL halo entry points fail with a described code (never abort) when librccl is missing.
+    Run in a fresh interpreter: ``psad_rccl_open`` keeps the first library a process opened, so an
+    earlier test that loaded the real librccl would make the failure path unobservable here."""
+    import subprocess
+    import sys
+    code = r"""
+import ctypes, sys
+sys.path.insert(0, %r)
+from pystencils_autodiff_amd.backends import hip_runtime as rt
+L = rt.lib()
+rc = L.psad_rccl_open(b'/nonexistent/librccl.so')
+assert rc == 20100, rc
+assert b'RCCL' in L.psad_error_string(rc)
+uid = ctypes.create_string_buffer(128)
+assert L.psad_rccl_unique_id(uid) == 20100
+comm = ctypes.c_void_p()
+assert L.psad_rccl_comm_init(uid, 1, 0, ctypes.byref(comm)) == 20100
+vp = ctypes.c_void_p
+z = (vp * 1)(0)
+n = (ctypes.c_size_t * 1)(0)
+assert L.psad_halo_exchange(None, 1, z, z, z, z, n, -1, -1, None) == 20100
+print('ok')
+""" % ROOT
+    proc = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=120)
+    assert proc.returncode == 0 and 'ok' in proc.stdout, proc.stdout + proc.stderr
