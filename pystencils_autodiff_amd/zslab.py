@@ -320,7 +320,8 @@ class ZSlabOp:
             self._bufs[key] = (lo, hi)
             pending += works
             halos[f.name] = (lo, hi)
-        kz = None if zlim == (0, zl) else zlim
+        # interior-only kernels always take the limits (their own bounds would skip the slab's end planes)
+        kz = None if (ir.zeros or ir.ghost_layers == 0) else zlim
         if self.use_cuda:
             compiled = k.compile()
             if split:
@@ -433,7 +434,7 @@ class ZSlabOp:
         compiled = k.compile()
         zl = kwargs[k.ir.fields_written[0].name].shape[0]
         zlim = (0, zl) if zlim is None else zlim
-        kz = None if zlim == (0, zl) else zlim
+        kz = None if (k.ir.zeros or k.ir.ghost_layers == 0) else zlim
         inner, faces = self._launches(zl, rz, zlim)
         if inner:
             compiled(z_range=inner, z_limits=kz, **kwargs)  # interior overlaps the exchange
