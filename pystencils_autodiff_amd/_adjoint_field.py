@@ -25,6 +25,7 @@ class AdjointField(Field):
                         for s in forward_field.strides)
         super().__init__(name, ftype, forward_field.dtype, forward_field.layout, shape, strides)
         self._index_dimensions = forward_field.index_dimensions
+        self._soa = forward_field.is_soa
         self.corresponding_forward_field = forward_field
         self.name_prefix = name_prefix
         self.latex_name = ADJOINT_FIELD_LATEX_HIGHLIGHT % (forward_field.latex_name or forward_field.name)

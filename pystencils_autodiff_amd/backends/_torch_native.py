@@ -102,21 +102,46 @@ BORDER_ZERO_MIN = 1 << 22
 BORDER_KERNEL = True
 
 
+def _soa_empty(shape, sdim, factory, dtype, device):
+    """A tensor of ``shape`` (spatial axes, then component axes) in fzyx (SoA) memory order: allocated
+    components-first and viewed with the component axes last."""
+    import torch
+    nidx = len(shape) - sdim
+    t = factory(tuple(shape[sdim:]) + tuple(shape[:sdim]), dtype=dtype, device=device)
+    return t.permute(*range(nidx, nidx + sdim), *range(nidx)) if nidx else t
+
+
+def _soa_components(t, sdim):
+    """The C-contiguous per-component views of an fzyx tensor."""
+    import itertools
+    return [t[(Ellipsis,) + idx] for idx in itertools.product(*[range(int(n)) for n in t.shape[sdim:]])]
+
+
 def _allocator(kernel, field_name, read_names=()):
     """How an output is allocated: ``torch.empty`` when the kernel writes all of it; for an interior-only
     kernel (``boundary_handling=None``, the reference's default) that assigns every component at offset 0,
     ``torch.empty`` plus zero fills of the untouched border slabs — the reference's ``torch.zeros``
-    values without a memset pass over the whole field; otherwise ``torch.zeros``."""
+    values without a memset pass over the whole field; otherwise ``torch.zeros``. fzyx (SoA) outputs are
+    allocated components-first (``_soa_empty``)."""
     import torch
-    if field_name in read_names:
-        return torch.zeros
-    if _full_write(kernel, field_name):
-        return torch.empty
     ir = kernel.ir
+    sdim = ir.ndim
+    soa = any(f.name == field_name and f.is_soa for f in ir.fields_written)
+
+    def plain(factory):
+        if not soa:
+            return factory
+
+        def alloc(shape, dtype, device):
+            return _soa_empty(shape, sdim, factory, dtype, device)
+        return alloc
+    if field_name in read_names:
+        return plain(torch.zeros)
+    if _full_write(kernel, field_name):
+        return plain(torch.empty)
     if not _components_complete(kernel, field_name) or \
             any(any(o != 0 for o in off) for fld, off, _, _ in ir.stores if fld.name == field_name):
-        return torch.zeros
-    sdim = ir.ndim
+        return plain(torch.zeros)
 
     ncomp = 1
     for f in ir.fields_written:
@@ -125,7 +150,10 @@ def _allocator(kernel, field_name, read_names=()):
                 ncomp *= int(n)
 
     def alloc(shape, dtype, device, pending=None):
-        t = torch.empty(shape, dtype=dtype, device=device)
+        t = _soa_empty(shape, sdim, torch.empty, dtype, device) if soa else \
+            torch.empty(shape, dtype=dtype, device=device)
+        parts = _soa_components(t, sdim) if soa else [t]
+        per = 1 if soa else ncomp
         if t.is_cuda:
             if not BORDER_KERNEL:
                 return t.zero_()
@@ -133,9 +161,10 @@ def _allocator(kernel, field_name, read_names=()):
             bounds = ir.iteration_bounds(tuple(shape[:sdim]))
             # the x ends of the interior rows are left to the kernel's x_border stores (or, if its launch
             # cannot, to a second fill after it: ``pending``)
-            zero_border(t, bounds, ncomp, x=pending is None)
-            if pending is not None:
-                pending.append(lambda: zero_border(t, bounds, ncomp, zy=False))
+            for p in parts:
+                zero_border(p, bounds, per, x=pending is None)
+                if pending is not None:
+                    pending.append(lambda p=p: zero_border(p, bounds, per, zy=False))
             return t
         if t.numel() < BORDER_ZERO_MIN:
             return t.zero_()
@@ -230,7 +259,10 @@ def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
                     f.spatial_dimensions, _index_shape(f)) for f in bwd_outputs]
         in_adj = [adj_of[f.name].name if adj_of.get(f.name) is not None else None for f in fwd_inputs]
 
-    def _to_device(t):
+    soa_fields = {f.name: f.spatial_dimensions for f in fwd_inputs + fwd_outputs if f.is_soa}
+
+    def _to_device(t, name=None):
+        """On the op's device, C-contiguous — or, for an fzyx (SoA) field, in fzyx order."""
         if not isinstance(t, torch.Tensor):
             return t
         if use_cuda:
@@ -238,10 +270,16 @@ def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
                 t = t.cuda()
         elif t.is_cuda:
             t = t.cpu()
+        sdim = soa_fields.get(name)
+        if sdim is not None and t.dim() > sdim:
+            from ..ps.field import _soa_strides
+            if tuple(t.stride()) != _soa_strides(tuple(t.shape), t.dim() - sdim):
+                t = _soa_empty(tuple(t.shape), sdim, torch.empty, t.dtype, t.device).copy_(t)
+            return t
         return t if t.is_contiguous() else t.contiguous()
 
     def forward(ctx, *args):
-        args = [_to_device(a) for a in args]
+        args = [_to_device(a, fwd_inputs[i].name if i < len(fwd_inputs) else None) for i, a in enumerate(args)]
         first = next((a for a in args if isinstance(a, torch.Tensor)), None)
         if first is None:
             raise ValueError(f"{op_name}: at least one input tensor is required")
@@ -280,8 +318,11 @@ def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
         like = None
         for g, (aname, dtype, fixed, strides, fname) in zip(grad_outputs, grad_specs):
             if g is None:
-                g = torch.zeros(fixed if fixed is not None else ctx.like_shape, dtype=dtype, device=ctx.like_device)
-            g = _to_device(g)
+                shape = fixed if fixed is not None else ctx.like_shape
+                g = _soa_empty(shape, soa_fields[fname], torch.zeros, dtype, ctx.like_device) \
+                    if fname in soa_fields and len(shape) > soa_fields[fname] else \
+                    torch.zeros(shape, dtype=dtype, device=ctx.like_device)
+            g = _to_device(g, fname)
             assert g.is_cuda == use_cuda, ("Some of the tensors where on the wrong device. "
                                            f"Op was compiled for CUDA: {str(use_cuda)}")
             if fixed is not None:

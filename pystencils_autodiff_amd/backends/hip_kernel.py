@@ -129,13 +129,15 @@ def _torch():
 
 class HipStencilKernel:
     def __init__(self, kernel):
+        from .kernel_ir import split_soa
         self.kernel = kernel
-        self.ir = kernel.ir
+        # fzyx vector fields run as one scalar field per component (kernel_ir.split_soa)
+        self.ir, self._soa = split_soa(kernel.ir)
         self.name = kernel.function_name
         self._variants = {}            # variant key -> (source, kernel name)
         self._plans = {}               # launch key -> _Plan
         self._specs = None
-        self._ref_index = [f.name for f in kernel.ir.fields].index(kernel.ir.fields_written[0].name)
+        self._ref_index = [f.name for f in self.ir.fields].index(self.ir.fields_written[0].name)
         self.last_variant = None
 
     # -- sources --------------------------------------------------------------------------------
@@ -243,6 +245,8 @@ class HipStencilKernel:
         device)``, or None for an empty domain (arguments as for ``__call__``)."""
         torch = _torch()
         ir = self.ir
+        if self._soa:
+            kwargs = self._bind_components(kwargs)
         tensors = []
         for name, dtype, ndim, fixed in self._field_specs():
             t = kwargs.get(name)
@@ -296,6 +300,25 @@ class HipStencilKernel:
         if plan.grid == 0:
             return plan.fn, 0, plan.block, b'', plan.xb, device
         return plan.fn, plan.grid, plan.block, plan.pack(ptrs, hptrs, scalars), plan.xb, device
+
+    def _bind_components(self, kwargs):
+        """fzyx vector tensors → one view per component (``split_soa``'s scalar fields); any strides are
+        accepted (a component whose plane is not C-contiguous takes the generic schedule)."""
+        torch = _torch()
+        kwargs = dict(kwargs)
+        sdim = self.ir.ndim
+        for name, comps in self._soa.items():
+            t = kwargs.pop(name, None)
+            if t is None:
+                raise TypeError(f"{self.name}: missing field argument '{name}'")
+            if not isinstance(t, torch.Tensor):
+                raise TypeError(f"{self.name}: field '{name}' must be a torch tensor on the GPU")
+            nidx = len(comps[0][1])
+            if t.dim() != sdim + nidx:
+                raise ValueError(f"{self.name}: field '{name}' expects {sdim + nidx} dims, got {t.dim()}")
+            for cfield, idx in comps:
+                kwargs[cfield.name] = t[(Ellipsis,) + tuple(idx)]
+        return kwargs
 
     def _make_plan(self, tensors, halo_list, shape, device, contiguous, force_schedule, z_range, x_border=False,
                    z_limits=None):

@@ -209,6 +209,41 @@ def lower(assignments, boundary_handling=None, data_type=None):
     return ir
 
 
+def split_soa(ir):
+    """The GPU view of a kernel with fzyx (SoA) vector fields: every component of such a field becomes a
+    scalar field of its own (``Field.component_field``), so each component plane is a C-contiguous array
+    and the stencil schedules (``zsum``, ``march``, ``pointwise``) run unchanged on it — a component read
+    ``u[o](k)`` is a scalar read ``u__ck[o]``. Returns ``(ir, components)`` with ``components`` =
+    ``{field name: [(component field, index), ...]}`` (empty, and ``ir`` itself, without SoA fields).
+    The split happens after ``lower``, so components completed with zero stores are kept as stores."""
+    soa = [f for f in ir.fields if f.is_soa]
+    if not soa:
+        return ir, {}
+    comps, sub = {}, {}
+    for f in soa:
+        comps[f.name] = [(f.component_field(idx), idx)
+                         for idx in itertools.product(*[range(int(n)) for n in f.index_shape])]
+    cf = {(name, idx): c for name, lst in comps.items() for c, idx in lst}
+
+    def acc(field, offsets, idx):
+        return Field.Access(cf[(field.name, tuple(idx))], tuple(offsets))
+    for r in ir.reads:
+        if r.field.is_soa:
+            sub[Field.Access(r.field, r.offsets, r.index)] = acc(r.field, r.offsets, r.index)
+    subexpressions = [(s, e.xreplace(sub)) for s, e in ir.subexpressions]
+    stores = []
+    for f, offs, idx, rhs in ir.stores:
+        lhs = acc(f, offs, idx) if f.is_soa else Field.Access(f, offs, idx)
+        stores.append((lhs, rhs.xreplace(sub)))
+    from ..ps import Assignment
+    ac = AssignmentCollection([Assignment(lhs, rhs) for lhs, rhs in stores],
+                              [Assignment(s, e) for s, e in subexpressions])
+    out = lower(ac, 'zeros' if ir.zeros else None, np.dtype(ir.compute_dtype).name)
+    if not out.zeros and out.ghost_layers != ir.ghost_layers:
+        raise AssertionError('SoA split changed the iteration space')
+    return out, comps
+
+
 class Parameter:
     """Kernel parameter (mirrors pystencils ``KernelFunction.Parameter``: ``.symbol.name``)."""
 

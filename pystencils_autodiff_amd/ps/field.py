@@ -13,7 +13,11 @@ depends on:
 * ``str(access)`` is the bracket form ``x[0,0]`` (with the field's LaTeX name,
   e.g. ``\\hat{x}[0,0]`` for adjoint fields);
 * spatial coordinate 0 is the first (slowest, C-layout) array axis;
-* fields are compared by value (name, dtype, shape, strides).
+* vector fields come in pystencils' two memory layouts: ``'numpy'``/``'zyxf'``
+  (AoS, components fastest) and ``'fzyx'``/``'soa'`` (SoA, one C-ordered
+  spatial array per component, components slowest); for scalar fields both
+  are the same memory (pystencils ``layout_string_to_tuple`` [ext]);
+* fields are compared by value (name, dtype, shape, strides, memory layout).
 """
 import re
 from enum import Enum
@@ -119,6 +123,18 @@ class FieldStrideSymbol(sp.Symbol):
         return super()._hashable_content() + (self.field_name, self.coordinate)
 
 
+def _soa_strides(shape, index_dimensions):
+    """Element strides of an ``fzyx`` (SoA) field: C order over the spatial axes, the component axes
+    slowest (each component a whole spatial array)."""
+    spatial = len(shape) - index_dimensions
+    sp_strides = _c_strides(shape[:spatial])
+    vol = 1
+    for n in shape[:spatial]:
+        vol = vol * n
+    idx_strides = tuple(s * vol for s in _c_strides(shape[spatial:]))
+    return tuple(sp_strides) + idx_strides
+
+
 def _c_strides(shape):
     strides = []
     acc = 1
@@ -141,6 +157,7 @@ class Field:
         self.strides = tuple(strides)
         self.latex_name = latex_name
         self._index_dimensions = None
+        self._soa = False
 
     # -- construction ---------------------------------------------------------------------------
     @staticmethod
@@ -148,17 +165,18 @@ class Field:
                           strides=None, field_type=FieldType.GENERIC):
         shape = tuple(int(s) for s in shape)
         spatial = len(shape) - index_dimensions
-        _check_layout(layout)
+        soa = _check_layout(layout) == 'fzyx' and index_dimensions > 0
         if strides is None:
-            strides = _c_strides(shape)
+            strides = _soa_strides(shape, index_dimensions) if soa else _c_strides(shape)
         f = Field(field_name, field_type, dtype, tuple(range(spatial)), shape, strides)
         f._index_dimensions = index_dimensions
+        f._soa = soa
         return f
 
     @staticmethod
     def create_generic(field_name, spatial_dimensions, dtype=np.float64, index_dimensions=0,
                        layout='numpy', index_shape=None, field_type=FieldType.GENERIC):
-        _check_layout(layout)
+        soa = _check_layout(layout) == 'fzyx'
         if index_shape is not None:
             index_dimensions = len(index_shape)
         total = spatial_dimensions + index_dimensions
@@ -170,6 +188,7 @@ class Field:
         strides = [FieldStrideSymbol(field_name, i) for i in range(total)]
         f = Field(field_name, field_type, dtype, tuple(range(spatial_dimensions)), shape, strides)
         f._index_dimensions = index_dimensions
+        f._soa = soa and index_dimensions > 0
         return f
 
     @staticmethod
@@ -183,6 +202,9 @@ class Field:
             dtype = array.dtype
         f = Field(field_name, field_type, dtype, tuple(range(len(shape) - index_dimensions)), shape, strides)
         f._index_dimensions = index_dimensions
+        # components slowest in memory: an fzyx (SoA) array
+        f._soa = index_dimensions > 0 and tuple(strides) == _soa_strides(shape, index_dimensions) and \
+            tuple(strides) != _c_strides(shape)
         return f
 
     # -- properties -----------------------------------------------------------------------------
@@ -197,6 +219,33 @@ class Field:
     @property
     def layout(self):
         return self._layout
+
+    @property
+    def is_soa(self):
+        """A vector field in ``fzyx`` layout (components slowest in memory)."""
+        return bool(self._soa) and self.index_dimensions > 0
+
+    @property
+    def memory_layout(self):
+        """``'fzyx'`` for SoA vector fields, ``'numpy'`` otherwise."""
+        return 'fzyx' if self.is_soa else 'numpy'
+
+    def component_field(self, idx):
+        """The scalar field holding component ``idx`` of an fzyx (SoA) field: the same spatial shape, C
+        strides, named ``<name>__c<i>[_<j>...]`` (the kernels bind it to the component's sub-array)."""
+        if not self.is_soa:
+            raise ValueError(f"'{self.name}' is not an fzyx vector field")
+        idx = tuple(int(i) for i in idx)
+        name = f"{self.name}__c{'_'.join(str(i) for i in idx)}"
+        sshape = tuple(self.spatial_shape)
+        if self.has_fixed_shape:
+            strides = _c_strides(tuple(int(n) for n in sshape))
+        else:
+            strides = tuple(FieldStrideSymbol(name, d) for d in range(len(sshape)))
+        f = Field(name, self.field_type, self.dtype, tuple(range(len(sshape))), sshape, strides)
+        f._index_dimensions = 0
+        f.soa_parent = (self, idx)
+        return f
 
     @property
     def ndim(self):
@@ -271,7 +320,7 @@ class Field:
 
     # -- identity -------------------------------------------------------------------------------
     def _hashable_contents(self):
-        return (self._field_name, self._dtype, self.shape, self.strides, self.index_dimensions)
+        return (self._field_name, self._dtype, self.shape, self.strides, self.index_dimensions, self.is_soa)
 
     def __hash__(self):
         return hash(self._hashable_contents())
@@ -394,11 +443,18 @@ class Field:
 
 
 def _check_layout(layout):
+    """Normalised memory layout: ``'numpy'`` (C order, components fastest: also ``'c'``, ``'zyxf'``,
+    ``'aos'``) or ``'fzyx'`` (components slowest: also ``'soa'``). Fortran-ordered spatial axes
+    (``'f'``, ``'reverse_numpy'``) are not handled."""
     if layout is None:
-        return
-    if str(layout).lower() not in ('numpy', 'c', 'zyxf'):
-        raise NotImplementedError(f"layout '{layout}' is not supported; only C-contiguous ('numpy') fields "
-                                  "are handled by the MI355X execution layer")
+        return 'numpy'
+    lay = str(layout).lower()
+    if lay in ('numpy', 'c', 'zyxf', 'aos'):
+        return 'numpy'
+    if lay in ('fzyx', 'soa'):
+        return 'fzyx'
+    raise NotImplementedError(f"layout '{layout}' is not supported; C-ordered spatial axes with the "
+                              "components fastest ('numpy'/'zyxf') or slowest ('fzyx') are")
 
 
 _NAME_RE = re.compile(r'\s*([A-Za-z_]\w*)\s*(\(([^)]*)\))?\s*$')

@@ -56,12 +56,13 @@ def readme_op(shape=(20, 30), dtype='float32'):
     return ps.AssignmentCollection({z[0, 0]: x[0, 0] * sp.log(x[0, 0] * y[0, 0])})
 
 
-def vector_laplace_7pt(shape=None, dtype='float32', ncomp=3):
-    """Component-wise 3-D 7-point Laplacian of a vector field ``u(c)`` (index dimension, components
-    fastest in memory) — the vector-field row of SURVEY.md §8(f) (``_autodiff.py:125-152``)."""
+def vector_laplace_7pt(shape=None, dtype='float32', ncomp=3, layout='numpy'):
+    """Component-wise 3-D 7-point Laplacian of a vector field ``u(c)`` (index dimension; components
+    fastest in memory, or slowest with ``layout='fzyx'``) — the vector-field row of SURVEY.md §8(f)
+    (``_autodiff.py:125-152``)."""
     spec = f"u({ncomp}), out({ncomp}): {dtype}[{','.join(str(v) for v in shape)}]" if shape else \
         f"u({ncomp}), out({ncomp}): {dtype}[3d]"
-    u, out = ps.fields(spec)
+    u, out = ps.fields(spec, layout=layout)
     nb = [(1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)]
     return ps.AssignmentCollection({out.center(c): sp.Add(*[u[o](c) for o in nb]) - 6 * u.center(c)
                                     for c in range(ncomp)})

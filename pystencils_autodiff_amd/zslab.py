@@ -195,6 +195,8 @@ class ZSlabOp:
         for k in self.kernels.values():
             if k.ir.ndim != 3 and k.ir.ndim != 2:
                 raise ValueError('z-slab decomposition needs 2-D or 3-D fields')
+            if any(f.is_soa for f in k.ir.fields):
+                raise NotImplementedError('z-slab decomposition of fzyx (SoA) vector fields')
         self._span = {} if z_offset is None or global_z is None else None
         self._fixed_span = None if self._span is not None else (int(z_offset), int(global_z))
         self._bufs = {}

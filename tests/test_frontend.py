@@ -88,5 +88,7 @@ def test_direction_strings_roundtrip():
 
 
 def test_unsupported_layout_raises():
+    """Fortran-ordered spatial axes are not handled; 'fzyx' is (tests/test_fzyx.py)."""
     with pytest.raises(NotImplementedError):
-        ps.fields("a: double[3,4]", layout='fzyx')
+        ps.fields("a: double[3,4]", layout='reverse_numpy')
+    assert ps.fields("a: double[3,4]", layout='fzyx').strides == (4, 1)
