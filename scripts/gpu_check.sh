@@ -23,7 +23,7 @@ if [[ "$STEPS" == *smoke* || "$STEPS" == all ]]; then
   tail -3 "$OUT/smoke.log"; stop_if_fatal $rc smoke
 fi
 if [[ "$STEPS" == *tests* || "$STEPS" == all ]]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1; rc=$?
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
   tail -15 "$OUT/pytest_gpu.log"; stop_if_fatal $rc pytest_gpu
 fi
 if [[ "$STEPS" == *bench* || "$STEPS" == all ]]; then
