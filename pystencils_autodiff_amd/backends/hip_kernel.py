@@ -45,6 +45,13 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             # tap pairs by inline-asm ds_read2_b32 (AR): 0.421 vs 0.459 ms at 768³, 0.062 vs 0.067 ms per
             # 8-GPU slab (profiles/r01_tune_27pt_ar.log) — the compiler's adjacent-x merges cost 26 v_mov
             cfg.update(CX=2, WX=2, NR=4, ZSUM=True, PK=True, AR=True, ZMIN=16, ZMAX=32, BLK=2048)
+            half = dict(CX=4, WX=1, NR=2, WS=True, D=3, ZMIN=24, ZMAX=24)
+            if ws_geometry(ir, MarchConfig(VE=ve, **{**cfg, **half})):
+                # fp16 storage: LDS-DMA loader wave into a half-precision ring, lanes own x-adjacent quads,
+                # taps converted in registers (emit_zsum -> _emit_zsum_half), 256×8 tiles, 24-plane chunks:
+                # 768³ 0.370-0.392 ms vs 0.431-0.448 ms for the register-prefetch AR form in the same
+                # process; 96×768² slab 0.048-0.055 vs 0.059-0.069 ms (profiles/r02_tune_27pt_half*.log)
+                cfg.update(half)
         else:
             cfg.update(CX=2, NR=4)                             # box stencil: full ring, LDS/VALU bound
     elif ir.ndim == 3 and zsum_ok:
@@ -79,7 +86,7 @@ def default_march_config(ir, ve, shape=None, tuning=None):
     for k, v in over.items():
         if k in ('CX', 'WX', 'NR', 'PD', 'WAVES', 'LDS_PAD', 'ZCT', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'DMA_AUX'):
             cfg[k] = int(v)
-        elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'LAZY', 'ZSUM', 'PK', 'ZU', 'PX', 'FASTLOAD', 'WS', 'AR', 'WSD', 'DST', 'DB', 'IL', 'ROWS', 'STSW'):
+        elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'ZSUM', 'PK', 'WS', 'AR'):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
         elif k == 'VIEW2D':
             cfg[k] = str(v)
@@ -93,7 +100,10 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             while cfg['CX'] > 1 and 64 * cfg['CX'] * cfg['WX'] // 2 >= X:
                 cfg['CX'] //= 2
             tx = 64 * cfg['CX'] * cfg['WX']
-            if cfg.get('WS') and cfg['CX'] > 1 and -(-X // (tx // 2)) * (tx // 2) < -(-X // tx) * tx:
+            ws0 = ws_geometry(ir, MarchConfig(VE=ve, **cfg)) if cfg.get('WS') else None
+            quads = ws0 is not None and ws0['kind'] == 'h'       # the half ring needs lanes owning quads
+            if cfg.get('WS') and cfg['CX'] > 1 and -(-X // (tx // 2)) * (tx // 2) < -(-X // tx) * tx and \
+                    (not quads or (cfg['CX'] // 2) % 4 == 0):
                 # WS tiles: half width when it pads x less (384³ 7-point: 0.116 → 0.081 ms with 48-plane
                 # chunks, profiles/r01_tune_odd_sizes.log)
                 cfg['CX'] //= 2
@@ -500,7 +510,7 @@ class HipStencilKernel:
             # planes beyond the loader's 32-bit buffer offsets: register-prefetch form of the same schedule
             cfg = MarchConfig(**{**cfg.__dict__, 'WS': False})
         xlo, xhi = ir.iteration_bounds(shape)[-1]
-        if x_border and cfg.ZSUM and not cfg.PX and (xlo > 0 or xhi < shape[-1]) and \
+        if x_border and cfg.ZSUM and (xlo > 0 or xhi < shape[-1]) and \
                 not (ir.ndim == 2 and cfg.VIEW2D == 'zy'):
             cfg = MarchConfig(**{**cfg.__dict__, 'XB': True})
         variant = ('march', cfg)

@@ -333,19 +333,8 @@ def _zsum_cases():
 @pytest.mark.parametrize('params', [dict(ZSUM=True), dict(ZSUM=True, CX=1, NR=3, ZC=5),
                                     dict(ZSUM=True, CX=4, NR=8, NT_STORE=True), dict(ZSUM=True, WX=2, CX=2, NR=2),
                                     dict(ZSUM=True, PK=True, CX=2, NR=3, ZC=7),
-                                    dict(ZSUM=True, ZU=True, CX=2, NR=2, ZC=5),
-                                    dict(ZSUM=True, PK=True, ZU=True, WX=2, CX=4, NR=2, ZC=4),
                                     dict(ZSUM=True, PK=True, AR=True, CX=2, NR=3, ZC=7),
                                     dict(ZSUM=True, PK=True, AR=True, WX=2, CX=4, NR=2, ZC=4),
-                                    dict(ZSUM=True, PK=True, AR=True, DST=True, CX=2, NR=3, ZC=7),
-                                    dict(ZSUM=True, WS=False, DST=True, CX=1, NR=3, ZC=5),
-                                    dict(ZSUM=True, WS=False, DB=True, PK=True, AR=True, CX=2, WX=2, NR=2, ZC=6),
-                                    dict(ZSUM=True, WS=False, DB=True, DST=True, CX=1, NR=3, ZC=5),
-                                    dict(ZSUM=True, IL=True, PK=True, AR=True, CX=2, NR=3, ZC=7),
-                                    dict(ZSUM=True, WS=False, IL=True, CX=1, NR=2, ZC=5),
-                                    dict(ZSUM=True, PK=True, AR=True, ROWS=True, CX=2, NR=3, ZC=7),
-                                    dict(ZSUM=True, PK=True, AR=True, ROWS=True, WX=2, CX=2, NR=4, ZC=5, PD=2),
-                                    dict(ZSUM=True, PK=True, AR=True, STSW=True, CX=2, NR=3, ZC=7),
                                     dict(ZSUM=True, WS=False, NW=1, CX=2, NR=3, ZC=5),
                                     dict(ZSUM=True, WS=False, NW=2, WX=2, PK=True, AR=True, CX=2, NR=2, ZC=6)])
 @pytest.mark.parametrize('case', _zsum_cases(), ids=lambda c: c[0])
@@ -377,13 +366,13 @@ def test_zsum_schedule_vs_oracle(params, case, bh):
             assert_close_rel(t.cpu().numpy(), ref[n], 1e-3 if is16 else 1e-6, f'{name} {which} {n}')
 
 
-@pytest.mark.parametrize('params', [dict(ZSUM=True, CX=1, NR=2, ZC=4), dict(ZSUM=True, CX=2, NR=2, PK=True, PX=True),
+@pytest.mark.parametrize('params', [dict(ZSUM=True, CX=1, NR=2, ZC=4), dict(ZSUM=True, CX=2, NR=2, PK=True),
                                     dict(ZSUM=True, CX=2, WX=2, NR=4, PK=True, AR=True),
-                                    dict(ZSUM=True, CX=2, WX=2, NR=1, PK=True, PX=True, ZC=3),
-                                    dict(ZSUM=True, CX=2, NR=2, FASTLOAD=False), dict(ZSUM=False, CX=1, NR=2)])
+                                    dict(ZSUM=True, CX=2, WX=2, NR=1, PK=True, ZC=3),
+                                    dict(ZSUM=False, CX=1, NR=2)])
 @pytest.mark.parametrize('case', _zsum_cases(), ids=lambda c: c[0])
 def test_interior_tiles_vs_oracle(params, case):
-    """Shapes with interior tiles (unguarded plane loads) AND edge tiles, odd extents in y."""
+    """Shapes with interior tiles AND edge tiles, odd extents in y."""
     from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
     name, builder = case
     op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
@@ -542,8 +531,10 @@ def _ws_cases():
                                     dict(ZSUM=True, WS=True, PK=True, CX=2, NR=3, ZC=7),
                                     dict(ZSUM=True, WS=True, D=3, CX=2, NR=8, ZC=64),
                                     dict(ZSUM=True, WS=True, PK=True, AR=True, CX=2, WX=2, NR=4, ZC=5),
-                                    dict(ZSUM=True, WS=True, WSD=True, PK=True, AR=True, CX=2, WX=2, NR=4, D=3),
-                                    dict(ZSUM=True, WS=True, WSD=True, D=2, CX=1, NR=3, ZC=5)])
+                                    dict(ZSUM=True, WS=True, CX=4, NR=2, D=2, ZC=5),
+                                    dict(ZSUM=True, WS=True, CX=8, NR=1, D=3, ZC=4),
+                                    dict(ZSUM=True, WS=True, CX=4, WX=2, NR=3, D=4),
+                                    dict(ZSUM=True, WS=True, CX=4, NR=3, D=1)])
 @pytest.mark.parametrize('shape', [(12, 35, 72), (7, 29, 520), (4, 5, 8), (9, 3, 264)])
 @pytest.mark.parametrize('case', _ws_cases(), ids=lambda c: c[0])
 def test_ws_loader_schedule_vs_oracle(params, shape, case):
@@ -568,7 +559,8 @@ def test_ws_loader_schedule_vs_oracle(params, shape, case):
         torch.cuda.synchronize()
         cfg = k.last_variant[1]
         assert k.last_variant[0] == 'march' and cfg.ZSUM
-        if not (params.get('PK') and dt == np.float64) and shape[-1] % (16 // np.dtype(dt).itemsize) == 0:
+        if not (params.get('PK') and dt == np.float64) and shape[-1] % (16 // np.dtype(dt).itemsize) == 0 and \
+                (dt != np.float16 or cfg.CX % 4 == 0):
             assert ws_geometry(k.ir, cfg) is not None, cfg
         for n, t in outs.items():
             assert_close_rel(t.cpu().numpy(), ref[n], TOL[dt], f'{name} {which} {n} {params}')

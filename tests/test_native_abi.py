@@ -94,20 +94,18 @@ def test_zsum_eligibility():
     assert plan[0]['rest'] == 0                                   # every centre-plane tap is a packed FMA too
 
 
-def test_zsum_packed_and_unrolled_variants_compile():
+def test_zsum_packed_variants_compile():
     op27 = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
     k = op27.forward_ast_gpu.compile()
     default = k.primary_variant()[1]
-    assert default.ZSUM and default.PK and default.AR and default.WX == 2   # measured default for box stencils
+    # measured default for fp16 box stencils: the half-precision ring (lanes own x-adjacent quads)
+    from pystencils_autodiff_amd.backends.hip_emitter import ws_geometry
+    assert default.ZSUM and default.WS and default.CX == 4 and ws_geometry(k.ir, default)['kind'] == 'h'
     for cfg in (MarchConfig(VE=8, CX=2, NR=4, ZSUM=True, PK=True),
-                MarchConfig(VE=8, CX=2, NR=4, ZSUM=True, PK=True, PX=True),
-                MarchConfig(VE=8, CX=2, NR=4, ZSUM=True, FASTLOAD=False),
-                MarchConfig(VE=8, CX=2, NR=4, ZSUM=True, PK=True, ZU=True),
                 MarchConfig(VE=8, CX=2, WX=2, NR=4, ZSUM=True, PK=True, AR=True),
                 MarchConfig(VE=8, CX=3, NR=2, ZSUM=True, PK=True)):       # odd CX: scalar fallback
         src, name = k.source(('march', cfg))
         assert ('f32x2 a0_' in src) == (cfg.PK and cfg.CX % 2 == 0)
-        assert ('p0 += 3' in src) == cfg.ZU                              # 2*RZ+1 phases, renamed accumulators
         assert ('ds_read2_b32 %0' in src) == (cfg.AR and cfg.CX % 2 == 0)   # paired taps by inline asm
         code = rt.compile_hip(src)
         assert _is_amdgpu_elf(code) and name.encode() in code
@@ -118,7 +116,8 @@ def test_zsum_packed_and_unrolled_variants_compile():
 
 def test_ws_loader_variants_compile():
     """Warp-specialised zsum (LDS-DMA loader wave): the measured default for star stencils in fp32 /
-    fp64, counted vmcnt waits within the 6-bit counter, compiles for gfx950; not used for fp16 storage."""
+    fp64, counted vmcnt waits within the 6-bit counter, compiles for gfx950; fp16 storage reads the raw
+    planes from a half-precision ring."""
     from pystencils_autodiff_amd.backends.hip_emitter import ws_geometry
     op = pa.AutoDiffOp(W.diffusion_7pt(), boundary_handling='zeros')
     k = op.forward_ast_gpu.compile()
@@ -136,14 +135,15 @@ def test_ws_loader_variants_compile():
         assert _is_amdgpu_elf(code) and name.encode() in code
     two = pa.AutoDiffOp(W.asym_7pt(), boundary_handling='zeros').backward_ast_gpu
     assert ws_geometry(two.ir, MarchConfig(VE=4, CX=4, NR=8, ZSUM=True, WS=True, D=4))['D'] <= 4
-    op27 = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')       # fp16 storage: converting loader
+    op27 = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')       # fp16 storage: half-precision ring
     k27 = op27.forward_ast_gpu.compile()
-    c27 = MarchConfig(VE=8, CX=2, WX=2, NR=4, ZSUM=True, WS=True, PK=True)
+    c27 = MarchConfig(VE=8, CX=4, WX=1, NR=4, ZSUM=True, WS=True, D=3)
     ws = ws_geometry(k27.ir, c27)
-    assert ws['kind'] == 'reg' and ws['NS'] == 2
+    assert ws['kind'] == 'h' and ws['NS'] == 4 and ws['lds_type'] == '_Float16' and ws['lds_bytes'] <= 160 * 1024
     src, name = k27.source(('march', c27))
-    assert '__builtin_amdgcn_raw_buffer_load_b128' in src and 'if (wave == 4)' in src
+    assert '__builtin_amdgcn_raw_ptr_buffer_load_lds' in src and 'if (wave == 4)' in src and 'f16x4' in src
     assert _is_amdgpu_elf(rt.compile_hip(src))
+    assert ws_geometry(k27.ir, MarchConfig(VE=8, CX=2, NR=4, ZSUM=True, WS=True)) is None    # lanes own quads
     assert ws_geometry(k27.ir, MarchConfig(VE=1, CX=2, NR=4, ZSUM=True, WS=True)) is None   # unaligned
 
 
