@@ -1,0 +1,88 @@
+"""TEST INFRASTRUCTURE ONLY (never imported by the package): an independent restatement of the lattice
+Boltzmann time step the ``AutoDiffLatticeBoltzmannStep`` kernels compute, written with array rolls
+instead of the symbolic pipeline.
+
+Reference path: ``/root/reference/src/pystencils_autodiff/lbm/_autodiff_lbstep.py:189-247,372-398`` runs
+lbmpy's [ext, absent] stream-pull-collide SRT kernel with periodic ghost-layer sync and buffer swaps;
+the equations (lbmpy's published SRT method, second-order equilibrium) are restated here:
+
+    f_i(x) = src_i(x − c_i)   (periodic)        ρ = Σ f_i,   u = Σ c_i f_i (/ρ if compressible)
+    feq_i = w_i ρ (1 + 3 c·u + 4.5 (c·u)² − 1.5 u²)   or, incompressible, w_i (ρ + 3 c·u + 4.5 (c·u)² − 1.5 u²)
+    dst_i = f_i + ω (feq_i − f_i)
+
+``xp`` is numpy or torch (torch: an autograd-able restatement whose gradient, by torch's reverse mode, is
+the adjoint oracle for the step's hand-derived transposed kernels). Pdf arrays are ``[*spatial, q]``.
+Parity with lbmpy itself is unpinned (lbmpy is not importable here)."""
+from fractions import Fraction
+
+D2Q9 = ([(0, 0), (0, 1), (0, -1), (-1, 0), (1, 0), (-1, 1), (1, 1), (-1, -1), (1, -1)],
+        [Fraction(4, 9)] + [Fraction(1, 9)] * 4 + [Fraction(1, 36)] * 4)
+D3Q19 = ([(0, 0, 0), (0, 1, 0), (0, -1, 0), (-1, 0, 0), (1, 0, 0), (0, 0, 1), (0, 0, -1), (-1, 1, 0), (1, 1, 0),
+          (-1, -1, 0), (1, -1, 0), (0, 1, 1), (0, -1, 1), (-1, 0, 1), (1, 0, 1), (0, 1, -1), (0, -1, -1),
+          (-1, 0, -1), (1, 0, -1)],
+         [Fraction(1, 3)] + [Fraction(1, 18)] * 6 + [Fraction(1, 36)] * 12)
+SETS = {'D2Q9': D2Q9, 'D3Q19': D3Q19}
+
+
+def _roll(xp, a, shift, axis):
+    if xp.__name__ == 'torch':
+        return xp.roll(a, shifts=shift, dims=axis)
+    return xp.roll(a, shift, axis=axis)
+
+
+def stream(f, stencil, xp):
+    """Pull streaming with periodic wrap: out_i(x) = f_i(x − c_i)."""
+    dirs, _ = SETS[stencil]
+    comps = []
+    for i, c in enumerate(dirs):
+        g = f[..., i]
+        for ax, s in enumerate(c):
+            if s:
+                g = _roll(xp, g, s, ax)
+        comps.append(g)
+    return xp.stack(comps, -1) if xp.__name__ != 'torch' else xp.stack(comps, dim=-1)
+
+
+def collide(f, omega, stencil, compressible, xp):
+    dirs, w = SETS[stencil]
+    D = len(dirs[0])
+    rho = f.sum(-1)
+    u = []
+    for a in range(D):
+        m = sum(c[a] * f[..., i] for i, c in enumerate(dirs) if c[a])
+        u.append(m / rho if compressible else m)
+    usq = sum(ua * ua for ua in u)
+    out = []
+    for i, c in enumerate(dirs):
+        cu = sum(ca * ua for ca, ua in zip(c, u) if ca)
+        poly = 3 * cu + 4.5 * cu * cu - 1.5 * usq
+        feq = float(w[i]) * rho * (1 + poly) if compressible else float(w[i]) * (rho + poly)
+        out.append(f[..., i] + omega * (feq - f[..., i]))
+    return xp.stack(out, -1) if xp.__name__ != 'torch' else xp.stack(out, dim=-1)
+
+
+def step(f, omega, stencil='D2Q9', compressible=False, xp=None):
+    """One stream-pull-collide time step on a periodic domain (``f``: ``[*spatial, q]``)."""
+    if xp is None:
+        import numpy as xp
+    return collide(stream(f, stencil, xp), omega, stencil, compressible, xp)
+
+
+def run(f, omega, steps, stencil='D2Q9', compressible=False, xp=None):
+    for _ in range(steps):
+        f = step(f, omega, stencil, compressible, xp)
+    return f
+
+
+def equilibrium(rho, u, stencil='D2Q9', compressible=False, xp=None):
+    """feq(ρ, u) as ``[*spatial, q]`` (``u``: ``[*spatial, d]``)."""
+    if xp is None:
+        import numpy as xp
+    dirs, w = SETS[stencil]
+    usq = sum(u[..., a] * u[..., a] for a in range(len(dirs[0])))
+    out = []
+    for i, c in enumerate(dirs):
+        cu = sum(ca * u[..., a] for a, ca in enumerate(c) if ca)
+        poly = 3 * cu + 4.5 * cu * cu - 1.5 * usq
+        out.append(float(w[i]) * rho * (1 + poly) if compressible else float(w[i]) * (rho + poly))
+    return xp.stack(out, -1) if xp.__name__ != 'torch' else xp.stack(out, dim=-1)

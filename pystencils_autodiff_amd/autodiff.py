@@ -181,8 +181,10 @@ def transposed_backward(forward_assignments, diff_fields_prefix='diff', constant
     if not has_exclusive_writes(backward):
         raise AssertionError("Backward assignments don't have exclusive writes. "
                              "You should consider using 'transposed-forward' mode for resolving those conflicts")
-    out_fields = list(write_fields)
-    in_fields = list(read_fields)
+    # the reference lists the fields in set order (``_autodiff.py:430-431``: hash-seed dependent across
+    # processes); sorted by ``str`` here, the TF-MAD mode's order, so positional arguments are stable
+    out_fields = sorted(write_fields, key=str)
+    in_fields = sorted(read_fields, key=str)
     field_map = {**adj_read, **adj_write}
     info = dict(forward_read_accesses=reads, forward_write_accesses=writes,
                 forward_input_fields=in_fields, forward_output_fields=out_fields,

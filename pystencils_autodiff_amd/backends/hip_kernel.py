@@ -157,6 +157,13 @@ class HipStencilKernel:
             return 'generic'
         if ir.pointwise:
             return 'generic' if ir.has_index_dims else 'pointwise'
+        taps = {}
+        for r in ir.reads:
+            taps.setdefault(r.field, set()).add(r.offsets)
+        if ir.stencil_fields and not ir.has_index_dims and all(len(taps.get(f, ())) == 1 for f in ir.stencil_fields):
+            # every stencil field read at ONE offset (pull-streaming lattice Boltzmann: component i at -c_i):
+            # staging planes in LDS buys no reuse, the one-thread-per-cell schedule streams each component
+            return 'generic'
         if ir.ndim in (2, 3) and all(all(o == 0 for o in s[1]) for s in ir.stores) and \
                 len({f.dtype for f in ir.fields}) == 1:
             if ir.has_index_dims:

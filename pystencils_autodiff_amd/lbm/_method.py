@@ -1,0 +1,137 @@
+"""Lattice Boltzmann update rules for ``AutoDiffLatticeBoltzmannStep`` (``lbm/_autodiff_lbstep.py``).
+
+The reference builds its update rule with lbmpy [ext] (``lbmpy.creationfunctions.create_lb_update_rule``,
+absent here: an un-vendored dependency of ``/root/reference/src/pystencils_autodiff/lbm/_autodiff_lbstep.py:8-10``).
+This module restates the part of lbmpy the step consumes, as ``AssignmentCollection``s of this package's
+``ps`` front-end: lbmpy's D2Q9 / D3Q19 / D3Q27 velocity sets (same direction order and weights), the
+single-relaxation-time (SRT/BGK) method with the second-order equilibrium (compressible, or lbmpy's
+incompressible form with reference density 1), and the ``stream_pull_collide`` kernel type:
+
+    f_i(x) = src_i(x − c_i)                                  (pull streaming)
+    ρ = Σ_i f_i,   u = Σ_i c_i f_i / ρ   (incompressible: / 1)
+    feq_i = w_i ρ (1 + 3 c_i·u + 9/2 (c_i·u)² − 3/2 u²)     (incompressible: w_i (ρ + 3 c_i·u + …))
+    dst_i(x) = f_i + ω (feq_i − f_i)
+
+plus the macroscopic getter (ρ, u from the pdfs) and setter (pdfs = feq(ρ, u)) the step's
+``create_macroscopic_*_op`` wrap. Parity with lbmpy is unpinned (lbmpy is absent); the oracle
+(``oracle/lbm.py``) restates the same equations independently with array rolls.
+"""
+import sympy as sp
+
+from .. import ps
+
+__all__ = ['LBStencil', 'create_lb_update_rule', 'macroscopic_getter', 'equilibrium_setter']
+
+
+class LBStencil:
+    """A DdQq velocity set in lbmpy's direction order (``lbmpy.stencils.LBStencil`` [ext]): ``directions``
+    (tuples over the spatial axes, axis 0 first) and the lattice weights."""
+
+    _SETS = {
+        'D2Q9': ([(0, 0), (0, 1), (0, -1), (-1, 0), (1, 0), (-1, 1), (1, 1), (-1, -1), (1, -1)],
+                 [sp.Rational(4, 9)] + [sp.Rational(1, 9)] * 4 + [sp.Rational(1, 36)] * 4),
+        'D3Q19': ([(0, 0, 0), (0, 1, 0), (0, -1, 0), (-1, 0, 0), (1, 0, 0), (0, 0, 1), (0, 0, -1),
+                   (-1, 1, 0), (1, 1, 0), (-1, -1, 0), (1, -1, 0), (0, 1, 1), (0, -1, 1), (-1, 0, 1),
+                   (1, 0, 1), (0, 1, -1), (0, -1, -1), (-1, 0, -1), (1, 0, -1)],
+                  [sp.Rational(1, 3)] + [sp.Rational(1, 18)] * 6 + [sp.Rational(1, 36)] * 12),
+    }
+
+    def __init__(self, name):
+        name = str(name).upper().replace('STENCIL.', '')
+        if name == 'D3Q27':
+            dirs = [(0, 0, 0), (0, 1, 0), (0, -1, 0), (-1, 0, 0), (1, 0, 0), (0, 0, 1), (0, 0, -1),
+                    (-1, 1, 0), (1, 1, 0), (-1, -1, 0), (1, -1, 0), (0, 1, 1), (0, -1, 1), (-1, 0, 1),
+                    (1, 0, 1), (0, 1, -1), (0, -1, -1), (-1, 0, -1), (1, 0, -1),
+                    (1, 1, 1), (-1, 1, 1), (1, -1, 1), (-1, -1, 1), (1, 1, -1), (-1, 1, -1), (1, -1, -1),
+                    (-1, -1, -1)]
+            w = {0: sp.Rational(8, 27), 1: sp.Rational(2, 27), 2: sp.Rational(1, 54), 3: sp.Rational(1, 216)}
+            weights = [w[sum(abs(c) for c in d)] for d in dirs]
+        elif name in self._SETS:
+            dirs, weights = self._SETS[name]
+        else:
+            raise ValueError(f"unknown stencil '{name}' (D2Q9, D3Q19, D3Q27)")
+        self.name = name
+        self.directions = [tuple(d) for d in dirs]
+        self.weights = list(weights)
+        self.D = len(self.directions[0])
+        self.Q = len(self.directions)
+        assert sum(self.weights) == 1
+
+    def __len__(self):
+        return self.Q
+
+    def inverse_direction_index(self, i):
+        return self.directions.index(tuple(-c for c in self.directions[i]))
+
+
+def _moments(stencil, f, compressible):
+    rho = sp.Symbol('rho')
+    us = sp.symbols(f'u_:{stencil.D}')
+    subs = [ps.Assignment(rho, sum(f))]
+    for a in range(stencil.D):
+        mom = sum(c[a] * fi for c, fi in zip(stencil.directions, f) if c[a])
+        subs.append(ps.Assignment(us[a], mom / rho if compressible else mom))
+    return rho, us, subs
+
+
+def _feq(stencil, i, rho, us, compressible):
+    c = stencil.directions[i]
+    cu = sum(ca * ua for ca, ua in zip(c, us) if ca)
+    usq = sum(ua ** 2 for ua in us)
+    poly = 3 * cu + sp.Rational(9, 2) * cu ** 2 - sp.Rational(3, 2) * usq
+    w = stencil.weights[i]
+    return w * rho * (1 + poly) if compressible else w * (rho + poly)
+
+
+def create_lb_update_rule(stencil='D2Q9', relaxation_rate=None, compressible=False, src_field=None, dst_field=None,
+                          data_type='float64', layout='fzyx', kernel_type='stream_pull_collide'):
+    """SRT (BGK) ``stream_pull_collide`` update rule (lbmpy ``create_lb_update_rule(stencil=…, method='srt',
+    relaxation_rate=…, compressible=…, kernel_type='stream_pull_collide')`` [ext]). ``relaxation_rate`` =
+    ω: a number, or a sympy symbol left as a kernel parameter (default: the symbol ``omega``). Fields:
+    ``src(q)``/``dst(q)`` vector fields in ``layout`` (``'fzyx'``: components slowest, lbmpy's default)
+    unless given."""
+    if kernel_type != 'stream_pull_collide':
+        raise NotImplementedError("only kernel_type='stream_pull_collide' is restated")
+    st = stencil if isinstance(stencil, LBStencil) else LBStencil(stencil)
+    if src_field is None or dst_field is None:
+        src_field, dst_field = ps.fields(f"src({st.Q}), dst({st.Q}): {data_type}[{st.D}D]", layout=layout)
+    omega = sp.Symbol('omega') if relaxation_rate is None else sp.sympify(relaxation_rate)
+    f = [src_field[tuple(-c for c in st.directions[i])](i) for i in range(st.Q)]
+    rho, us, subs = _moments(st, f, compressible)
+    main = [ps.Assignment(dst_field.center(i), f[i] + omega * (_feq(st, i, rho, us, compressible) - f[i]))
+            for i in range(st.Q)]
+    ac = ps.AssignmentCollection(main, subs)
+    ac.stencil = st
+    ac.compressible = compressible
+    ac.relaxation_rate = omega
+    return ac
+
+
+def macroscopic_getter(stencil, pdf_field, density_field, velocity_field, compressible=False):
+    """ρ = Σ f_i, u = Σ c_i f_i (/ρ): lbmpy's ``macroscopic_values_getter`` [ext] for the SRT method."""
+    st = stencil if isinstance(stencil, LBStencil) else LBStencil(stencil)
+    f = [pdf_field.center(i) for i in range(st.Q)]
+    rho, us, subs = _moments(st, f, compressible)
+    main = [ps.Assignment(density_field.center, rho)] + \
+        [ps.Assignment(velocity_field.center(a), us[a]) for a in range(st.D)]
+    return ps.AssignmentCollection(main, subs)
+
+
+def equilibrium_setter(stencil, pdf_field, density_field, velocity_field, compressible=False):
+    """pdfs = feq(ρ, u): lbmpy's ``macroscopic_values_setter`` [ext] (equilibrium initialisation)."""
+    st = stencil if isinstance(stencil, LBStencil) else LBStencil(stencil)
+    rho = density_field.center
+    us = [velocity_field.center(a) for a in range(st.D)]
+    return ps.AssignmentCollection([ps.Assignment(pdf_field.center(i), _feq(st, i, rho, us, compressible))
+                                    for i in range(st.Q)], [])
+
+
+def _check_directions():
+    for name in ('D2Q9', 'D3Q19', 'D3Q27'):
+        st = LBStencil(name)
+        assert len(set(st.directions)) == st.Q
+        for a in range(st.D):                      # isotropy: Σ w c_a c_b = δ_ab / 3
+            for b in range(st.D):
+                m = sum(w * c[a] * c[b] for w, c in zip(st.weights, st.directions))
+                assert m == (sp.Rational(1, 3) if a == b else 0), (name, a, b, m)
+    return True

@@ -154,6 +154,54 @@ def run_slab(name, builder, shape, dtype, full_cells, steps=20, warmup=3):
     sys.stdout.flush()
 
 
+def run_lbm(name, stencil, shape, dtype, T=10, reps=3, compressible=False):
+    """Lattice Boltzmann time-step op (lbm.AutoDiffLatticeBoltzmannStep.create_timestep_op): T forward steps
+    and the T adjoint steps, HIP events around Op.apply and backward. MLUPS = cells · T / time; algorithmic
+    bytes per cell and step: forward 2q·s (read src, write dst), adjoint 3q·s (read diffdst and the recorded
+    src, write diffsrc), s = element size; the ghost sync, state records and adjoint border fills are extra."""
+    import torch
+
+    from pystencils_autodiff_amd import lbm
+    rule = lbm.create_lb_update_rule(stencil, compressible=compressible, data_type=str(dtype).replace('torch.', ''))
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.5, target='gpu')
+    Op = step.create_timestep_op(T)
+    q = rule.stencil.Q
+    g = torch.Generator(device='cuda').manual_seed(0)
+    f0 = (torch.full(tuple(shape) + (q,), 1.0 / q, device='cuda', dtype=torch.float64) *
+          (1 + 0.01 * torch.rand(tuple(shape) + (q,), generator=g, device='cuda', dtype=torch.float64))).to(dtype)
+    x = f0.clone().requires_grad_(True)
+    gr = torch.rand(tuple(shape) + (q,), generator=g, device='cuda', dtype=dtype)
+    fw, bw = [], []
+    for i in range(reps + 1):
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record()
+        out = Op.apply(x)
+        e1.record()
+        out.backward(gr)
+        e2.record()
+        torch.cuda.synchronize()
+        x.grad = None
+        if i:
+            fw.append(e0.elapsed_time(e1))
+            bw.append(e1.elapsed_time(e2))
+    cells = 1
+    for n in shape:
+        cells *= n
+    es = torch.tensor([], dtype=dtype).element_size()
+    f_ms, b_ms = sorted(fw)[len(fw) // 2], sorted(bw)[len(bw) // 2]
+    res = {'config': name, 'shape': list(shape), 'dtype': str(dtype).replace('torch.', ''), 'time_steps': T,
+           'fwd_mlups': round(cells * T / (f_ms * 1e-3) / 1e6, 1), 'bwd_mlups': round(cells * T / (b_ms * 1e-3) / 1e6, 1),
+           'fwd_ms': round(f_ms, 4), 'bwd_ms': round(b_ms, 4),
+           'fwd_GBps': round(2 * q * es * cells * T / (f_ms * 1e-3) / 1e9, 1),
+           'bwd_GBps': round(3 * q * es * cells * T / (b_ms * 1e-3) / 1e9, 1)}
+    res['fwd_frac'] = round(res['fwd_GBps'] / PEAK, 4)
+    res['bwd_frac'] = round(res['bwd_GBps'] / PEAK, 4)
+    print(json.dumps(res))
+    sys.stdout.flush()
+    del x, out, gr, f0, Op
+    torch.cuda.empty_cache()
+
+
 def run_cpu(name, builder, shape, bh, nin, steps=2000):
     """BASELINE config 1 as stated: the op on the CPU backend (use_cuda=False, the C kernels), host
     wall time per forward + backward."""
@@ -210,6 +258,12 @@ def main():
         if only and name not in only:
             continue
         run_slab(name, b, shape, dt, cells)
+    lbms = [('lbm_d2q9_f32_2048^2', 'D2Q9', (2048, 2048), torch.float32),
+            ('lbm_d3q19_f32_192^3', 'D3Q19', (192, 192, 192), torch.float32)]
+    for name, stencil, shape, dt in lbms:
+        if only and name not in only:
+            continue
+        run_lbm(name, stencil, shape, dt)
 
 
 if __name__ == '__main__':

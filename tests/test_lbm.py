@@ -1,0 +1,172 @@
+"""Lattice Boltzmann time-step op (§8 f3; reference ``lbm/_autodiff_lbstep.py``): forward steps against an
+independent array-roll restatement (``oracle/lbm.py``), the adjoint steps against torch's reverse mode
+through that restatement, conservation at full sizes. Parity with lbmpy itself is unpinned (lbmpy absent):
+the oracle restates lbmpy's published SRT equations."""
+import numpy as np
+import pytest
+
+from oracle import lbm as OL
+from pystencils_autodiff_amd import lbm, ps
+
+
+def _init(stencil, shape, compressible, seed=0):
+    rng = np.random.default_rng(seed)
+    D = len(shape)
+    Q = {'D2Q9': 9, 'D3Q19': 19}[stencil]
+    rho = 1 + 0.05 * rng.standard_normal(shape)
+    u = 0.04 * rng.standard_normal(shape + (D,))
+    return OL.equilibrium(rho, u, stencil, compressible) + 0.01 * rng.standard_normal(shape + (Q,))
+
+
+def _oracle_grad(f0, omega, T, stencil, compressible, g, device='cpu'):
+    import torch
+    ft = torch.tensor(f0, requires_grad=True, device=device)
+    out = OL.run(ft, omega, T, stencil, compressible, xp=torch)
+    (gref,) = torch.autograd.grad(out, ft, torch.as_tensor(g, device=device))
+    return out.detach().cpu().numpy(), gref.cpu().numpy()
+
+
+CPU_CASES = [('D2Q9', (10, 7), False, 'fzyx'), ('D2Q9', (9, 12), True, 'numpy'), ('D3Q19', (6, 5, 4), False, 'fzyx')]
+
+
+@pytest.mark.parametrize('stencil,shape,compressible,layout', CPU_CASES)
+def test_lbm_steps_cpu_vs_oracle(stencil, shape, compressible, layout):
+    """T forward steps (periodic sync, pull-stream-collide, swap) and T adjoint steps on the C kernels."""
+    rule = lbm.create_lb_update_rule(stencil, compressible=compressible, layout=layout)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.4, target='cpu')
+    f0 = _init(stencil, shape, compressible)
+    T = 4
+    step.set_pdfs(f0)
+    step.run(T, record=True)
+    g = np.random.default_rng(1).standard_normal(f0.shape)
+    ref, gref = _oracle_grad(f0, 1.4, T, stencil, compressible, g)
+    assert np.abs(step.pdf_array - ref).max() <= 1e-13 * np.abs(ref).max()
+    step.set_adjoint_pdfs(g)
+    step.run_backward(T)
+    assert np.abs(step.adjoint_pdf_array - gref).max() <= 1e-12 * np.abs(gref).max()
+
+
+def test_lbm_timestep_op_cpu_autograd():
+    import torch
+    rule = lbm.create_lb_update_rule('D2Q9', compressible=True)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=(8, 6), relaxation_rate=1.1, target='cpu')
+    Op = step.create_timestep_op(3)
+    f0 = _init('D2Q9', (8, 6), True, seed=3)
+    x = torch.tensor(f0, requires_grad=True)
+    out = Op.apply(x)
+    g = torch.tensor(np.random.default_rng(4).standard_normal(f0.shape))
+    out.backward(g)
+    ref, gref = _oracle_grad(f0, 1.1, 3, 'D2Q9', True, g.numpy())
+    assert np.abs(out.detach().numpy() - ref).max() <= 1e-13
+    assert np.abs(x.grad.numpy() - gref).max() <= 1e-12 * np.abs(gref).max()
+    assert Op.num_time_steps == 3 and Op.lb_step is step
+
+
+def test_lbm_field_guessing_and_names():
+    rule = lbm.create_lb_update_rule('D2Q9')
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=(4, 4), relaxation_rate=1.0, target='cpu')
+    assert step.pdf_field.name == 'src' and step.temporary_field.name == 'dst'
+    assert step.backward_pdf_array_name == 'diffdst' and step._backward_tmp_array_name == 'diffsrc'
+    a, b, c = ps.fields("a(9), b(9), c(9): float64[2D]")
+    two_src = ps.AssignmentCollection([ps.Assignment(c.center(i), a.center(i) + b.center(i)) for i in range(9)])
+    with pytest.raises(lbm.PdfFieldNotDetectedException):
+        lbm.AutoDiffLatticeBoltzmannStep(two_src, domain_size=(4, 4), target='cpu')
+    step2 = lbm.AutoDiffLatticeBoltzmannStep(two_src, a, c, domain_size=(4, 4), target='cpu', constant_fields=[b])
+    assert step2.pdf_field == a
+    with pytest.raises(ValueError):
+        lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=(4, 4), target='cpu')     # omega needs a value
+
+
+def test_lbm_update_rule_lattice():
+    for name, q in (('D2Q9', 9), ('D3Q19', 19), ('D3Q27', 27)):
+        st = lbm.LBStencil(name)
+        assert st.Q == q and sum(st.weights) == 1
+        for i in range(q):
+            assert st.directions[st.inverse_direction_index(i)] == tuple(-c for c in st.directions[i])
+
+
+def test_lbm_macroscopic_ops_cpu():
+    import torch
+    rule = lbm.create_lb_update_rule('D2Q9', compressible=True)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=(6, 5), relaxation_rate=1.0, target='cpu')
+    setter = step.create_macroscopic_setter_op()
+    getter = step.create_macroscopic_getter_op()
+    rng = np.random.default_rng(2)
+    rho = torch.tensor(1 + 0.1 * rng.standard_normal((6, 5)))
+    vel = torch.tensor(0.05 * rng.standard_normal((6, 5, 2)))
+    (pdfs,) = setter.apply(rho, vel)
+    assert np.abs(pdfs.numpy() - OL.equilibrium(rho.numpy(), vel.numpy(), 'D2Q9', True)).max() < 1e-14
+    r2, v2 = getter.apply(pdfs)
+    assert np.abs(r2.numpy() - rho.numpy()).max() < 1e-13 and np.abs(v2.numpy() - vel.numpy()).max() < 1e-13
+
+
+# --------------------------------------------------------------------------------------------------------
+# GPU (HIP kernels)
+# --------------------------------------------------------------------------------------------------------
+GPU_CASES = [('D2Q9', (40, 33), False, 'fzyx', 'float64'), ('D2Q9', (37, 64), True, 'numpy', 'float64'),
+             ('D2Q9', (64, 48), True, 'fzyx', 'float32'), ('D3Q19', (20, 17, 12), False, 'fzyx', 'float64'),
+             ('D3Q19', (16, 12, 24), True, 'fzyx', 'float32')]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('stencil,shape,compressible,layout,dtype', GPU_CASES)
+def test_lbm_steps_gpu_vs_oracle(stencil, shape, compressible, layout, dtype):
+    import torch
+    rule = lbm.create_lb_update_rule(stencil, compressible=compressible, layout=layout, data_type=dtype)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.3, target='gpu')
+    f0 = _init(stencil, shape, compressible)
+    T = 5
+    tdt = getattr(torch, dtype)
+    step.set_pdfs(torch.tensor(f0, dtype=tdt, device='cuda'))
+    step.run(T, record=True)
+    g = np.random.default_rng(1).standard_normal(f0.shape)
+    ref, gref = _oracle_grad(f0, 1.3, T, stencil, compressible, g)
+    tol = 1e-12 if dtype == 'float64' else 1e-5
+    got = step.pdf_array.double().cpu().numpy()
+    assert np.abs(got - ref).max() <= tol * np.abs(ref).max()
+    step.set_adjoint_pdfs(torch.tensor(g, dtype=tdt, device='cuda'))
+    step.run_backward(T)
+    gg = step.adjoint_pdf_array.double().cpu().numpy()
+    assert np.abs(gg - gref).max() <= tol * 10 * np.abs(gref).max()
+    kf = step.autodiff_op.forward_ast_gpu.compile()
+    if layout == 'fzyx':
+        assert kf.last_variant[0] == 'generic'       # SoA components: one-thread-per-cell streaming schedule
+
+
+@pytest.mark.gpu
+def test_lbm_timestep_op_gpu_autograd():
+    import torch
+    rule = lbm.create_lb_update_rule('D2Q9', compressible=True, data_type='float64')
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=(48, 40), relaxation_rate=1.7, target='gpu')
+    Op = step.create_timestep_op(6)
+    f0 = _init('D2Q9', (48, 40), True, seed=5)
+    x = torch.tensor(f0, requires_grad=True, device='cuda')
+    out = Op.apply(x)
+    g = torch.tensor(np.random.default_rng(6).standard_normal(f0.shape), device='cuda')
+    out.backward(g)
+    ref, gref = _oracle_grad(f0, 1.7, 6, 'D2Q9', True, g.cpu().numpy(), device='cuda')
+    assert np.abs(out.detach().cpu().numpy() - ref).max() <= 1e-12
+    assert np.abs(x.grad.cpu().numpy() - gref).max() <= 1e-11 * np.abs(gref).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('stencil,shape', [('D2Q9', (2048, 1024)), ('D3Q19', (128, 96, 160))])
+def test_lbm_full_size_properties(stencil, shape):
+    """Full sizes: mass is conserved by the periodic steps (fp64 sum), and the adjoint of T steps equals
+    torch's reverse mode through the oracle run on the GPU (fp32 kernels vs fp64 oracle)."""
+    import torch
+    rule = lbm.create_lb_update_rule(stencil, compressible=False, data_type='float32')
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.5, target='gpu')
+    f0 = _init(stencil, shape, False, seed=9)
+    step.set_pdfs(torch.tensor(f0, dtype=torch.float32, device='cuda'))
+    m0 = step.pdf_array.double().sum().item()
+    T = 3
+    step.run(T, record=True)
+    m1 = step.pdf_array.double().sum().item()
+    assert abs(m1 - m0) <= 1e-6 * abs(m0)
+    g = np.random.default_rng(10).standard_normal(f0.shape)
+    _, gref = _oracle_grad(f0, 1.5, T, stencil, False, g, device='cuda')
+    step.set_adjoint_pdfs(torch.tensor(g, dtype=torch.float32, device='cuda'))
+    step.run_backward(T)
+    gg = step.adjoint_pdf_array.double().cpu().numpy()
+    assert np.abs(gg - gref).max() <= 1e-5 * np.abs(gref).max()
