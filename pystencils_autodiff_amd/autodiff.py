@@ -46,10 +46,13 @@ class AutoDiffBoundaryHandling(str, Enum):
     ``None``: interior cells only (a stencil-radius wide border is not written).
     ``'zeros'``: out-of-domain reads are 0, every cell is written, forward and backward.
     ``'valid'``: not implemented by the reference either (``_autodiff.py:246-247``).
+    ``'periodic'``: (extension, not in the reference) reads and offset writes wrap around the domain,
+    every cell is written — the lattice Boltzmann step's periodic lattice (``lbm/``) without ghost layers.
     """
     NONE = None
     ZEROS = 'zeros'
     VALID = 'valid'
+    PERIODIC = 'periodic'
 
 
 class DiffModes(str, Enum):

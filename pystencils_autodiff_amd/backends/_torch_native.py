@@ -91,7 +91,7 @@ def _full_write(kernel, field_name=None):
     """True if the kernel writes every cell of its outputs (no untouched border) and, for the given output
     (all outputs if None), every component of a vector field — else the output keeps the reference's
     ``torch.zeros`` allocation (``_torch_native.py:64,108``)."""
-    if not (kernel.ir.zeros or kernel.ir.ghost_layers == 0):
+    if not (kernel.ir.zeros or kernel.ir.periodic or kernel.ir.ghost_layers == 0):
         return False
     return _components_complete(kernel, field_name)
 

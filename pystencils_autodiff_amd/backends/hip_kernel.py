@@ -157,6 +157,8 @@ class HipStencilKernel:
             return 'generic'
         if ir.pointwise:
             return 'generic' if ir.has_index_dims else 'pointwise'
+        if ir.periodic:
+            return 'generic'                   # wrapped reads: one thread per cell
         taps = {}
         for r in ir.reads:
             taps.setdefault(r.field, set()).add(r.offsets)
@@ -192,7 +194,8 @@ class HipStencilKernel:
             elif kind == 'march':
                 src = emit_march(self.ir, kname, variant[1])
             else:
-                src = emit_generic(self.ir, kname, idx32='idx32' in variant[1:], contig='contig' in variant[1:])
+                src = emit_generic(self.ir, kname, idx32='idx32' in variant[1:], contig='contig' in variant[1:],
+                                   shared='shared' in variant[1:])
             self._variants[variant] = (src, kname)
         return self._variants[variant]
 
@@ -371,18 +374,26 @@ class HipStencilKernel:
     def _plan_generic(self, tensors, shape, device):
         from .hip_emitter import magic_u32
         ir = self.ir
+        if ir.periodic and any(r >= int(n) for r, n in zip(ir.radius, shape)):
+            raise ValueError(f'periodic kernel: stencil radius {ir.radius} must be below the extent {shape}')
         bounds = ir.iteration_bounds(shape)
         ncell = int(np.prod([hi - lo for lo, hi in bounds]))
         idx32 = 0 < ncell < 2 ** 31
         contig = all(t.is_contiguous() for t in tensors)
-        variant = ('generic',) + (('idx32',) if idx32 else ()) + (('contig',) if contig else ())
+        # one shape and one set of strides for every tensor, offsets within 32 bits: shared 32-bit addressing
+        reach = max(list(ir.radius) + [0]) + 1
+        shared = len({(tuple(t.shape), tuple(t.stride())) for t in tensors}) == 1 and \
+            sum(abs(int(st)) * (int(n) - 1 + reach) for st, n in zip(tensors[0].stride(), tensors[0].shape)) < 2 ** 31 - 1
+        variant = ('generic',) + (('idx32',) if idx32 else ()) + (('contig',) if contig else ()) + \
+            (('shared',) if shared else ())
         fn = self.function(variant, device)
         statics = [int(n) for n in shape]
-        for t in tensors:
+        for t in (tensors[:1] if shared else tensors):
             statics += [int(s_) for s_ in t.stride()]
+        kinds = ['ptr'] * len(tensors) + ['i64'] * len(shape) + ['i32' if shared else 'i64'] * (len(statics) - len(shape))
         for lo, hi in bounds:
             statics += [lo, hi]
-        kinds = ['ptr'] * len(tensors) + ['i64'] * len(statics)
+            kinds += ['i64', 'i64']
         if idx32:
             extra = [ncell]
             kinds.append('u32')

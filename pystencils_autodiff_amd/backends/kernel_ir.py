@@ -74,6 +74,7 @@ class KernelIR:
     radius: Tuple[int, ...]                # per-axis max |read offset|
     compute_dtype: np.dtype
     symbol_names: Dict[sp.Symbol, str] = dc_field(default_factory=dict)
+    periodic: bool = False                 # reads / offset writes wrap around, full iteration space
 
     @cached_property
     def pointwise(self):
@@ -96,7 +97,7 @@ class KernelIR:
 
     def iteration_bounds(self, shape):
         """Per-axis [lo, hi) of the cells this kernel writes."""
-        g = 0 if self.zeros else self.ghost_layers
+        g = 0 if self.zeros or self.periodic else self.ghost_layers
         return [(g, max(g, int(n) - g)) for n in shape]
 
 
@@ -112,6 +113,8 @@ def lower(assignments, boundary_handling=None, data_type=None):
         assignments = AssignmentCollection(list(assignments), [])
     zeros = boundary_handling is not None and str(getattr(boundary_handling, 'value', boundary_handling)) \
         in ('zeros', 'valid')
+    periodic = boundary_handling is not None and str(getattr(boundary_handling, 'value', boundary_handling)) \
+        == 'periodic'
 
     subexpressions, stores = [], []
     had_conditionals = False
@@ -124,6 +127,8 @@ def lower(assignments, boundary_handling=None, data_type=None):
         else:
             subexpressions.append((a.lhs, rhs))
     zeros = zeros or had_conditionals
+    if periodic and had_conditionals:
+        raise ValueError("periodic boundary handling of assignments with conditional (zero-padded) reads")
     if not stores:
         raise ValueError('kernel without field writes')
 
@@ -163,7 +168,7 @@ def lower(assignments, boundary_handling=None, data_type=None):
 
     radius = tuple(max([abs(int(r.offsets[d])) for r in reads] + [0]) for d in range(ndim))
     ghost_layers = max([max([abs(int(o)) for o in offs] + [0]) for offs in all_accesses] + [0])
-    if zeros or ghost_layers == 0:
+    if zeros or periodic or ghost_layers == 0:
         # components of a vector output that no assignment writes are the zeros of the reference's
         # torch.zeros allocation (_torch_native.py:61-73); with every cell written they become zero
         # stores, so the output is allocated uninitialised and written in one pass (no memset sweep)
@@ -196,7 +201,7 @@ def lower(assignments, boundary_handling=None, data_type=None):
     scalars = sorted(scalars, key=lambda s: s.name)
     ir = KernelIR(ndim=ndim, fields=fields, fields_read=fields_read, fields_written=fields_written,
                   reads=reads, scalars=scalars, subexpressions=subexpressions, stores=stores, zeros=zeros,
-                  ghost_layers=ghost_layers, radius=radius, compute_dtype=compute)
+                  ghost_layers=ghost_layers, radius=radius, compute_dtype=compute, periodic=periodic)
     sym = {}
     for r in reads:
         acc = Field.Access(r.field, r.offsets, r.index)
@@ -238,8 +243,8 @@ def split_soa(ir):
     from ..ps import Assignment
     ac = AssignmentCollection([Assignment(lhs, rhs) for lhs, rhs in stores],
                               [Assignment(s, e) for s, e in subexpressions])
-    out = lower(ac, 'zeros' if ir.zeros else None, np.dtype(ir.compute_dtype).name)
-    if not out.zeros and out.ghost_layers != ir.ghost_layers:
+    out = lower(ac, 'zeros' if ir.zeros else ('periodic' if ir.periodic else None), np.dtype(ir.compute_dtype).name)
+    if not out.zeros and not out.periodic and out.ghost_layers != ir.ghost_layers:
         raise AssertionError('SoA split changed the iteration space')
     return out, comps
 

@@ -2,25 +2,27 @@
 
 ``AutoDiffLatticeBoltzmannStep`` keeps the reference's constructor, field guessing and naming
 (``_autodiff_lbstep.py:27-66,142-160``) but is not an lbmpy ``LatticeBoltzmannStep`` subclass (lbmpy is
-absent): it owns its two pdf arrays (``src`` / ``tmp``, one periodic ghost layer per side, the field's
-memory layout) and runs the time loop the reference's ``run`` / ``run_backward`` drive through lbmpy
-(``:336-398``) directly on the HIP kernels of an ``AutoDiffOp``:
+absent): it owns its pdf arrays (the field's memory layout, lbmpy's default ``fzyx`` = one C-contiguous
+plane per component) and runs the time loop the reference's ``run`` / ``run_backward`` drive through
+lbmpy (``:336-398``) directly on the HIP kernels of an ``AutoDiffOp`` built with
+``boundary_handling='periodic'``: the kernels wrap their reads (and the adjoint its writes) around the
+lattice, so there are no ghost layers, no per-step ghost sync (lbmpy's ``_sync_src``) and no adjoint
+fold-back — one kernel launch per step in each direction:
 
-    forward step:  periodic ghost sync of src → stream-pull-collide kernel (interior cells) → swap
-    adjoint step:  zero the border of diffsrc → transposed kernel (reads diffdst and the RECORDED src of
-                   that step, scatters to diffsrc at x − c_i) → fold ghost contributions back onto the
-                   periodic images (the adjoint of the sync) → swap
+    forward step:  dst = stream-pull-collide(src)                      → swap
+    adjoint step:  diffsrc = transposed kernel(diffdst, recorded src)  → swap
+                   (scatter to x − c_i: for a fixed component i, x ↦ x − c_i is a bijection of the
+                   periodic lattice, so every (component, cell) is written exactly once, no zero fill)
 
 Deliberate deviations, each because the reference's behaviour is not a gradient:
 * the adjoint is the ``DiffModes.TRANSPOSED`` form (``_autodiff.py:354-437``), not TF-MAD. TF-MAD
   evaluates ∂f/∂src at the unshifted cell (``_autodiff.py:102-109``), exact only for linear stencils, and
   its vector-field branch keeps only the last component's assignment (``_autodiff.py:138-152``); the
-  collision is nonlinear and all components are needed. For pull streaming each component is read at ONE
-  offset, so the transposed (scatter) adjoint still writes every (component, cell) exactly once.
+  collision is nonlinear and all components are needed.
 * the backward of T steps needs each step's src state (the collision Jacobian depends on it): the forward
-  records them (``record=True`` / the timestep op); the reference's ``run_backward`` re-uses whatever the
-  arrays hold.
-Only periodic domains are built (lbmpy's boundary handling / ``AdjointBoundaryCondition``,
+  records them (``record=True`` / the timestep op: T + 1 arrays, written in turn, no copies); the
+  reference's ``run_backward`` re-uses whatever the arrays hold.
+Only periodic lattices are built (lbmpy's boundary handling / ``AdjointBoundaryCondition``,
 ``adjoint_boundaryconditions.py``, needs lbmpy's flag fields).
 """
 import numpy as np
@@ -101,12 +103,12 @@ class AutoDiffLatticeBoltzmannStep:
         if domain_size is None:
             if not src.has_fixed_shape:
                 raise ValueError('domain_size is required for variable-size pdf fields')
-            domain_size = tuple(int(s) - 2 for s in src.spatial_shape)
+            domain_size = tuple(int(s) for s in src.spatial_shape)
         self.domain_size = tuple(int(s) for s in domain_size)
         if len(self.domain_size) != src.spatial_dimensions or min(self.domain_size) < 2:
             raise ValueError(f'domain_size {self.domain_size} does not fit the {src.spatial_dimensions}-D pdf field')
-        # interior-only kernels (ghost layer 1, ``boundary_handling=None``) and the transposed adjoint
-        self._autodiff = AutoDiffOp(update_rule, 'LBM', boundary_handling=None, diff_mode='transposed',
+        # periodic kernels (wrapped reads, every cell written) and the transposed adjoint
+        self._autodiff = AutoDiffOp(update_rule, 'LBM', boundary_handling='periodic', diff_mode='transposed',
                                     time_constant_fields=list(time_constant_fields) or None,
                                     constant_fields=list(constant_fields))
         self._additional_fields = [f for f in self._autodiff.forward_input_fields if f not in (src, tmp)]
@@ -150,21 +152,24 @@ class AutoDiffLatticeBoltzmannStep:
         return self._autodiff
 
     # -- arrays ------------------------------------------------------------------------------------
-    def _alloc(self):
-        """A padded pdf array in the field's memory layout: spatial axes first in the returned view."""
+    def _alloc(self, zero=True):
+        """A pdf array in the field's memory layout, spatial axes first in the returned view (``zero=False``:
+        uninitialised, for arrays a kernel writes completely)."""
         Q = int(self.pdf_field.index_shape[0])
-        padded = [s + 2 for s in self.domain_size]
+        dims = list(self.domain_size)
         dt = self.pdf_field.dtype.numpy_dtype
         if self._gpu:
             torch = _torch()
             tdt = getattr(torch, np.dtype(dt).name)
             dev = self._device or torch.device('cuda', torch.cuda.current_device())
+            new = torch.zeros if zero else torch.empty
             if self.pdf_field.is_soa:
-                return torch.zeros([Q] + padded, dtype=tdt, device=dev).permute(*range(1, len(padded) + 1), 0)
-            return torch.zeros(padded + [Q], dtype=tdt, device=dev)
+                return new([Q] + dims, dtype=tdt, device=dev).permute(*range(1, len(dims) + 1), 0)
+            return new(dims + [Q], dtype=tdt, device=dev)
+        new = np.zeros if zero else np.empty
         if self.pdf_field.is_soa:
-            return np.moveaxis(np.zeros([Q] + padded, dtype=dt), 0, -1)
-        return np.zeros(padded + [Q], dtype=dt)
+            return np.moveaxis(new([Q] + dims, dtype=dt), 0, -1)
+        return new(dims + [Q], dtype=dt)
 
     def _array(self, name):
         if name not in self._arrays:
@@ -173,43 +178,12 @@ class AutoDiffLatticeBoltzmannStep:
 
     @property
     def pdf_array(self):
-        """Interior view of the current pdfs (``[*domain_size, q]``)."""
-        return self._interior(self._array(self._pdf_arr_name))
+        """The current pdfs (``[*domain_size, q]``)."""
+        return self._array(self._pdf_arr_name)
 
     def set_pdfs(self, pdfs):
-        a = self._array(self._pdf_arr_name)
-        self._interior(a)[...] = pdfs
+        self._array(self._pdf_arr_name)[...] = pdfs
         self._records = None
-
-    def _interior(self, a):
-        return a[tuple(slice(1, -1) for _ in self.domain_size)]
-
-    def _slab(self, a, axis, i):
-        return a[tuple(i if d == axis else slice(None) for d in range(len(self.domain_size)))]
-
-    def _sync(self, a):
-        """Periodic ghost layers, axis by axis (the corner ghosts come out right): the reference's
-        ``_sync_src`` periodic communication."""
-        for d, n in enumerate(self.domain_size):
-            self._slab(a, d, 0)[...] = self._slab(a, d, n)
-            self._slab(a, d, n + 1)[...] = self._slab(a, d, 1)
-
-    def _sync_adjoint(self, g):
-        """Adjoint of ``_sync``: ghost contributions are added to the interior cells they were copied from
-        (axes in reverse order), then the ghosts are cleared."""
-        for d in reversed(range(len(self.domain_size))):
-            n = self.domain_size[d]
-            self._slab(g, d, n)[...] += self._slab(g, d, 0)
-            self._slab(g, d, 1)[...] += self._slab(g, d, n + 1)
-            self._slab(g, d, 0)[...] = 0
-            self._slab(g, d, n + 1)[...] = 0
-
-    def _clear_border(self, g):
-        """Cells the transposed kernel may leave unwritten: the two outermost layers on each side (for
-        |c| ≤ 1 a component is written at x = y − c for interior y only)."""
-        for d, n in enumerate(self.domain_size):
-            for i in (0, 1, n, n + 1):
-                self._slab(g, d, i)[...] = 0
 
     # -- kernels -----------------------------------------------------------------------------------
     def _kernels(self):
@@ -229,38 +203,40 @@ class AutoDiffLatticeBoltzmannStep:
 
     # -- time loops --------------------------------------------------------------------------------
     def time_step(self, extra=None):
-        """One forward step on the owned arrays: sync, stream-pull-collide, swap."""
-        a, b = self._array(self._pdf_arr_name), self._array(self._tmp_arr_name)
-        self._sync(a)
+        """One forward step on the owned arrays: stream-pull-collide, swap. While recording, the step writes
+        into a fresh array and its src stays as the record (no copies)."""
+        a = self._array(self._pdf_arr_name)
         if self._records is not None:
-            self._records.append(a.clone() if self._gpu else a.copy())
+            self._records.append(a)
+            b = self._alloc(zero=False)
+            self._fwd(a, b, extra or {})
+            self._arrays[self._pdf_arr_name] = b
+            return
+        b = self._array(self._tmp_arr_name)
         self._fwd(a, b, extra or {})
         self._arrays[self._pdf_arr_name], self._arrays[self._tmp_arr_name] = b, a
 
     def run(self, time_steps, record=False, extra=None):
-        """``time_steps`` forward steps; ``record=True`` keeps each step's src state for ``run_backward``."""
+        """``time_steps`` forward steps; ``record=True`` keeps each step's src state for ``run_backward``
+        (T + 1 pdf arrays live until the backward has consumed them)."""
         self._records = [] if record else None
         for _ in range(int(time_steps)):
             self.time_step(extra)
 
     def backward_time_step(self, src_state, extra=None, extra_adj=None):
-        """One adjoint step: diffsrc = Sᵀ Kᵀ(diffdst) with the collision Jacobian at ``src_state``."""
+        """One adjoint step: diffsrc = Kᵀ(diffdst) with the collision Jacobian at ``src_state``."""
         g_dst = self._array(self.backward_pdf_array_name)
         g_src = self._array(self._backward_tmp_array_name)
-        self._clear_border(g_src)
         self._bwd(src_state, g_dst, g_src, extra or {}, extra_adj or {})
-        self._sync_adjoint(g_src)
         self._arrays[self.backward_pdf_array_name], self._arrays[self._backward_tmp_array_name] = g_src, g_dst
 
     def set_adjoint_pdfs(self, grad):
-        """The adjoint of the current (final) pdfs, interior values; the ghost layer stays zero."""
-        g = self._array(self.backward_pdf_array_name)
-        g[...] = 0
-        self._interior(g)[...] = grad
+        """The adjoint of the current (final) pdfs."""
+        self._array(self.backward_pdf_array_name)[...] = grad
 
     @property
     def adjoint_pdf_array(self):
-        return self._interior(self._array(self.backward_pdf_array_name))
+        return self._array(self.backward_pdf_array_name)
 
     def run_backward(self, time_steps, extra=None, extra_adj=None):
         """``time_steps`` adjoint steps in reverse over the states the last ``run(..., record=True)`` kept;

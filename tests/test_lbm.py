@@ -170,3 +170,47 @@ def test_lbm_full_size_properties(stencil, shape):
     step.run_backward(T)
     gg = step.adjoint_pdf_array.double().cpu().numpy()
     assert np.abs(gg - gref).max() <= 1e-5 * np.abs(gref).max()
+
+
+def _periodic_case():
+    import sympy as sp
+    u, v = ps.fields("u, v: float64[2D]")
+    ac = ps.AssignmentCollection([ps.Assignment(v.center, 0.3 * u[1, 0] - 0.7 * u[0, -1] + 0.25 * u[-1, 1]
+                                                + sp.Rational(1, 5) * u.center)])
+    return ac
+
+
+def _periodic_ref(x):
+    return 0.3 * np.roll(x, -1, 0) - 0.7 * np.roll(x, 1, 1) + 0.25 * np.roll(np.roll(x, 1, 0), -1, 1) + 0.2 * x
+
+
+def test_periodic_boundary_cpu():
+    """``boundary_handling='periodic'`` (extension used by the LBM step): wrapped reads, forward and the
+    TF-MAD adjoint (exact for this linear stencil) against array rolls."""
+    import pystencils_autodiff_amd as pa
+    op = pa.AutoDiffOp(_periodic_case(), boundary_handling='periodic')
+    x = np.random.default_rng(0).standard_normal((9, 7))
+    out = np.empty_like(x)
+    op.forward_ast_cpu.compile()(u=x, v=out)
+    assert np.abs(out - _periodic_ref(x)).max() < 1e-14
+    g = np.random.default_rng(1).standard_normal((9, 7))
+    gu = np.empty_like(x)
+    op.backward_ast_cpu.compile()(diffv=g, diffu=gu)
+    assert abs(np.vdot(_periodic_ref(x), g) - np.vdot(x, gu)) < 1e-12 * np.abs(g).sum()
+
+
+@pytest.mark.gpu
+def test_periodic_boundary_gpu():
+    import torch
+    import pystencils_autodiff_amd as pa
+    op = pa.AutoDiffOp(_periodic_case(), boundary_handling='periodic')
+    fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    x = torch.tensor(np.random.default_rng(0).standard_normal((67, 129)), device='cuda', requires_grad=True)
+    (out,) = fn.apply(x)
+    assert np.abs(out.detach().cpu().numpy() - _periodic_ref(x.detach().cpu().numpy())).max() < 1e-13
+    g = torch.tensor(np.random.default_rng(1).standard_normal((67, 129)), device='cuda')
+    out.backward(g)
+    lhs = float((out.detach() * g).sum())
+    rhs = float((x.detach() * x.grad).sum())
+    assert abs(lhs - rhs) < 1e-11 * float(g.abs().sum())
+    assert op.forward_ast_gpu.compile().last_variant[0] == 'generic'
