@@ -107,10 +107,15 @@ class AutoDiffLatticeBoltzmannStep:
         self.domain_size = tuple(int(s) for s in domain_size)
         if len(self.domain_size) != src.spatial_dimensions or min(self.domain_size) < 2:
             raise ValueError(f'domain_size {self.domain_size} does not fit the {src.spatial_dimensions}-D pdf field')
-        # periodic kernels (wrapped reads, every cell written) and the transposed adjoint
+        # periodic kernels (wrapped reads, every cell written) and the transposed adjoint — for the rules of
+        # ``create_lb_update_rule`` written through the collision's structure (``create_lb_adjoint_rule``)
+        backward = None
+        if getattr(update_rule, 'stencil', None) is not None and not time_constant_fields:
+            from ._method import create_lb_adjoint_rule
+            backward = create_lb_adjoint_rule(update_rule)
         self._autodiff = AutoDiffOp(update_rule, 'LBM', boundary_handling='periodic', diff_mode='transposed',
                                     time_constant_fields=list(time_constant_fields) or None,
-                                    constant_fields=list(constant_fields))
+                                    constant_fields=list(constant_fields), backward_assignments=backward)
         self._additional_fields = [f for f in self._autodiff.forward_input_fields if f not in (src, tmp)]
         scalars = sorted({s for a in update_rule.all_assignments for s in a.rhs.free_symbols
                           if isinstance(s, sp.Symbol) and not isinstance(s, ps.Field.Access)}
@@ -170,6 +175,20 @@ class AutoDiffLatticeBoltzmannStep:
         if self.pdf_field.is_soa:
             return np.moveaxis(new([Q] + dims, dtype=dt), 0, -1)
         return new(dims + [Q], dtype=dt)
+
+    def empty_pdfs(self):
+        """An uninitialised pdf tensor in the step's memory layout (``[*domain_size, q]`` view; for ``fzyx``
+        one contiguous plane per component) — inputs in this layout enter the timestep op without a copy."""
+        return self._alloc(zero=False)
+
+    def _as_layout(self, t):
+        """``t`` itself if it has the step's memory layout, else a copy in it."""
+        ref = self._array(self._pdf_arr_name)
+        if tuple(t.shape) == tuple(ref.shape) and tuple(t.stride()) == tuple(ref.stride()) and t.dtype == ref.dtype:
+            return t
+        out = self._alloc(zero=False)
+        out.copy_(t)
+        return out
 
     def _array(self, name):
         if name not in self._arrays:
@@ -262,23 +281,39 @@ class AutoDiffLatticeBoltzmannStep:
         class LbmTimesteps(torch.autograd.Function):
             @staticmethod
             def forward(ctx, pdfs):
-                if step._gpu and not pdfs.is_cuda:
-                    pdfs = pdfs.cuda()
-                step.set_pdfs(pdfs.detach() if step._gpu else pdfs.detach().cpu().numpy())
-                step.run(T, record=True)
-                ctx.records = step._records
-                step._records = None
-                out = step.pdf_array
-                return out.clone() if step._gpu else torch.from_numpy(out.copy())
+                if not step._gpu:
+                    step.set_pdfs(pdfs.detach().cpu().numpy())
+                    step.run(T, record=True)
+                    ctx.records = step._records
+                    step._records = None
+                    return torch.from_numpy(step.pdf_array.copy())
+                # states on fresh arrays in the field's layout: the input is the first state when it has
+                # that layout already (``empty_pdfs``), the output is the last — no copies
+                states = [step._as_layout(pdfs.detach())]
+                for _ in range(T):
+                    out = step._alloc(zero=False)
+                    step._fwd(states[-1], out, {})
+                    states.append(out)
+                ctx.records = states[:-1]
+                return states[-1]
 
             @staticmethod
             def backward(ctx, grad):
-                step._records = ctx.records
-                step.set_adjoint_pdfs(grad if step._gpu else grad.detach().cpu().numpy())
-                step.run_backward(T)
+                if not step._gpu:
+                    step._records = ctx.records
+                    step.set_adjoint_pdfs(grad.detach().cpu().numpy())
+                    step.run_backward(T)
+                    ctx.records = None
+                    return torch.from_numpy(step.adjoint_pdf_array.copy())
+                g = step._as_layout(grad)
+                cur, spare = g, None                # cur: adjoint of state t + 1 (never written when it is g)
+                for t in reversed(range(T)):
+                    nxt = spare if spare is not None else step._alloc(zero=False)
+                    step._bwd(ctx.records[t], cur, nxt, {}, {})
+                    spare = cur if cur is not g else None
+                    cur = nxt
                 ctx.records = None
-                g = step.adjoint_pdf_array
-                return g.clone() if step._gpu else torch.from_numpy(g.copy())
+                return cur
 
         LbmTimesteps.num_time_steps = T
         LbmTimesteps.lb_step = self

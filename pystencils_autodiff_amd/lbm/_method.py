@@ -20,7 +20,8 @@ import sympy as sp
 
 from .. import ps
 
-__all__ = ['LBStencil', 'create_lb_update_rule', 'macroscopic_getter', 'equilibrium_setter']
+__all__ = ['LBStencil', 'create_lb_update_rule', 'create_lb_adjoint_rule', 'macroscopic_getter',
+           'equilibrium_setter']
 
 
 class LBStencil:
@@ -105,6 +106,45 @@ def create_lb_update_rule(stencil='D2Q9', relaxation_rate=None, compressible=Fal
     ac.compressible = compressible
     ac.relaxation_rate = omega
     return ac
+
+
+def create_lb_adjoint_rule(update_rule, diff_fields_prefix='diff'):
+    """The exact adjoint of a ``create_lb_update_rule`` rule in scatter form (what ``DiffModes.TRANSPOSED``
+    derives, ``_autodiff.py:354-437``, written through the collision's structure instead of Q² expanded
+    partial derivatives). With g_i = diffdst_i(y) and the pulled f_j = src_j(y − c_j) of cell y:
+
+        diffsrc_j(y − c_j) = (1 − ω) g_j + ω (A + Σ_a B_a ∂u_a/∂f_j),
+        A = Σ_i g_i ∂feq_i/∂ρ,   B_a = Σ_i g_i ∂feq_i/∂u_a,
+        ∂u_a/∂f_j = (c_ja − u_a)/ρ  (compressible)   or   c_ja  (incompressible)
+
+    — O(q·d) arithmetic per cell instead of O(q²). For a fixed component j the map y ↦ y − c_j is a
+    bijection of the (periodic) lattice, so every (j, cell) of diffsrc is written exactly once."""
+    st = update_rule.stencil
+    comp = update_rule.compressible
+    omega = update_rule.relaxation_rate
+    src = update_rule.free_fields
+    dst = update_rule.bound_fields
+    (src,), (dst,) = tuple(src), tuple(dst)
+    from .._adjoint_field import AdjointField
+    dsrc, ddst = AdjointField(src, diff_fields_prefix), AdjointField(dst, diff_fields_prefix)
+    f = [src[tuple(-c for c in st.directions[i])](i) for i in range(st.Q)]
+    g = [ddst.center(i) for i in range(st.Q)]
+    rho, us, subs = _moments(st, f, comp)
+    feq = [_feq(st, i, rho, us, comp) for i in range(st.Q)]
+    A = sp.Symbol('adj_rho')
+    B = sp.symbols(f'adj_u_:{st.D}')
+    subs.append(ps.Assignment(A, sum(gi * sp.diff(fe, rho) for gi, fe in zip(g, feq))))
+    for a in range(st.D):
+        subs.append(ps.Assignment(B[a], sum(gi * sp.diff(fe, us[a]) for gi, fe in zip(g, feq))))
+    if comp:
+        inv = sp.Symbol('inv_rho')
+        subs.append(ps.Assignment(inv, 1 / rho))
+    main = []
+    for j, c in enumerate(st.directions):
+        du = [(c[a] - us[a]) * inv if comp else c[a] for a in range(st.D)]
+        rhs = (1 - omega) * g[j] + omega * (A + sum(B[a] * du[a] for a in range(st.D) if du[a] != 0))
+        main.append(ps.Assignment(dsrc[tuple(-ci for ci in c)](j), rhs))
+    return ps.AssignmentCollection(main, subs)
 
 
 def macroscopic_getter(stencil, pdf_field, density_field, velocity_field, compressible=False):

@@ -169,8 +169,12 @@ def run_lbm(name, stencil, shape, dtype, T=10, reps=3, compressible=False):
     g = torch.Generator(device='cuda').manual_seed(0)
     f0 = (torch.full(tuple(shape) + (q,), 1.0 / q, device='cuda', dtype=torch.float64) *
           (1 + 0.01 * torch.rand(tuple(shape) + (q,), generator=g, device='cuda', dtype=torch.float64))).to(dtype)
-    x = f0.clone().requires_grad_(True)
-    gr = torch.rand(tuple(shape) + (q,), generator=g, device='cuda', dtype=dtype)
+    # inputs in the step's fzyx layout (one plane per component): no layout copies inside the op
+    x = step.empty_pdfs()
+    x.copy_(f0)
+    x.requires_grad_(True)
+    gr = step.empty_pdfs()
+    gr.copy_(torch.rand(tuple(shape) + (q,), generator=g, device='cuda', dtype=dtype))
     fw, bw = [], []
     for i in range(reps + 1):
         e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))

@@ -134,16 +134,29 @@ def test_lbm_steps_gpu_vs_oracle(stencil, shape, compressible, layout, dtype):
 
 
 @pytest.mark.gpu
-def test_lbm_timestep_op_gpu_autograd():
+@pytest.mark.parametrize('native_layout', [False, True])
+def test_lbm_timestep_op_gpu_autograd(native_layout):
+    """The T-step op: inputs and gradients in numpy layout (copied into fzyx) or already in the step's
+    layout (``empty_pdfs``: used in place, never written)."""
     import torch
     rule = lbm.create_lb_update_rule('D2Q9', compressible=True, data_type='float64')
     step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=(48, 40), relaxation_rate=1.7, target='gpu')
     Op = step.create_timestep_op(6)
     f0 = _init('D2Q9', (48, 40), True, seed=5)
-    x = torch.tensor(f0, requires_grad=True, device='cuda')
-    out = Op.apply(x)
     g = torch.tensor(np.random.default_rng(6).standard_normal(f0.shape), device='cuda')
+    if native_layout:
+        x = step.empty_pdfs()
+        x.copy_(torch.tensor(f0, device='cuda'))
+        x.requires_grad_(True)
+        g2 = step.empty_pdfs()
+        g2.copy_(g)
+        g = g2
+    else:
+        x = torch.tensor(f0, requires_grad=True, device='cuda')
+    g_before = g.clone()
+    out = Op.apply(x)
     out.backward(g)
+    assert torch.equal(g, g_before)
     ref, gref = _oracle_grad(f0, 1.7, 6, 'D2Q9', True, g.cpu().numpy(), device='cuda')
     assert np.abs(out.detach().cpu().numpy() - ref).max() <= 1e-12
     assert np.abs(x.grad.cpu().numpy() - gref).max() <= 1e-11 * np.abs(gref).max()
