@@ -193,6 +193,162 @@ def _launch(call, kwargs, pending):
             fill()
 
 
+_native = None
+
+
+def native_module():
+    """The ``_psad_torch`` extension (``csrc/psad_torch.cpp``): the op's autograd node in C++. Raises if it
+    has not been built, like ``libpsad_hip.so``; ``PSAD_NATIVE_AUTOGRAD=0`` selects the Python Function."""
+    global _native
+    if _native is None:
+        import os
+        if os.environ.get('PSAD_NATIVE_AUTOGRAD', '1') == '0':
+            _native = False
+        else:
+            import torch  # noqa: F401  (the extension resolves torch's symbols from the loaded libraries)
+            try:
+                from .. import _psad_torch
+            except ImportError as exc:
+                raise ImportError(f"{exc}: build the extension with `python -m pystencils_autodiff_amd.build`") \
+                    from exc
+            _native = _psad_torch
+    return _native or None
+
+
+# c10::ScalarType codes of the dtypes the kernels take
+_SCALAR_TYPE = {'float16': 5, 'float32': 6, 'float64': 7}
+
+
+class _NativePath:
+    """The forward + adjoint launches of one op as a C++ ``torch::autograd::Function`` (``_psad_torch``):
+    the backward then runs on torch's autograd device thread without Python (no GIL hand-off), the forward
+    without the Python Function's bookkeeping. One native plan per input signature (input shapes, dtypes,
+    device, scalar values), resolved by the kernels' own ``prepare`` on the first call. Ops the plan
+    cannot express take the Python Function: fzyx fields, outputs with a zero border larger than
+    ``BORDER_ZERO_MIN`` (the border kernel beats a memset there), no backward kernel, inputs that are
+    not contiguous 32-byte-aligned device tensors."""
+
+    def __init__(self, spec):
+        self.spec = spec
+        self.plans = {}
+
+    def _kind(self, alloc, shape):
+        import torch
+        if alloc is torch.empty:
+            return False
+        if alloc is torch.zeros:
+            return True
+        if getattr(alloc, 'border', False):
+            n = 1
+            for s in shape:
+                n *= int(s)
+            return True if n < BORDER_ZERO_MIN else None
+        return None
+
+    def __call__(self, args):
+        import torch
+        s = self.spec
+        if len(args) != len(s['fwd_inputs']) or not args or not isinstance(args[0], torch.Tensor):
+            return None
+        try:
+            scal = tuple(s['class_kwargs'][n] for n in s['scalar_names'])
+        except KeyError:
+            return None
+        a0 = args[0]
+        key = (scal, tuple(a0.shape), a0.dtype, a0.device)
+        pid = self.plans.get(key)
+        if pid is None:
+            pid = self._build(args, scal)
+            if pid is None:
+                return None
+            self.plans[key] = pid
+        outs = native_module().apply(pid, list(args))
+        return None if outs is None else tuple(outs)
+
+    def _build(self, args, scal):
+        import struct
+
+        import torch
+        s = self.spec
+        for a in args:
+            if not isinstance(a, torch.Tensor) or not a.is_cuda or not a.is_contiguous() or a.data_ptr() % 32 \
+                    or a.device != args[0].device or str(a.dtype).replace('torch.', '') not in _SCALAR_TYPE:
+                return None
+        dev = args[0].device
+        scalars = dict(zip(s['scalar_names'], scal))
+
+        def alloc_specs(outs, like_shape, kw):
+            shapes, dtypes, zero, names = [], [], [], []
+            for name, dtype, fixed, alloc, sdim, ishape in outs:
+                shape = tuple(fixed) if fixed is not None else tuple(like_shape[:sdim]) + tuple(ishape)
+                z = self._kind(alloc, shape)
+                if z is None or str(dtype).replace('torch.', '') not in _SCALAR_TYPE:
+                    return None
+                kw[name] = torch.empty(shape, dtype=dtype, device=dev)
+                shapes.append(list(shape))
+                dtypes.append(_SCALAR_TYPE[str(dtype).replace('torch.', '')])
+                zero.append(z)
+                names.append(name)
+            return shapes, dtypes, zero, names
+
+        def resolve(call, kw, table):
+            prep = call.prepare(**{n: v for n, v in kw.items()})
+            if prep is None:
+                return None
+            fn, grid, block, packed, xb, _ = prep
+            names = [f[0] for f in call._field_specs()]
+            if grid == 0 or xb or len(packed) < 8 * len(names) or any(n not in table for n in names):
+                return None
+            if list(struct.unpack_from(f'<{len(names)}Q', packed)) != [kw[n].data_ptr() for n in names]:
+                return None                     # pointer slots are not the leading 8-byte arguments
+            return int(fn), int(grid), int(block), bytes(packed), [table.index(n) for n in names]
+
+        fwd_call, bwd_call = s['fwd_call'], s['bwd_call']
+        if getattr(fwd_call, '_soa', None) or getattr(bwd_call, '_soa', None):
+            return None
+        kw = dict(scalars)
+        in_names = [f.name for f in s['fwd_inputs']]
+        for name, a in zip(in_names, args):
+            kw[name] = a
+        fo = alloc_specs(s['fwd_out'], tuple(args[0].shape), kw)
+        if fo is None:
+            return None
+        fwd_table = in_names + fo[3]
+        try:
+            fl = resolve(fwd_call, kw, fwd_table)
+        except (TypeError, ValueError):
+            return None
+        if fl is None:
+            return None
+        saved_names = [n for n in s['saved_fwd'] if n in kw]
+        bkw = dict(scalars)
+        for n in saved_names:
+            bkw[n] = kw[n]
+        grad_names = []
+        for i, (aname, dtype, fixed, strides, fname) in enumerate(s['grad_specs']):
+            g = torch.empty_like(kw[fname])
+            grad_names.append(aname if aname is not None else f'\0grad{i}')
+            if aname is not None:
+                bkw[aname] = g
+        bo = alloc_specs(s['bwd_out'], tuple(kw[s['fwd_out'][0][0]].shape), bkw)
+        if bo is None:
+            return None
+        bwd_table = saved_names + grad_names + bo[3]
+        try:
+            bl = resolve(bwd_call, bkw, bwd_table)
+        except (TypeError, ValueError):
+            return None
+        if bl is None:
+            return None
+        grad_of_input = [bwd_table.index(a, len(saved_names) + len(grad_names)) if a is not None and a in bo[3]
+                         else -1 for a in s['in_adj']]
+        return native_module().register_plan(
+            s['op_name'], dev.index, [list(a.shape) for a in args],
+            [_SCALAR_TYPE[str(a.dtype).replace('torch.', '')] for a in args],
+            fo[0], fo[1], fo[2], *fl[:4], fl[4], [fwd_table.index(n) for n in saved_names],
+            bo[0], bo[1], bo[2], *bl[:4], bl[4], grad_of_input)
+
+
 def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
     import torch
 
@@ -348,11 +504,29 @@ def create_autograd_function(autodiff_obj, use_cuda, op_name=None):
             rtn = rtn[0]
         return rtn
 
+    native = None
+    if use_cuda and backward_kernel is not None and not soa_fields and native_module() is not None:
+        native = _NativePath({
+            'op_name': op_name, 'fwd_inputs': fwd_inputs, 'fwd_out': fwd_out, 'bwd_out': bwd_out,
+            'grad_specs': grad_specs, 'saved_fwd': saved_fwd, 'in_adj': in_adj, 'class_kwargs': class_kwargs,
+            'scalar_names': sorted(set(fwd_scalars) | set(bwd_scalars)), 'fwd_call': fwd_call, 'bwd_call': bwd_call})
+    function_apply = torch.autograd.Function.apply.__func__
+
+    def apply(cls, *args, **kwargs):
+        """``Op.apply(*inputs)``: through the native autograd node when the call fits its plan, else the
+        Python Function (same kernels, same results)."""
+        if native is not None and not kwargs:
+            outs = native(args)
+            if outs is not None:
+                return outs
+        return function_apply(cls, *args, **kwargs)
+
     parameters = module.kernel_wrappers[0].get_parameters()
     cls = type(op_name, (torch.autograd.Function,), {
         'forward': staticmethod(forward),
         'backward': staticmethod(backward),
         'call': classmethod(call),
+        'apply': classmethod(apply),
     })
     cls.class_kwargs = class_kwargs
     cls.kernel = forward_kernel

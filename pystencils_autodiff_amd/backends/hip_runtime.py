@@ -47,7 +47,19 @@ def lib():
         if not os.path.exists(library_path):
             raise HipError(f"{library_path} is missing: build the MI355X extension with "
                            "`python -m pystencils_autodiff_amd.build` (no CPU fallback exists for the GPU path)")
-        L = ctypes.CDLL(library_path)
+        # Calls keep the GIL (PyDLL): launches and stream-ordered enqueues return in microseconds, and
+        # dropping the GIL around each one (ctypes.CDLL) hands it to torch's autograd device thread and
+        # back — 2-D 4096² apply+backward 115 -> 52 us per step with the default multithreaded engine
+        # (scripts/probes/autograd_handoff.py, profiles/r02_autograd_handoff.log). The calls that can
+        # run for milliseconds (hiprtc compile, code-object load) go through a CDLL handle and release it.
+        L = ctypes.PyDLL(library_path)
+        C = ctypes.CDLL(library_path)
+        L.psad_rtc_compile = C.psad_rtc_compile
+        L.psad_module_load = C.psad_module_load
+        L.psad_rccl_open = C.psad_rccl_open               # and the collective RCCL setup calls
+        L.psad_rccl_unique_id = C.psad_rccl_unique_id
+        L.psad_rccl_comm_init = C.psad_rccl_comm_init
+        L.psad_rccl_comm_destroy = C.psad_rccl_comm_destroy
         c_int, c_size, vp, cp = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p
         L.psad_abi_version.restype = c_int
         L.psad_rtc_version.restype = c_int

@@ -1,8 +1,10 @@
-"""Build the in-tree native library ``libpsad_hip.so`` (``python -m pystencils_autodiff_amd.build``).
+"""Build the in-tree native libraries (``python -m pystencils_autodiff_amd.build``).
 
-``hipcc --offload-arch=gfx950`` is not needed for the shim itself (it holds no
-device code — kernels are emitted at run time and compiled by hiprtc); it is
-compiled with hipcc so the HIP runtime / hiprtc headers and libraries resolve.
+* ``libpsad_hip.so`` — the C ABI (``include/psad.h``). ``hipcc --offload-arch=gfx950`` is not needed for
+  the shim itself (it holds no device code — kernels are emitted at run time and compiled by hiprtc); it
+  is compiled with hipcc so the HIP runtime / hiprtc headers and libraries resolve.
+* ``_psad_torch.so`` — the op's native autograd node (``csrc/psad_torch.cpp``), a torch extension module
+  compiled with g++ against torch's headers and linked to ``libpsad_hip.so`` (host code only).
 """
 import os
 import subprocess
@@ -12,6 +14,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRCS = [os.path.join(HERE, 'csrc', f) for f in ('psad_hip.cpp', 'psad_halo.cpp')]
 OUT = os.path.join(HERE, 'libpsad_hip.so')
+TORCH_SRC = os.path.join(HERE, 'csrc', 'psad_torch.cpp')
+TORCH_OUT = os.path.join(HERE, '_psad_torch.so')
 
 
 def build(force=False, verbose=False):
@@ -30,5 +34,37 @@ def build(force=False, verbose=False):
     return OUT
 
 
+def build_torch_ext(force=False, verbose=False):
+    """``_psad_torch.so``: g++ (no device code) with torch's include / library paths."""
+    deps = [TORCH_SRC, OUT, os.path.join(ROOT, 'include', 'psad.h')]
+    if not force and os.path.exists(TORCH_OUT) and \
+            all(os.path.getmtime(TORCH_OUT) >= os.path.getmtime(d) for d in deps):
+        return TORCH_OUT
+    import sysconfig
+
+    import torch
+    from torch.utils import cpp_extension
+    cxx = os.environ.get('CXX', 'g++')
+    tlib = cpp_extension.library_paths()[0]
+    cmd = [cxx, '-O2', '-fPIC', '-shared', '-std=c++17', '-D__HIP_PLATFORM_AMD__=1', '-DUSE_ROCM=1',
+           '-DTORCH_EXTENSION_NAME=_psad_torch',
+           f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}",
+           *[f'-I{p}' for p in cpp_extension.include_paths()], f"-I{sysconfig.get_paths()['include']}",
+           '-I/opt/rocm/include', f"-I{os.path.join(ROOT, 'include')}", TORCH_SRC, '-o', TORCH_OUT + '.tmp',
+           f'-L{tlib}', '-lc10', '-lc10_hip', '-ltorch', '-ltorch_cpu', '-ltorch_python', f'-L{HERE}', '-lpsad_hip',
+           f'-Wl,-rpath,$ORIGIN:{tlib}']
+    if verbose:
+        print(' '.join(cmd))
+    proc = subprocess.run(cmd, capture_output=True, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError(f"building _psad_torch.so failed:\n{proc.stdout}\n{proc.stderr}")
+    os.replace(TORCH_OUT + '.tmp', TORCH_OUT)
+    return TORCH_OUT
+
+
+def build_all(force=False, verbose=False):
+    return build(force, verbose), build_torch_ext(force, verbose)
+
+
 if __name__ == '__main__':
-    print(build(force='--force' in sys.argv, verbose=True))
+    print(build_all(force='--force' in sys.argv, verbose=True))

@@ -1,0 +1,207 @@
+// psad_torch.cpp — native autograd node for the torch_native op (_psad_torch extension module).
+//
+// The reference's op is a Python torch.autograd.Function (backends/_torch_native.py:10-142) whose backward
+// torch's autograd engine runs on its per-device thread: the Python backward needs the GIL on that thread,
+// and for a small field the engine's thread hand-off plus the Python body is longer than the kernels
+// (2-D 4096² 5-point: 44 µs of kernels, 115-166 µs per apply+backward step,
+// scripts/probes/autograd_handoff.py). Here the same forward/backward launches are a C++
+// torch::autograd::Function: the forward allocates, patches the tensor pointers into a launch-argument
+// template and launches through the C ABI (psad_launch, include/psad.h) on the current stream; the
+// backward does the same for the adjoint kernel on the engine's thread without touching Python.
+//
+// A plan (both launches, resolved once by the Python op for one input signature — shapes, dtypes, scalar
+// values — by HipStencilKernel.prepare) holds: the function handle, grid and block, the packed argument
+// template whose first n_ptr 8-byte slots are the field pointers (hip_kernel._Plan.pack), and for each
+// slot the index of the tensor in the call's table. Forward table: inputs ++ outputs; backward table:
+// saved forward tensors ++ output gradients ++ adjoint outputs. apply() returns None when a call does not
+// match its plan (device, dtype, shape, contiguity, 32-byte alignment): the Python op then takes the
+// general path.
+#include <torch/extension.h>
+
+#include <c10/hip/HIPStream.h>
+
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "psad.h"
+
+namespace {
+
+struct Launch {
+    void* fn = nullptr;
+    unsigned grid = 0, block = 0;
+    std::string args;          // packed template; pointer i at byte 8*i
+    std::vector<int64_t> slot; // pointer i <- table[slot[i]]
+};
+
+struct Alloc {
+    std::vector<int64_t> shape;
+    at::ScalarType dtype;
+    bool zero;                 // torch.zeros (outputs the kernel reads or writes only in part)
+};
+
+struct Plan {
+    int device = 0;
+    // forward
+    std::vector<std::vector<int64_t>> in_shape;
+    std::vector<at::ScalarType> in_dtype;
+    std::vector<Alloc> fwd_out;
+    Launch fwd;
+    std::vector<int64_t> saved;      // forward-table indices kept for the backward
+    // backward
+    std::vector<Alloc> bwd_out;
+    Launch bwd;
+    std::vector<int64_t> grad_of_input;   // per forward input: backward-table index or -1
+    std::string name;
+};
+
+std::mutex g_mutex;
+std::vector<std::unique_ptr<Plan>> g_plans;   // plans live as long as the process (graphs may outlive ops)
+
+const Plan& plan_at(int64_t id) {
+    std::lock_guard<std::mutex> lock(g_mutex);
+    TORCH_CHECK(id >= 0 && id < static_cast<int64_t>(g_plans.size()), "psad: unknown plan ", id);
+    return *g_plans[id];
+}
+
+at::Tensor allocate(const Alloc& a, int device) {
+    auto opt = at::TensorOptions().dtype(a.dtype).device(at::kCUDA, device);
+    return a.zero ? at::zeros(a.shape, opt) : at::empty(a.shape, opt);
+}
+
+bool aligned(const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 31u) == 0; }
+
+void launch(const Launch& l, const std::vector<at::Tensor>& table, int device) {
+    std::string args = l.args;
+    for (size_t i = 0; i < l.slot.size(); ++i) {
+        void* p = table[l.slot[i]].data_ptr();
+        std::memcpy(&args[8 * i], &p, sizeof(p));
+    }
+    hipStream_t stream = c10::hip::getCurrentHIPStream(device).stream();
+    int rc = psad_launch(l.fn, l.grid, 1, 1, l.block, 1, 1, 0, stream, args.data(), args.size());
+    TORCH_CHECK(rc == 0, "psad: hipModuleLaunchKernel failed: ", psad_error_string(rc), " (code ", rc, ")");
+}
+
+struct StencilFunction : public torch::autograd::Function<StencilFunction> {
+    static torch::autograd::variable_list forward(torch::autograd::AutogradContext* ctx, int64_t id,
+                                                  at::TensorList inputs) {
+        const Plan& p = plan_at(id);
+        std::vector<at::Tensor> table(inputs.begin(), inputs.end());
+        std::vector<at::Tensor> outs;
+        for (const auto& a : p.fwd_out) {
+            outs.push_back(allocate(a, p.device));
+            table.push_back(outs.back());
+        }
+        launch(p.fwd, table, p.device);
+        std::vector<at::Tensor> saved;
+        for (auto i : p.saved) saved.push_back(table[i]);
+        ctx->save_for_backward(saved);
+        ctx->saved_data["plan"] = id;
+        return outs;
+    }
+
+    static torch::autograd::variable_list backward(torch::autograd::AutogradContext* ctx,
+                                                   torch::autograd::variable_list grads) {
+        const Plan& p = plan_at(ctx->saved_data["plan"].toInt());
+        std::vector<at::Tensor> table = ctx->get_saved_variables();
+        for (auto& g : grads) {
+            // undefined gradients arrive as zeros (materialize_grads); the adjoint kernel reads dense,
+            // 32-byte-aligned fields like the ones its plan was made for
+            at::Tensor t = g.is_contiguous() ? g : g.contiguous();
+            if (!aligned(t)) t = t.clone();
+            table.push_back(t);
+        }
+        std::vector<at::Tensor> outs;
+        for (const auto& a : p.bwd_out) {
+            outs.push_back(allocate(a, p.device));
+            table.push_back(outs.back());
+        }
+        launch(p.bwd, table, p.device);
+        torch::autograd::variable_list result(1 + p.grad_of_input.size());   // [plan id] + inputs
+        for (size_t i = 0; i < p.grad_of_input.size(); ++i)
+            if (p.grad_of_input[i] >= 0) result[1 + i] = table[p.grad_of_input[i]];
+        return result;
+    }
+};
+
+Launch make_launch(uint64_t fn, int64_t grid, int64_t block, const py::bytes& args, std::vector<int64_t> slot) {
+    Launch l;
+    l.fn = reinterpret_cast<void*>(fn);
+    l.grid = static_cast<unsigned>(grid);
+    l.block = static_cast<unsigned>(block);
+    l.args = std::string(args);
+    TORCH_CHECK(l.args.size() >= 8 * slot.size(), "psad: argument template shorter than its pointer slots");
+    l.slot = std::move(slot);
+    return l;
+}
+
+std::vector<Alloc> make_allocs(const std::vector<std::vector<int64_t>>& shapes, const std::vector<int64_t>& dtypes,
+                               const std::vector<bool>& zero) {
+    TORCH_CHECK(shapes.size() == dtypes.size() && shapes.size() == zero.size(), "psad: allocation spec mismatch");
+    std::vector<Alloc> r;
+    for (size_t i = 0; i < shapes.size(); ++i)
+        r.push_back(Alloc{shapes[i], static_cast<at::ScalarType>(dtypes[i]), static_cast<bool>(zero[i])});
+    return r;
+}
+
+int64_t register_plan(const std::string& name, int64_t device, std::vector<std::vector<int64_t>> in_shape,
+                      std::vector<int64_t> in_dtype, std::vector<std::vector<int64_t>> fwd_shape,
+                      std::vector<int64_t> fwd_dtype, std::vector<bool> fwd_zero, uint64_t fwd_fn, int64_t fwd_grid,
+                      int64_t fwd_block, py::bytes fwd_args, std::vector<int64_t> fwd_slot,
+                      std::vector<int64_t> saved, std::vector<std::vector<int64_t>> bwd_shape,
+                      std::vector<int64_t> bwd_dtype, std::vector<bool> bwd_zero, uint64_t bwd_fn, int64_t bwd_grid,
+                      int64_t bwd_block, py::bytes bwd_args, std::vector<int64_t> bwd_slot,
+                      std::vector<int64_t> grad_of_input) {
+    auto p = std::make_unique<Plan>();
+    p->name = name;
+    p->device = static_cast<int>(device);
+    TORCH_CHECK(in_shape.size() == in_dtype.size() && grad_of_input.size() == in_shape.size(),
+                "psad: input spec mismatch");
+    p->in_shape = std::move(in_shape);
+    for (auto d : in_dtype) p->in_dtype.push_back(static_cast<at::ScalarType>(d));
+    p->fwd_out = make_allocs(fwd_shape, fwd_dtype, fwd_zero);
+    p->fwd = make_launch(fwd_fn, fwd_grid, fwd_block, fwd_args, std::move(fwd_slot));
+    p->saved = std::move(saved);
+    p->bwd_out = make_allocs(bwd_shape, bwd_dtype, bwd_zero);
+    p->bwd = make_launch(bwd_fn, bwd_grid, bwd_block, bwd_args, std::move(bwd_slot));
+    p->grad_of_input = std::move(grad_of_input);
+    const int64_t n_fwd = static_cast<int64_t>(p->in_shape.size() + p->fwd_out.size());
+    for (auto i : p->fwd.slot) TORCH_CHECK(i >= 0 && i < n_fwd, "psad: forward slot out of range");
+    for (auto i : p->saved) TORCH_CHECK(i >= 0 && i < n_fwd, "psad: saved index out of range");
+    const int64_t n_bwd = static_cast<int64_t>(p->saved.size() + p->fwd_out.size() + p->bwd_out.size());
+    for (auto i : p->bwd.slot) TORCH_CHECK(i >= 0 && i < n_bwd, "psad: backward slot out of range");
+    for (auto i : p->grad_of_input) TORCH_CHECK(i >= -1 && i < n_bwd, "psad: gradient index out of range");
+    std::lock_guard<std::mutex> lock(g_mutex);
+    g_plans.push_back(std::move(p));
+    return static_cast<int64_t>(g_plans.size()) - 1;
+}
+
+// Forward through the plan, or None when the call does not match it.
+py::object apply(int64_t id, const std::vector<at::Tensor>& inputs) {
+    const Plan& p = plan_at(id);
+    if (inputs.size() != p.in_shape.size()) return py::none();
+    for (size_t i = 0; i < inputs.size(); ++i) {
+        const at::Tensor& t = inputs[i];
+        if (!t.defined() || !t.is_cuda() || t.get_device() != p.device || t.scalar_type() != p.in_dtype[i] ||
+            t.sizes() != at::IntArrayRef(p.in_shape[i]) || !t.is_contiguous() || !aligned(t))
+            return py::none();
+    }
+    auto outs = StencilFunction::apply(id, at::TensorList(inputs));
+    return py::cast(outs);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_psad_torch, m) {
+    m.doc() = "native autograd node of the torch_native stencil op (see psad_torch.cpp)";
+    m.def("register_plan", &register_plan);
+    m.def("apply", &apply);
+    m.def("num_plans", []() {
+        std::lock_guard<std::mutex> lock(g_mutex);
+        return static_cast<int64_t>(g_plans.size());
+    });
+}
