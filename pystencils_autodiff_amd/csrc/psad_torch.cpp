@@ -20,8 +20,10 @@
 
 #include <c10/hip/HIPStream.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstring>
+#include <limits>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -61,6 +63,7 @@ struct Plan {
 
 std::mutex g_mutex;
 std::vector<std::unique_ptr<Plan>> g_plans;   // plans live as long as the process (graphs may outlive ops)
+std::atomic<bool> g_poison{false};             // tests: fill uninitialised outputs with NaN
 
 const Plan& plan_at(int64_t id) {
     std::lock_guard<std::mutex> lock(g_mutex);
@@ -70,7 +73,10 @@ const Plan& plan_at(int64_t id) {
 
 at::Tensor allocate(const Alloc& a, int device) {
     auto opt = at::TensorOptions().dtype(a.dtype).device(at::kCUDA, device);
-    return a.zero ? at::zeros(a.shape, opt) : at::empty(a.shape, opt);
+    if (a.zero) return at::zeros(a.shape, opt);
+    at::Tensor t = at::empty(a.shape, opt);
+    if (g_poison.load(std::memory_order_relaxed)) t.fill_(std::numeric_limits<double>::quiet_NaN());
+    return t;
 }
 
 bool aligned(const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 31u) == 0; }
@@ -200,6 +206,8 @@ PYBIND11_MODULE(_psad_torch, m) {
     m.doc() = "native autograd node of the torch_native stencil op (see psad_torch.cpp)";
     m.def("register_plan", &register_plan);
     m.def("apply", &apply);
+    m.def("set_debug_poison", [](bool on) { g_poison.store(on); },
+          "fill the outputs allocated uninitialised with NaN (tests: a kernel that leaves cells unwritten shows)");
     m.def("num_plans", []() {
         std::lock_guard<std::mutex> lock(g_mutex);
         return static_cast<int64_t>(g_plans.size());

@@ -789,24 +789,33 @@ def test_ws_residency_chunking_shapes_vs_oracle(shape):
 @pytest.mark.parametrize('builder,shape', [(W.asym_7pt, (20, 33, 70)), (W.stencil_27pt, (9, 24, 80)),
                                            (W.laplace_5pt, (40, 70)), (W.asym_7pt, (6, 9, 300)),
                                            (W.vector_laplace_7pt, (7, 10, 40, 3))])
-def test_interior_only_border_allocation_gpu(monkeypatch, bmin, builder, shape):
+@pytest.mark.parametrize('native', [False, True])
+def test_interior_only_border_allocation_gpu(monkeypatch, bmin, builder, shape, native):
     """boundary_handling=None: torch.empty outputs with zeroed border slabs (or one memset) on the GPU;
-    uninitialised memory poisoned with NaN."""
+    uninitialised memory poisoned with NaN. ``native``: through the C++ autograd node (which allocates
+    small interior-only outputs with one memset, ``_NativePath``), its uninitialised outputs poisoned too."""
     from pystencils_autodiff_amd.backends import _torch_native as TN
     monkeypatch.setattr(TN, 'BORDER_KERNEL', bmin == 0)
     empty = torch.empty
     monkeypatch.setattr(torch, 'empty', lambda *a, **k: empty(*a, **k).fill_(float('nan')))
-    op, fn = _op(builder(), None)
+    m = TN.native_module()
+    if not native:
+        monkeypatch.setattr(TN, '_native', False)
     g = np.random.default_rng(6)
     dt = np.float16 if builder is W.stencil_27pt else np.float32
     u = g.uniform(-1, 1, shape).astype(dt)
     d = g.uniform(-1, 1, shape).astype(dt)
-    (out,), (du,) = _run(fn, [u], [d])
+    m.set_debug_poison(native)
+    try:
+        op, fn = _op(builder(), None)
+        (out,), (du,) = _run(fn, [u], [d])
+    finally:
+        m.set_debug_poison(False)
     tol = 1e-3 if dt == np.float16 else 1e-6
     assert_close_rel(out, OE.evaluate(op.forward_assignments, {'u': u}, boundary_handling=None)['out'], tol, 'out')
     assert_close_rel(du, OE.evaluate(op.backward_assignments, {'diffout': d}, boundary_handling=None)['diffu'],
                      tol, 'diffu')
-    if bmin == 0:
+    if bmin == 0 and not native:
         v = op.forward_ast_gpu.compile().last_variant[1]
         assert v.XB or not v.ZSUM              # zsum launches store the x ends themselves
 

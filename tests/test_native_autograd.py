@@ -86,7 +86,12 @@ def test_native_node_matches_python_function(case, builder, bh, shape, dtype, ni
     probe = fn_n.apply(*ins)
     g = torch.Generator().manual_seed(1)
     grads = [(torch.rand(o.shape, generator=g, dtype=torch.float64) * 2 - 1).to(dtype).cuda() for o in probe]
-    outs_n, res_n = _run(fn_n, ins, grads)
+    from pystencils_autodiff_amd.backends._torch_native import native_module
+    native_module().set_debug_poison(True)          # cells a kernel leaves unwritten would read NaN
+    try:
+        outs_n, res_n = _run(fn_n, ins, grads)
+    finally:
+        native_module().set_debug_poison(False)
     outs_p, res_p = _run(fn_p, ins, grads)
     assert all(_is_native(o) for o in outs_n), outs_n[0].grad_fn.name()
     assert not any(_is_native(o) for o in outs_p)
@@ -173,7 +178,7 @@ def test_native_constant_input_has_no_gradient():
 def test_native_extension_loads_and_validates_plans():
     from pystencils_autodiff_amd.backends._torch_native import native_module
     m = native_module()
-    assert m is not None and all(hasattr(m, f) for f in ('register_plan', 'apply', 'num_plans'))
+    assert m is not None and all(hasattr(m, f) for f in ('register_plan', 'apply', 'num_plans', 'set_debug_poison'))
     n0 = m.num_plans()
     args = b'\0' * 32
     ok = dict(name='t', device=0, in_shape=[[4, 4]], in_dtype=[6], fwd_shape=[[4, 4]], fwd_dtype=[6],
