@@ -86,7 +86,7 @@ def default_march_config(ir, ve, shape=None, tuning=None):
     for k, v in over.items():
         if k in ('CX', 'WX', 'NR', 'PD', 'WAVES', 'LDS_PAD', 'ZCT', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'DMA_AUX'):
             cfg[k] = int(v)
-        elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'ZSUM', 'PK', 'WS', 'AR'):
+        elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'ZSUM', 'PK', 'WS', 'AR', 'DPP'):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
         elif k == 'VIEW2D':
             cfg[k] = str(v)
