@@ -279,7 +279,7 @@ def test_vector_field_generic_schedule():
 @pytest.mark.parametrize('params', [
     dict(CX=4, NR=8, PD=2, NT_STORE=True), dict(CX=1, NR=1), dict(CX=2, WX=2, NR=3, PD=2),
     dict(CX=2, NR=4, FULL_RING=True), dict(CX=4, NR=8, ZC=5), dict(CX=1, WX=4, NR=2, PD=2, ZC=3),
-    dict(CX=2, NR=3, NW=1, ZC=4), dict(CX=1, WX=2, NW=2, NR=2, PD=2), dict(CX=4, WX=3, NW=3, NR=2, ZC=5),
+    dict(CX=2, NR=3, NW=1, ZC=4), dict(CX=1, WX=2, NW=2, NR=2, PD=2),
 ])
 @pytest.mark.parametrize('builder', [W.diffusion_7pt, W.asym_7pt, W.stencil_27pt])
 def test_march_tunings_vs_oracle(params, builder):
