@@ -276,6 +276,21 @@ class _NativePath:
                 return None
         dev = args[0].device
         scalars = dict(zip(s['scalar_names'], scal))
+        from .hip_kernel import _Plane
+        seeds = {}
+        fake = [0]
+
+        def stand_in(shape, dtype):
+            # a C-contiguous, 256-byte-aligned pointer record: plans depend on shapes, dtypes and alignment
+            # only, so no output- or gradient-sized buffer is allocated to resolve them
+            if dtype not in seeds:
+                seeds[dtype] = torch.empty(1, dtype=dtype, device=dev)
+            strides, acc = [], 1
+            for n in reversed(shape):
+                strides.insert(0, acc)
+                acc *= int(n)
+            fake[0] += 1
+            return _Plane(seeds[dtype], fake[0] << 40, tuple(int(n) for n in shape), tuple(strides))
 
         def alloc_specs(outs, like_shape, kw):
             shapes, dtypes, zero, names = [], [], [], []
@@ -284,7 +299,7 @@ class _NativePath:
                 z = self._kind(alloc, shape)
                 if z is None or str(dtype).replace('torch.', '') not in _SCALAR_TYPE:
                     return None
-                kw[name] = torch.empty(shape, dtype=dtype, device=dev)
+                kw[name] = stand_in(shape, dtype)
                 shapes.append(list(shape))
                 dtypes.append(_SCALAR_TYPE[str(dtype).replace('torch.', '')])
                 zero.append(z)
@@ -326,7 +341,7 @@ class _NativePath:
             bkw[n] = kw[n]
         grad_names = []
         for i, (aname, dtype, fixed, strides, fname) in enumerate(s['grad_specs']):
-            g = torch.empty_like(kw[fname])
+            g = stand_in(kw[fname].shape, kw[fname].dtype)
             grad_names.append(aname if aname is not None else f'\0grad{i}')
             if aname is not None:
                 bkw[aname] = g
