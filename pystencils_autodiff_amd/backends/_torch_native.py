@@ -205,12 +205,15 @@ def native_module():
         if os.environ.get('PSAD_NATIVE_AUTOGRAD', '1') == '0':
             _native = False
         else:
-            import torch  # noqa: F401  (the extension resolves torch's symbols from the loaded libraries)
+            import torch  # (the extension resolves torch's symbols from the loaded libraries)
             try:
                 from .. import _psad_torch
             except ImportError as exc:
-                raise ImportError(f"{exc}: build the extension with `python -m pystencils_autodiff_amd.build`") \
-                    from exc
+                if torch.cuda.is_available():
+                    raise ImportError(f"{exc}: build the extension with `python -m pystencils_autodiff_amd.build`") \
+                        from exc
+                # no GPU here: nothing launches, ops are only built (hiprtc) — the Python Function will do
+                _psad_torch = False
             _native = _psad_torch
     return _native or None
 
