@@ -26,7 +26,9 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=20)
-    p.add_argument('--warmup', type=int, default=3)
+    # 10 warmup steps (28 ms at 1024³) cover the power-management transient a sustained HBM-bound load
+    # first causes (dispatches 0-9 of the kernel trace run up to 4 % slower, profiles/r02g_bench_dispatches.txt)
+    p.add_argument('--warmup', type=int, default=10)
     p.add_argument('--edge', type=int, default=1024, help='cube edge (default: the 1024³ north-star config)')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-seconds', type=float, default=12.0, help='budget of the CPU baseline sample')

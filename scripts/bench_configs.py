@@ -41,6 +41,24 @@ def graph_step(fn, ins, grads, steps):
     return (time.perf_counter() - t0) / (steps * 10)
 
 
+SETTLE_MS = 400.0
+
+
+def settle(step, ms=SETTLE_MS):
+    """Run ``step`` as a continuous load until ``ms`` have passed: a sustained HBM-bound load first drives
+    the chip into a power-management transient (27-point 768³ dispatches rise from ~368 to ~510 us and settle
+    at ~375 us; kernel trace in profiles/r02_power_transient_27pt.txt; 0.08 s of settling still left the
+    27-point op at 0.409 ms, 0.5 s gave 0.377 ms = the kernel, profiles/r02_op_vs_kernel27_settled.log) — timed
+    steps start after it."""
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        for _ in range(8):          # a continuous load (no host sync between steps)
+            step()
+        torch.cuda.synchronize()
+
+
 def run(name, builder, shape, dtype, bh, nin, steps=20, warmup=3, bytes_fwd=None, bytes_bwd=None):
     import torch
 
@@ -53,6 +71,13 @@ def run(name, builder, shape, dtype, bh, nin, steps=20, warmup=3, bytes_fwd=None
     outs = fn.apply(*ins)
     grads = [(torch.rand(o.shape, generator=g, device='cuda') * 2 - 1).to(dtype) for o in outs]
     ev = []
+
+    def one():
+        o_ = fn.apply(*ins)
+        torch.autograd.backward(list(o_), grads)
+        for t in ins:
+            t.grad = None
+    settle(one)
     for i in range(warmup + steps):
         e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
         e0.record()
@@ -138,6 +163,7 @@ def run_slab(name, builder, shape, dtype, full_cells, steps=20, warmup=3):
             k(halos=halos, z_range=((0, 1), (Z - 1, Z)), **kw)
     for _ in range(warmup):
         step()
+    settle(step)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record()
@@ -176,6 +202,11 @@ def run_lbm(name, stencil, shape, dtype, T=10, reps=3, compressible=False):
     gr = step.empty_pdfs()
     gr.copy_(torch.rand(tuple(shape) + (q,), generator=g, device='cuda', dtype=dtype))
     fw, bw = [], []
+
+    def one():
+        Op.apply(x).backward(gr)
+        x.grad = None
+    settle(one)
     for i in range(reps + 1):
         e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
         e0.record()
