@@ -145,16 +145,17 @@ def main():
 
     stream = torch.cuda.current_stream()
     ev = []
+    # every N times the same autograd engine mode: the backward runs in this thread. At N>1 torch's autograd
+    # device thread doubles the host cost of every HIP / RCCL call of a slab sweep
+    # (scripts/probes/slab_step.py ... sweeps: 95 vs 52 us per sweep), which at 8 ranks is what the GPU
+    # would wait on; same work, same autograd graph. N=1 also reports the default engine (below).
+    torch.autograd.set_multithreading_enabled(False)
 
     if distributed:
         # the same drop-in contract over this rank's slab: Function.apply + backward, with the
         # RCCL halo exchange inside the forward and the backward (zslab.py)
         zop = ZSlabOp(op, use_cuda=True)
         fn = zop.autograd_function()
-        # the backward then runs in this thread: torch's autograd device thread doubles the host cost of
-        # every HIP / RCCL call of a slab sweep (scripts/probes/slab_step.py ... sweeps: 95 vs 52 us per
-        # sweep), which at 8 ranks is what the GPU would wait on; same work, same autograd graph
-        torch.autograd.set_multithreading_enabled(False)
         zop.connect(u.device)       # setup, not a step: the RCCL communicator exists before warmup
         zop.warm_exchange(u=u, diffout=d)   # and RCCL's peer connections (set up on first use)
     # setup, not a step: the 1024^3 kernel variants compiled (hiprtc) and loaded, and the output and
@@ -212,6 +213,19 @@ def main():
     bytes_fwd = BYTES_PER_CELL_SWEEP * zl * n * n
     achieved = bytes_fwd / (fwd_ms * 1e-3) / 1e9
     result_extra = {}
+    if not distributed:
+        # the same step with torch's default engine (backward on its device thread; the op's backward is
+        # the C++ node, so no Python runs there)
+        torch.autograd.set_multithreading_enabled(True)
+        for _ in range(3):
+            step(False)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step(False)
+        torch.cuda.synchronize()
+        result_extra['value_default_engine'] = round(cells_total * args.steps / (time.perf_counter() - t1) / 1e6, 1)
+        torch.autograd.set_multithreading_enabled(False)
     if args.kernel_only and not distributed:
         out = torch.empty_like(u)
         du = torch.empty_like(u)
@@ -254,8 +268,8 @@ def main():
                                    f'{n}^3 forward + TF-MAD adjoint per step',
                        'cells': cells_total, 'decomposition': f'z-slab x{world}' if world > 1 else 'single GPU',
                        'path': ('AutoDiffOp.create_tensorflow_op(backend=torch_native) apply+backward' if world == 1
-                                else 'ZSlabOp(AutoDiffOp).autograd_function() apply+backward, RCCL halo exchange, '
-                                     'autograd engine single-threaded (set_multithreading_enabled(False))')},
+                                else 'ZSlabOp(AutoDiffOp).autograd_function() apply+backward, RCCL halo exchange')
+                       + ', autograd engine single-threaded (set_multithreading_enabled(False)) at every N'},
             'fwd_ms': round(fwd_ms, 4),
             'bwd_ms': round(bwd_ms, 4),
             'hbm_roofline_frac_step': round(2 * BYTES_PER_CELL_SWEEP * cells_total / (ms_per_step * 1e-3) / 1e9
