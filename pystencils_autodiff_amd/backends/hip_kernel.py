@@ -56,11 +56,18 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             cfg.update(CX=2, NR=4)                             # box stencil: full ring, LDS/VALU bound
     elif ir.ndim == 3 and zsum_ok:
         cfg.update(ZSUM=True)                                  # 1024³ 7-point: 1.495 ms vs 1.629 ms lite ring
-        if ws_geometry(ir, MarchConfig(VE=ve, **{**cfg, 'WS': True})):
+        ws0 = ws_geometry(ir, MarchConfig(VE=ve, **{**cfg, 'WS': True}))
+        if ws0:
             # star stencils, storage = compute type: LDS-DMA loader wave, 4 planes in flight, 256×16 tiles,
             # 128-plane chunks (one 5-wave workgroup per CU). 1024³ 7-point 1.411 ms vs 1.506 ms register
-            # prefetch (128×32 tiles); one 8-GPU slab 0.182 vs 0.187 ms (profiles/r01_tune_ws_*.log)
-            cfg.update(WS=True, CX=4, NR=4, D=4, ZMAX=128, BLK=256)
+            # prefetch (128×32 tiles); one 8-GPU slab 0.182 vs 0.187 ms (profiles/r01_tune_ws_*.log).
+            # fp16 storage (half-precision ring): 256×32 tiles, the same 16 KB per plane and workgroup:
+            # 7-point fp16 1024³ 0.786 vs 0.889 ms, 768³ 0.372 vs 0.405, 128×1024² slab 0.092 vs 0.098,
+            # 512³ 0.086 vs 0.087 (profiles/r02_tune_f16s_*.log). Chunks down to 8 planes: small domains are
+            # latency bound with few long chunks (128³ 0.0106 vs 0.0197-0.021 ms, 256³ 0.0244 vs 0.032-0.036;
+            # the chunk model keeps 1024³ / 768³ / 512³ / the 8-GPU slabs where they were,
+            # profiles/r02_tune_small_*.log)
+            cfg.update(WS=True, CX=4, NR=8 if ws0['kind'] == 'h' else 4, D=4, ZMIN=8, ZMAX=128, BLK=256)
     if ir.ndim == 2:
         cfg.update(CX=4, WX=1, NR=4, VIEW2D='yx', NT_STORE=False)   # 256×16 tiles (4096²: 0.024 ms, 5.6 TB/s)
     if ir.has_index_dims:

@@ -566,6 +566,31 @@ def test_ws_loader_schedule_vs_oracle(params, shape, case):
             assert_close_rel(t.cpu().numpy(), ref[n], TOL[dt], f'{name} {which} {n} {params}')
 
 
+@pytest.mark.parametrize('shape', [(10, 70, 264), (33, 97, 520), (130, 64, 256)])
+@pytest.mark.parametrize('builder', [lambda: W.asym_7pt(dtype='float16'), lambda: W.diffusion_7pt(dtype='float16')],
+                         ids=['asym_f16', '7pt_f16'])
+def test_ws_fp16_star_default_tiles_vs_oracle(builder, shape):
+    """fp16 star stencils at their defaults: half-precision ring with 256×32 tiles (NR=8) and WS chunks down to
+    8 planes (the chunk model picks them for small domains) — forward and adjoint vs the float64 oracle."""
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
+    rng = np.random.default_rng(sum(shape) + 1)
+    arrays = {f.name: rng.uniform(-1, 1, shape).astype(np.float16) for f in op.forward_input_fields}
+    arrays.update({f.name: rng.uniform(-1, 1, shape).astype(np.float16) for f in op.backward_input_fields
+                   if f.name not in arrays})
+    for which, ac in (('f', op.forward_assignments), ('b', op.backward_assignments)):
+        k = StencilKernel(ac, boundary_handling='zeros', function_name=f'f16s_{which}', target='gpu').compile()
+        ins = {f.name: arrays[f.name] for f in k.ir.fields_read}
+        ref = OE.evaluate(ac, ins, boundary_handling='zeros')
+        outs = {f.name: torch.full(shape, float('nan'), dtype=torch.float16, device='cuda') for f in k.ir.fields_written}
+        k(**{n: torch.from_numpy(a).cuda() for n, a in ins.items()}, **outs)
+        torch.cuda.synchronize()
+        kind, cfg = k.last_variant[0], k.last_variant[1]
+        assert kind == 'march' and cfg.WS and cfg.NR == 8 and cfg.CX == 4, cfg
+        for n, t in outs.items():
+            assert_close_rel(t.cpu().numpy(), ref[n], TOL[np.float16], f'{which} {n} {shape}')
+
+
 @pytest.mark.parametrize('params', [dict(), dict(ZSUM=True, WS=True, D=2, CX=1, NR=2, ZC=3),
                                     dict(ZSUM=True, WS=True, D=4, CX=2, NR=4)])
 def test_ws_halos_and_two_range_launches(params):
