@@ -566,6 +566,40 @@ def test_ws_loader_schedule_vs_oracle(params, shape, case):
             assert_close_rel(t.cpu().numpy(), ref[n], TOL[dt], f'{name} {which} {n} {params}')
 
 
+@pytest.mark.parametrize('case', [
+    ('7pt_f32', W.diffusion_7pt, np.float32, (9, 37, 262), 2), ('7pt_f32', W.diffusion_7pt, np.float32, (6, 20, 261), 1),
+    ('asym_f32', W.asym_7pt, np.float32, (11, 29, 134), 2),
+    ('27pt_f16', W.stencil_27pt, np.float16, (7, 33, 260), 4), ('27pt_f16', W.stencil_27pt, np.float16, (5, 19, 258), 2),
+    ('7pt_f16', lambda: W.diffusion_7pt(dtype='float16'), np.float16, (8, 41, 132), 4),
+    ('7pt_f64', lambda: W.diffusion_7pt(dtype='float64'), np.float64, (6, 17, 65), 1),
+    ('5pt_f32', W.laplace_5pt, np.float32, (130, 262), 2), ('5pt_f32', W.laplace_5pt, np.float32, (67, 129), 'generic')],
+    ids=lambda c: f'{c[0]}_{"x".join(map(str, c[3]))}')
+def test_row_pitch_vector_width_vs_oracle(case):
+    """Rows whose byte pitch is not a multiple of 16: the widest plane-load vector the rows allow (8- / 4-byte
+    register-prefetch loads, else scalar; 2-D scalar rows take the generic schedule) — forward and adjoint
+    vs the float64 oracle, through the drop-in op."""
+    name, builder, dt, shape, expect = case
+    op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
+    rng = np.random.default_rng(sum(shape) + 3)
+    arrays = {f.name: rng.uniform(-1, 1, shape).astype(dt) for f in op.forward_input_fields}
+    arrays.update({f.name: rng.uniform(-1, 1, shape).astype(dt) for f in op.backward_input_fields
+                   if f.name not in arrays})
+    for which, ac, k in (('f', op.forward_assignments, op.forward_ast_gpu.compile()),
+                         ('b', op.backward_assignments, op.backward_ast_gpu.compile())):
+        ins = {f.name: arrays[f.name] for f in k.ir.fields_read}
+        ref = OE.evaluate(ac, ins, boundary_handling='zeros')
+        outs = {f.name: torch.full(shape, float('nan'), dtype=getattr(torch, np.dtype(dt).name), device='cuda')
+                for f in k.ir.fields_written}
+        k(**{n: torch.from_numpy(a).cuda() for n, a in ins.items()}, **outs)
+        torch.cuda.synchronize()
+        if expect == 'generic':
+            assert k.last_variant[0] == 'generic', k.last_variant
+        else:
+            assert k.last_variant[0] == 'march' and k.last_variant[1].VE == expect, k.last_variant
+        for n, t in outs.items():
+            assert_close_rel(t.cpu().numpy(), ref[n], TOL[dt], f'{name} {which} {n} {shape}')
+
+
 @pytest.mark.parametrize('shape', [(10, 70, 264), (33, 97, 520), (130, 64, 256)])
 @pytest.mark.parametrize('builder', [lambda: W.asym_7pt(dtype='float16'), lambda: W.diffusion_7pt(dtype='float16')],
                          ids=['asym_f16', '7pt_f16'])
