@@ -528,19 +528,31 @@ class HipStencilKernel:
         by_name = {f.name: t for f, t in zip(ir.fields, tensors)}
         esize = 16 // ve
 
-        def fits(v):
-            return X % v == 0 and all(by_name[f.name].data_ptr() % (v * esize) == 0 for f in stencil) and \
-                all(h.data_ptr() % (v * esize) == 0 for h in halo_list if h is not None)
-        # widest plane-load vector the rows allow: 16 bytes (and the LDS-DMA loader) when the row pitch is a
-        # multiple of 16 bytes, else 8 / 4 bytes (register-prefetch loads) before scalar ones — X = 262 fp32:
-        # 8-byte loads instead of 4-byte (profiles/r02_misaligned*.log)
-        ve = next(v for v in (ve, ve // 2, ve // 4, 1) if v >= 1 and fits(v))
-        if ve == 1 and ir.ndim == 2 and not halo_list and z_range is None and z_limits is None and \
-                not ir.has_index_dims:
-            # 2-D rows of scalar loads: the one-thread-per-cell schedule streams them faster (4097² 5-point
-            # 0.028 vs 0.046 ms, 4095×4094 0.027 vs 0.043; profiles/r02_misaligned.log)
-            return self._plan_generic(tensors, shape, device)
-        cfg = self._march_cfg(ve, shape)
+        def fits(v, step=None):
+            step = v * esize if step is None else step
+            return (step != v * esize or X % v == 0) and \
+                all(by_name[f.name].data_ptr() % step == 0 for f in stencil) and \
+                all(h.data_ptr() % step == 0 for h in halo_list if h is not None)
+        xm = False
+        if not fits(ve) and esize >= 4 and fits(ve, step=esize) and not ir.has_index_dims and \
+                all(np.dtype(f.dtype.numpy_dtype).itemsize == esize for f in ir.fields):
+            # fp32 / fp64 rows whose pitch is not a multiple of 16 bytes: the LDS-DMA ring still takes 16-byte
+            # pieces (element-aligned) and zero-fills past each row end (XM) — where the WS schedule applies
+            probe = self._march_cfg(ve, shape)
+            xm = bool(probe.WS) and ws_geometry(ir, probe) is not None
+        if xm:
+            cfg = MarchConfig(**{**self._march_cfg(ve, shape).__dict__, 'XM': True})
+        else:
+            # widest plane-load vector the rows allow: 16 bytes (and the LDS-DMA loader) when the row pitch is a
+            # multiple of 16 bytes, else 8 / 4 bytes (register-prefetch loads) before scalar ones — X = 262
+            # fp32: 8-byte loads instead of 4-byte (profiles/r02_misaligned*.log)
+            ve = next(v for v in (ve, ve // 2, ve // 4, 1) if v >= 1 and fits(v))
+            if ve == 1 and ir.ndim == 2 and not halo_list and z_range is None and z_limits is None and \
+                    not ir.has_index_dims:
+                # 2-D rows of scalar loads: the one-thread-per-cell schedule streams them faster (4097² 5-point
+                # 0.028 vs 0.046 ms, 4095×4094 0.027 vs 0.043; profiles/r02_misaligned.log)
+                return self._plan_generic(tensors, shape, device)
+            cfg = self._march_cfg(ve, shape)
         if halo_list and ir.ndim == 2 and cfg.VIEW2D == 'yx':
             cfg = MarchConfig(**{**cfg.__dict__, 'VIEW2D': 'zy'})
         from .hip_emitter import ncomp
