@@ -534,10 +534,11 @@ class HipStencilKernel:
                 all(by_name[f.name].data_ptr() % step == 0 for f in stencil) and \
                 all(h.data_ptr() % step == 0 for h in halo_list if h is not None)
         xm = False
-        if not fits(ve) and esize >= 4 and fits(ve, step=esize) and not ir.has_index_dims and \
+        if not fits(ve) and (X * esize) % 4 == 0 and fits(ve, step=4) and not ir.has_index_dims and \
                 all(np.dtype(f.dtype.numpy_dtype).itemsize == esize for f in ir.fields):
-            # fp32 / fp64 rows whose pitch is not a multiple of 16 bytes: the LDS-DMA ring still takes 16-byte
-            # pieces (element-aligned) and zero-fills past each row end (XM) — where the WS schedule applies
+            # rows whose pitch is not a multiple of 16 bytes but of 4 (fp32 / fp64, fp16 with X even): the LDS-DMA
+            # ring still takes 16-byte pieces (dword-aligned; the image in LDS keeps its layout) and zero-fills
+            # past each row end (XM) — where the WS schedule applies
             probe = self._march_cfg(ve, shape)
             xm = bool(probe.WS) and ws_geometry(ir, probe) is not None
         if xm:

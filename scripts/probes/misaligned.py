@@ -37,6 +37,9 @@ def main():
              ('27pt f16', W.stencil_27pt, torch.float16, (128, 300, 264)),
              ('27pt f16', W.stencil_27pt, torch.float16, (128, 300, 260)),
              ('27pt f16', W.stencil_27pt, torch.float16, (255, 255, 255)),
+             ('27pt f16', W.stencil_27pt, torch.float16, (256, 256, 258)),
+             ('27pt f16', W.stencil_27pt, torch.float16, (768, 768, 766)),
+             ('7pt f16', lambda: W.diffusion_7pt(dtype='float16'), torch.float16, (256, 256, 258)),
              ('5pt f32', W.laplace_5pt, torch.float32, (4096, 4096)),
              ('5pt f32', W.laplace_5pt, torch.float32, (4097, 4097)),
              ('5pt f32', W.laplace_5pt, torch.float32, (4095, 4094))]

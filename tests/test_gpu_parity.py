@@ -571,16 +571,19 @@ def test_ws_loader_schedule_vs_oracle(params, shape, case):
     ('7pt_f32', W.diffusion_7pt, np.float32, (9, 37, 262), 'xm'), ('7pt_f32', W.diffusion_7pt, np.float32, (6, 20, 261), 'xm'),
     ('7pt_f32', W.diffusion_7pt, np.float32, (13, 45, 255), 'xm'), ('asym_f32', W.asym_7pt, np.float32, (11, 29, 134), 'xm'),
     ('27pt_f32', lambda: W.stencil_27pt(dtype='float32'), np.float32, (9, 23, 259), 'xm'),
-    ('27pt_f16', W.stencil_27pt, np.float16, (7, 33, 260), 4), ('27pt_f16', W.stencil_27pt, np.float16, (5, 19, 258), 2),
-    ('7pt_f16', lambda: W.diffusion_7pt(dtype='float16'), np.float16, (8, 41, 132), 4),
+    ('27pt_f16', W.stencil_27pt, np.float16, (7, 33, 260), 'xm'), ('27pt_f16', W.stencil_27pt, np.float16, (5, 19, 258), 'xm'),
+    ('27pt_f16', W.stencil_27pt, np.float16, (6, 17, 131), 1),
+    ('7pt_f16', lambda: W.diffusion_7pt(dtype='float16'), np.float16, (8, 41, 132), 'xm'),
+    ('7pt_f16', lambda: W.diffusion_7pt(dtype='float16'), np.float16, (9, 70, 262), 'xm'),
+    ('7pt_f16', lambda: W.diffusion_7pt(dtype='float16'), np.float16, (5, 23, 133), 1),
     ('7pt_f64', lambda: W.diffusion_7pt(dtype='float64'), np.float64, (6, 17, 65), 'xm'),
     ('5pt_f32', W.laplace_5pt, np.float32, (130, 262), 2), ('5pt_f32', W.laplace_5pt, np.float32, (67, 129), 'generic')],
     ids=lambda c: f'{c[0]}_{"x".join(map(str, c[3]))}')
 def test_row_pitch_vector_width_vs_oracle(case):
-    """Rows whose byte pitch is not a multiple of 16: fp32 / fp64 keep the LDS-DMA ring with element-aligned
-    16-byte pieces and a zero fill past each row end (XM); fp16 takes the widest plane-load vector the rows
-    allow (8- / 4-byte register-prefetch loads), 2-D scalar rows the generic schedule — forward and adjoint
-    vs the float64 oracle, NaN-poisoned outputs, through the drop-in op."""
+    """Rows whose byte pitch is not a multiple of 16: with a dword-aligned pitch (fp32 / fp64, fp16 with X even)
+    the LDS-DMA ring keeps 16-byte pieces and zero-fills past each row end (XM); odd fp16 rows take the widest
+    plane-load vector they allow (register-prefetch loads), 2-D scalar rows the generic schedule — forward and
+    adjoint of the op's kernels vs the float64 oracle, NaN-poisoned outputs."""
     name, builder, dt, shape, expect = case
     op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
     rng = np.random.default_rng(sum(shape) + 3)
@@ -597,7 +600,7 @@ def test_row_pitch_vector_width_vs_oracle(case):
         torch.cuda.synchronize()
         if expect == 'generic':
             assert k.last_variant[0] == 'generic', k.last_variant
-        elif expect == 'xm':            # fp32 / fp64: the LDS-DMA ring at element alignment
+        elif expect == 'xm':            # the LDS-DMA ring with dword-aligned pieces
             assert k.last_variant[0] == 'march' and k.last_variant[1].WS and k.last_variant[1].XM, k.last_variant
         else:
             assert k.last_variant[0] == 'march' and k.last_variant[1].VE == expect, k.last_variant
