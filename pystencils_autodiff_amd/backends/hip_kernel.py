@@ -535,7 +535,8 @@ class HipStencilKernel:
                 all(h.data_ptr() % step == 0 for h in halo_list if h is not None)
         xm = False
         if not fits(ve) and (X * esize) % 4 == 0 and fits(ve, step=4) and not ir.has_index_dims and \
-                all(np.dtype(f.dtype.numpy_dtype).itemsize == esize for f in ir.fields):
+                all(np.dtype(f.dtype.numpy_dtype).itemsize == esize for f in ir.fields) and \
+                int(np.prod(shape[1:])) * esize < 2 ** 31 - 1024:       # (the loader's 32-bit offsets, below)
             # rows whose pitch is not a multiple of 16 bytes but of 4 (fp32 / fp64, fp16 with X even): the LDS-DMA
             # ring still takes 16-byte pieces (dword-aligned; the image in LDS keeps its layout) and zero-fills
             # past each row end (XM) — where the WS schedule applies
@@ -565,6 +566,8 @@ class HipStencilKernel:
         ws = ws_geometry(ir, cfg)
         if ws and int(np.prod(shape[1:])) * cmax * max(ws['esize'], ws.get('ssize', 0)) >= 2 ** 31 - 1024:
             # planes beyond the loader's 32-bit buffer offsets: register-prefetch form of the same schedule
+            # (never with XM: its rows straddle, which only the loader's zero fill repairs)
+            assert not cfg.XM
             cfg = MarchConfig(**{**cfg.__dict__, 'WS': False})
         xlo, xhi = ir.iteration_bounds(shape)[-1]
         if x_border and cfg.ZSUM and (xlo > 0 or xhi < shape[-1]) and \
