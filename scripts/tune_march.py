@@ -54,6 +54,7 @@ def main():
                'laplace5': (W.laplace_5pt, torch.float32),
                'diffusion7_f64': (lambda: W.diffusion_7pt(dtype='float64'), torch.float64),
                'diffusion7_f16': (lambda: W.diffusion_7pt(dtype='float16'), torch.float16),
+               'laplace5_f64': (lambda: W.laplace_5pt(dtype='float64'), torch.float64),
                'stencil27_f32': (lambda: W.stencil_27pt(dtype='float32'), torch.float32),
                'veclap3': (W.vector_laplace_7pt, torch.float32)}[a.workload]
     op = AutoDiffOp(builder[0](), boundary_handling='zeros')
