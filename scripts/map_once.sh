@@ -1,4 +1,5 @@
 set -u
+# (record: the MAP / XR knobs this script sets were measured and removed; see DESIGN.md §4, profiles/r02_xr_bench_ab.txt)
 # Workgroup -> tile mapping: XCD-aware remap with x-fastest tiles (default) vs no remap vs y-fastest tiles.
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp PSAD_CACHE_DIR=/tmp/psad_cache
 python -m pystencils_autodiff_amd.build > /dev/null || exit 3
