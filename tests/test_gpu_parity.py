@@ -664,6 +664,44 @@ def test_ws_halos_and_two_range_launches(params):
     assert_close_rel(full.cpu().numpy(), ref, 1e-6)
 
 
+@pytest.mark.parametrize('dtype,X', [(torch.float32, 134), (torch.float32, 133), (torch.float64, 67),
+                                     (torch.float16, 262)])
+@pytest.mark.parametrize('bh', ['zeros', None])
+def test_xm_rows_halos_two_range_and_interior_only(dtype, X, bh):
+    """Rows whose pitch is not a multiple of 16 bytes on the LDS-DMA ring (XM): z-slab launch pattern (halo
+    planes read in place, interior planes then both faces in one two-range launch) == one full-domain launch,
+    bitwise; ``None`` boundary handling (interior-only writes) too; vs the float64 oracle."""
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    dts = {torch.float32: 'float32', torch.float64: 'float64', torch.float16: 'float16'}[dtype]
+    op = pa.AutoDiffOp(W.asym_7pt(dtype=dts), boundary_handling=bh)
+    k = StencilKernel(op.forward_assignments, boundary_handling=bh, function_name='xmh', target='gpu').compile()
+    g = torch.Generator().manual_seed(X)
+    u = torch.rand((30, 21, X), generator=g).to(dtype).cuda()
+    full = torch.zeros_like(u)
+    k(u=u, out=full)
+    assert k.last_variant[1].WS and k.last_variant[1].XM, k.last_variant
+    kz = None if bh == 'zeros' else (1, 29)
+    parts = [(0, 11), (11, 19), (19, 30)]
+    outs = []
+    from pystencils_autodiff_amd.zslab import ZSlabOp
+    for a, b in parts:
+        sl = u[a:b].contiguous()
+        out = torch.zeros_like(sl)
+        lo = u[a - 1:a].contiguous() if a > 0 else None
+        hi = u[b:b + 1].contiguous() if b < 30 else None
+        zl = None if kz is None else (max(0, kz[0] - a), min(b - a, kz[1] - a))
+        inner, faces = ZSlabOp._launches(b - a, 1, zl or (0, b - a))     # the z-slab sweep's launch split
+        if inner:
+            k(u=sl, out=out, z_range=inner, z_limits=zl)
+        ZSlabOp._launch_faces(k, {'u': (lo, hi)}, faces, zl, {'u': sl, 'out': out})
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(outs), full)
+    ref = OE.evaluate(op.forward_assignments, {'u': u.double().cpu().numpy()}, boundary_handling=bh)['out']
+    tol = TOL[{torch.float32: np.float32, torch.float64: np.float64, torch.float16: np.float16}[dtype]]
+    assert_close_rel(full.double().cpu().numpy(), ref, tol)
+
+
 @pytest.mark.parametrize('radius', (1, 2, 3))
 @pytest.mark.parametrize('ndim', (2, 3))
 def test_fixed_constant_bh_one_sided_box(radius, ndim):
