@@ -6,7 +6,10 @@ One step = one forward sweep + one TF-MAD adjoint sweep of the 7-point diffusion
 ``out.backward``), inputs resident in HBM. N>1: the 1024³ domain is split into z-slabs
 (``zslab.py``) with an RCCL halo exchange per sweep — strong scaling, total work fixed.
 
-Run: ``python bench.py [--gpus N] [--steps K] [--warmup W]``; N>1 via
+``--workload stencil27_f16`` runs BASELINE config 5 instead (27-point anisotropic stencil, fp16 storage,
+768³ by default) through the same path, at 1 GPU or as 8 z-slabs; the default stays the headline.
+
+Run: ``python bench.py [--gpus N] [--steps K] [--warmup W] [--workload W] [--edge E]``; N>1 via
 ``torch.distributed.run --nproc-per-node N``.
 """
 import argparse
@@ -19,7 +22,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md), GB/s
-BYTES_PER_CELL_SWEEP = 8       # fp32 7-point: read u once + write out once
+
+# the BASELINE configs bench.py can run: builder, storage dtype, default cube edge, algorithmic bytes per cell
+# and sweep (distinct fields read + written), labels
+WORKLOADS = {
+    'diffusion7_f32': dict(builder='diffusion_7pt', dtype='float32', edge=1024, bytes=8, label='3D 7-point fp32',
+                           dtype_tag='f32',
+                           desc='3D 7-point diffusion out=u+0.1*(sum6 u[nb]-6u), boundary zeros, fp32'),
+    'stencil27_f16': dict(builder='stencil_27pt', dtype='float16', edge=768, bytes=4, label='3D 27-point fp16',
+                          dtype_tag='f16 storage, f32 arithmetic',
+                          desc='3D 27-point anisotropic stencil (27 distinct weights), boundary zeros, fp16 storage '
+                               'with fp32 arithmetic (BASELINE config 5)'),
+}
 
 
 def parse():
@@ -29,7 +43,10 @@ def parse():
     # 10 warmup steps (28 ms at 1024³) cover the power-management transient a sustained HBM-bound load
     # first causes (dispatches 0-9 of the kernel trace run up to 4 % slower, profiles/r02g_bench_dispatches.txt)
     p.add_argument('--warmup', type=int, default=10)
-    p.add_argument('--edge', type=int, default=1024, help='cube edge (default: the 1024³ north-star config)')
+    p.add_argument('--workload', default='diffusion7_f32', choices=sorted(WORKLOADS),
+                   help='diffusion7_f32 (default, the headline) or stencil27_f16 (BASELINE config 5)')
+    p.add_argument('--edge', type=int, default=None,
+                   help='cube edge (default: the workload\'s BASELINE size, 1024 / 768)')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-seconds', type=float, default=12.0, help='budget of the CPU baseline sample')
     p.add_argument('--kernel-only', action='store_true', help='also time the raw kernel loop')
@@ -48,7 +65,7 @@ def cpu_model():
     return platform.processor() or 'unknown'
 
 
-def cpu_baseline(budget_s):
+def cpu_baseline(budget_s, workload='diffusion7_f32', edge=1024):
     """The oracle's C restatement of the reference CPU kernel on bounded slabs of the workload: first with
     ONE thread — the reference's default (``create_kernel`` without ``cpu_openmp``, ``_autodiff.py:487-489``),
     reported as ``value`` — then with OpenMP over this process's cores (``cpu_openmp=True``)."""
@@ -58,36 +75,48 @@ def cpu_baseline(budget_s):
     lib = cref.load(build_dir=build_dir, march='native')
     affinity = len(os.sched_getaffinity(0))
     mt = int(os.environ.get('OMP_NUM_THREADS', '0')) or affinity
+    w27 = workload == 'stencil27_f16'
+    if w27:
+        from pystencils_autodiff_amd import workloads as W
+        wf = np.asarray(W.WEIGHTS_27PT, dtype=np.float32)
+        wb = wf[::-1].copy()                     # the TF-MAD adjoint: the same stencil with flipped offsets
+    dt = np.float16 if w27 else np.float32
 
     def run(threads, planes, budget):
         got = lib.set_threads(threads)
-        shape = (planes, 1024, 1024)
+        shape = (planes, edge, edge)
         rng = np.random.default_rng(0)
-        u = rng.uniform(0, 1, shape).astype(np.float32)
-        d = rng.uniform(-1, 1, shape).astype(np.float32)
-        out, du = np.empty_like(u), np.empty_like(u)
-        lib.diffusion7_f32(u, 0.1, out)          # warm-up (first touch, thread pool)
+        u = rng.uniform(0, 1, shape).astype(dt)
+        d = rng.uniform(-1, 1, shape).astype(dt)
+        if w27:
+            sweeps = (lambda: lib.stencil27_f16(u, wf), lambda: lib.stencil27_f16(d, wb))
+        else:
+            out, du = np.empty_like(u), np.empty_like(u)
+            sweeps = (lambda: lib.diffusion7_f32(u, 0.1, out), lambda: lib.diffusion7_f32(d, 0.1, du))
+        sweeps[0]()                              # warm-up (first touch, thread pool)
         reps, t0 = 0, time.perf_counter()
         while True:
-            lib.diffusion7_f32(u, 0.1, out)      # forward sweep
-            lib.diffusion7_f32(d, 0.1, du)       # adjoint sweep (same symmetric stencil on diffout)
+            sweeps[0]()                          # forward sweep
+            sweeps[1]()                          # adjoint sweep
             reps += 1
             el = time.perf_counter() - t0
             if el >= budget or reps >= 5000:
                 break
         return got, reps, el, round(reps * u.size / el / 1e6, 2)
 
-    t1, reps1, el1, v1 = run(1, 16, budget_s / 2)
-    tm, repsm, elm, vm = run(mt, 64, budget_s / 2)
+    p1, pm = (16, 64) if not w27 else (16, 48)
+    t1, reps1, el1, v1 = run(1, p1, budget_s / 2)
+    tm, repsm, elm, vm = run(mt, pm, budget_s / 2)
     model = cpu_model()
+    kind = 'fp16 27-point (F16C conversions, fp32 arithmetic)' if w27 else 'fp32 7-point'
     return {'value': v1, 'unit': 'Mcells/s', 'cores': t1, 'kind': 'port',
-            'sample': f'{reps1} fwd+bwd sweeps of a 16x1024x1024 fp32 slab of the 1024^3 workload in {el1:.1f} s, '
-                      f'1 thread (the reference default: no cpu_openmp); oracle/stencil_ref.c (pystencils CPU '
-                      f'loop nest restated), gcc -O3 -march=native -fopenmp; host CPU {model}',
+            'sample': f'{reps1} fwd+bwd sweeps of a {p1}x{edge}x{edge} {kind} slab of the {edge}^3 workload in '
+                      f'{el1:.1f} s, 1 thread (the reference default: no cpu_openmp); oracle/stencil_ref.c '
+                      f'(pystencils CPU loop nest restated), gcc -O3 -march=native -fopenmp; host CPU {model}',
             'threads_1': {'value': v1, 'threads': t1, 'sweeps': reps1, 'seconds': round(el1, 2),
-                          'sample': '16x1024x1024 fp32'},
+                          'sample': f'{p1}x{edge}x{edge}'},
             'threads_mt': {'value': vm, 'threads': tm, 'sweeps': repsm, 'seconds': round(elm, 2),
-                           'sample': '64x1024x1024 fp32', 'cpu_openmp': True},
+                           'sample': f'{pm}x{edge}x{edge}', 'cpu_openmp': True},
             'cpu_model': model, 'cpus_available': affinity}
 
 
@@ -129,18 +158,21 @@ def main():
     from pystencils_autodiff_amd import workloads as W
     from pystencils_autodiff_amd.zslab import ZSlabOp, slab_bounds
 
-    n = args.edge
+    wl = WORKLOADS[args.workload]
+    n = args.edge or wl['edge']
+    tdtype = getattr(torch, wl['dtype'])
+    bytes_per_cell = wl['bytes']
     lo, hi = slab_bounds(n, world, rank)
     zl = hi - lo
-    op = pa.AutoDiffOp(W.diffusion_7pt(), boundary_handling='zeros')
+    op = pa.AutoDiffOp(getattr(W, wl['builder'])(), boundary_handling='zeros')
     fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
     fwd_k = op.forward_ast_gpu.compile()
     bwd_k = op.backward_ast_gpu.compile()
 
     g = torch.Generator(device='cuda').manual_seed(0 + rank)
-    u = torch.rand((zl, n, n), generator=g, device='cuda', dtype=torch.float32)
+    u = torch.rand((zl, n, n), generator=g, device='cuda', dtype=torch.float32).to(tdtype)
     g1 = torch.Generator(device='cuda').manual_seed(1000 + rank)
-    d = torch.rand((zl, n, n), generator=g1, device='cuda', dtype=torch.float32) * 2 - 1
+    d = (torch.rand((zl, n, n), generator=g1, device='cuda', dtype=torch.float32) * 2 - 1).to(tdtype)
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
@@ -210,7 +242,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     # kernel-level: algorithmic bytes of one forward launch over this rank's slab / its event time
-    bytes_fwd = BYTES_PER_CELL_SWEEP * zl * n * n
+    bytes_fwd = bytes_per_cell * zl * n * n
     achieved = bytes_fwd / (fwd_ms * 1e-3) / 1e9
     result_extra = {}
     if not distributed:
@@ -241,18 +273,22 @@ def main():
         kt = time.perf_counter() - t1
         result_extra['kernel_only_mcells_s'] = round(cells_total * args.steps / kt / 1e6, 1)
 
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        # after the timed loop, at every N (north_star: the CPU path "in the same run"); the other ranks
+        # wait at the barrier below
+        try:
+            cpu = cpu_baseline(args.cpu_seconds, args.workload, n)
+        except Exception as exc:  # noqa: BLE001 - report, don't fail the GPU bench
+            cpu = {'value': None, 'unit': 'Mcells/s', 'cores': None, 'kind': 'port', 'sample': f'failed: {exc}'}
+    if distributed:
+        dist.barrier()
     if rank == 0:
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            try:
-                cpu = cpu_baseline(args.cpu_seconds)
-            except Exception as exc:  # noqa: BLE001 - report, don't fail the GPU bench
-                cpu = {'value': None, 'unit': 'Mcells/s', 'cores': None, 'kind': 'port', 'sample': f'failed: {exc}'}
-        workload = f'diffusion7_f32_{n}^3'
+        workload = f'{args.workload}_{n}^3'
         kname = fwd_k.source(fwd_k.last_variant)[1] if fwd_k.last_variant else fwd_k.name
         traffic, traffic_src = load_traffic(workload, kname)
         res = {
-            'metric': f'Mcells/s forward+backward, 3D 7-point fp32 {n}^3',
+            'metric': f'Mcells/s forward+backward, {wl["label"]} {n}^3',
             'value': round(value, 1),
             'unit': 'Mcells/s',
             'n_gpus': world,
@@ -262,17 +298,17 @@ def main():
             'higher_is_better': True,
             'scaling': 'strong',
             'vs_baseline': None,
-            'dtype': 'f32',
+            'dtype': wl['dtype_tag'],
             'data': 'synthetic: u~U(0,1), diffout~U(-1,1) (torch generator seeds 0/1000+rank)',
-            'config': {'workload': f'3D 7-point diffusion out=u+0.1*(sum6 u[nb]-6u), boundary zeros, fp32, '
-                                   f'{n}^3 forward + TF-MAD adjoint per step',
+            'config': {'workload': f'{wl["desc"]}, {n}^3 forward + TF-MAD adjoint per step',
+                       'name': args.workload,
                        'cells': cells_total, 'decomposition': f'z-slab x{world}' if world > 1 else 'single GPU',
                        'path': ('AutoDiffOp.create_tensorflow_op(backend=torch_native) apply+backward' if world == 1
                                 else 'ZSlabOp(AutoDiffOp).autograd_function() apply+backward, RCCL halo exchange')
                        + ', autograd engine single-threaded (set_multithreading_enabled(False)) at every N'},
             'fwd_ms': round(fwd_ms, 4),
             'bwd_ms': round(bwd_ms, 4),
-            'hbm_roofline_frac_step': round(2 * BYTES_PER_CELL_SWEEP * cells_total / (ms_per_step * 1e-3) / 1e9
+            'hbm_roofline_frac_step': round(2 * bytes_per_cell * cells_total / (ms_per_step * 1e-3) / 1e9
                                             / (HBM_PEAK_GBS * world), 4),
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,

@@ -226,7 +226,8 @@ class _NativePath:
     """The forward + adjoint launches of one op as a C++ ``torch::autograd::Function`` (``_psad_torch``):
     the backward then runs on torch's autograd device thread without Python (no GIL hand-off), the forward
     without the Python Function's bookkeeping. One native plan per input signature (input shapes, dtypes,
-    device, scalar values), resolved by the kernels' own ``prepare`` on the first call. Ops the plan
+    device), resolved by the kernels' own ``prepare`` on the first call; the scalar parameters are patched into
+    the argument buffers per call (their byte offsets are part of the plan). Ops the plan
     cannot express take the Python Function: fzyx fields, outputs with a zero border larger than
     ``BORDER_ZERO_MIN`` (the border kernel beats a memset there), no backward kernel, inputs that are
     not contiguous 32-byte-aligned device tensors."""
@@ -258,14 +259,22 @@ class _NativePath:
         except KeyError:
             return None
         a0 = args[0]
-        key = (scal, tuple(a0.shape), a0.dtype, a0.device)
+        if not isinstance(a0, torch.Tensor):
+            return None
+        key = (tuple(a0.shape), a0.dtype, a0.device)
         pid = self.plans.get(key)
         if pid is None:
             pid = self._build(args, scal)
-            if pid is None:
-                return None
-            self.plans[key] = pid
-        outs = native_module().apply(pid, list(args))
+            # a signature the plan cannot express is remembered as such (-1): later calls go straight to the
+            # Python Function instead of resolving stand-in launches again
+            self.plans[key] = -1 if pid is None else pid
+        if pid is None or pid < 0:
+            return None
+        try:
+            scal = [float(v) for v in scal]
+        except (TypeError, ValueError):
+            return None
+        outs = native_module().apply(pid, list(args), scal)
         return None if outs is None else tuple(outs)
 
     def _build(self, args, scal):
@@ -319,7 +328,12 @@ class _NativePath:
                 return None
             if list(struct.unpack_from(f'<{len(names)}Q', packed)) != [kw[n].data_ptr() for n in names]:
                 return None                     # pointer slots are not the leading 8-byte arguments
-            return int(fn), int(grid), int(block), bytes(packed), [table.index(n) for n in names]
+            snames = [sc.name for sc in call.ir.scalars]
+            slots = [[off, int(f64), s['scalar_names'].index(n)]
+                     for (off, f64), n in zip(call.last_plan.scalar_slots(len(snames)), snames)]
+            if len(slots) != len(snames):
+                return None
+            return int(fn), int(grid), int(block), bytes(packed), [table.index(n) for n in names], slots
 
         fwd_call, bwd_call = s['fwd_call'], s['bwd_call']
         if getattr(fwd_call, '_soa', None) or getattr(bwd_call, '_soa', None):
@@ -363,8 +377,8 @@ class _NativePath:
         return native_module().register_plan(
             s['op_name'], dev.index, [list(a.shape) for a in args],
             [_SCALAR_TYPE[str(a.dtype).replace('torch.', '')] for a in args],
-            fo[0], fo[1], fo[2], *fl[:4], fl[4], [fwd_table.index(n) for n in saved_names],
-            bo[0], bo[1], bo[2], *bl[:4], bl[4], grad_of_input)
+            fo[0], fo[1], fo[2], *fl[:4], fl[4], fl[5], [fwd_table.index(n) for n in saved_names],
+            bo[0], bo[1], bo[2], *bl[:4], bl[4], bl[5], grad_of_input, len(s['scalar_names']))
 
 
 def create_autograd_function(autodiff_obj, use_cuda, op_name=None):

@@ -156,6 +156,7 @@ class HipStencilKernel:
         self._specs = None
         self._ref_index = [f.name for f in self.ir.fields].index(self.ir.fields_written[0].name)
         self.last_variant = None
+        self.last_plan = None
 
     # -- sources --------------------------------------------------------------------------------
     def schedule(self):
@@ -311,7 +312,10 @@ class HipStencilKernel:
         hptrs = [h.data_ptr() if h is not None else 0 for h in halo_list]
         contiguous = all(t.is_contiguous() for t in tensors)
         strides = None if contiguous else tuple(tuple(t.stride()) for t in tensors)
-        align = tuple(p % 32 == 0 for p in ptrs + hptrs)
+        # the alignment CLASS of every pointer (trailing zero bits, capped at 32 bytes): the plan's load path
+        # depends on 16-, 8-, 4- and 2-byte alignment (LDS-DMA ring, narrower vectors, XM rows), so a plan built
+        # for one class must not serve a pointer of another
+        align = tuple(_align_class(p) for p in ptrs + hptrs)
         key = (force_schedule, bool(x_border), shape, strides, align,
                tuple(h.numel() if h is not None else -1 for h in halo_list), _zkey(z_range),
                tuple(z_limits) if z_limits is not None else None, device)
@@ -324,6 +328,7 @@ class HipStencilKernel:
                                    z_limits)
             self._plans[key] = plan
         self.last_variant = plan.variant
+        self.last_plan = plan
         if plan.grid == 0:
             return plan.fn, 0, plan.block, b'', plan.xb, device
         return plan.fn, plan.grid, plan.block, plan.pack(ptrs, hptrs, scalars), plan.xb, device
@@ -639,6 +644,11 @@ class _Plane:
         return True
 
 
+def _align_class(p):
+    """log2 of the largest power of two (≤ 32) dividing the address ``p`` (0 counts as 32-byte aligned)."""
+    return min((p & -p).bit_length() - 1, 5) if p else 5
+
+
 def _is_pair(z_range):
     return len(z_range) == 2 and all(isinstance(r, (tuple, list)) for r in z_range)
 
@@ -663,16 +673,23 @@ class _Plan:
         self.block = block
         self.xb = xb                     # the launch also zeroes x outside the iteration bounds
         fmt, off = '<', 0
+        self.kinds, self.offsets = list(kinds), []       # byte offset of every argument in the packed buffer
         for k in kinds:
             c, size = self._CODES[k]
             pad = (-off) % size
             fmt += 'x' * pad + c
+            self.offsets.append(off + pad)
             off += pad + size
         fmt += 'x' * ((-off) % 8)
         self.struct = struct.Struct(fmt)
         self.n_ptr = n_ptr
         self.n_halo = n_halo
         self.statics = list(statics)
+
+    def scalar_slots(self, n):
+        """``(byte offset, is f64)`` of the last ``n`` arguments (the kernel's scalar parameters)."""
+        return [(o, k == 'f64') for o, k in zip(self.offsets[len(self.offsets) - n:], self.kinds[len(self.kinds) - n:])] \
+            if n else []
 
     def pack(self, ptrs, hptrs, scalars):
         return self.struct.pack(*ptrs, *(hptrs if hptrs else [0] * self.n_halo), *self.statics, *scalars)

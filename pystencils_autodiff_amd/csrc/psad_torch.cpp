@@ -9,15 +9,17 @@
 // template and launches through the C ABI (psad_launch, include/psad.h) on the current stream; the
 // backward does the same for the adjoint kernel on the engine's thread without touching Python.
 //
-// A plan (both launches, resolved once by the Python op for one input signature — shapes, dtypes, scalar
-// values — by HipStencilKernel.prepare) holds: the function handle, grid and block, the packed argument
-// template whose first n_ptr 8-byte slots are the field pointers (hip_kernel._Plan.pack), and for each
-// slot the index of the tensor in the call's table. Forward table: inputs ++ outputs; backward table:
+// A plan (both launches, resolved once by the Python op for one input signature — shapes, dtypes, device —
+// by HipStencilKernel.prepare) holds: the function handle, grid and block, the packed argument template
+// whose first n_ptr 8-byte slots are the field pointers (hip_kernel._Plan.pack), for each slot the index of
+// the tensor in the call's table, and the byte offsets of the scalar parameters, patched per call from the
+// op's class_kwargs (a coefficient that changes every step reuses the plan). Forward table: inputs ++ outputs; backward table:
 // saved forward tensors ++ output gradients ++ adjoint outputs. apply() returns None when a call does not
 // match its plan (device, dtype, shape, contiguity, 32-byte alignment): the Python op then takes the
 // general path.
 #include <torch/extension.h>
 
+#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 
 #include <atomic>
@@ -38,6 +40,7 @@ struct Launch {
     unsigned grid = 0, block = 0;
     std::string args;          // packed template; pointer i at byte 8*i
     std::vector<int64_t> slot; // pointer i <- table[slot[i]]
+    std::vector<int64_t> s_off, s_f64, s_idx;   // scalar j at byte s_off[j] (f64 or f32) <- scalars[s_idx[j]]
 };
 
 struct Alloc {
@@ -58,6 +61,7 @@ struct Plan {
     std::vector<Alloc> bwd_out;
     Launch bwd;
     std::vector<int64_t> grad_of_input;   // per forward input: backward-table index or -1
+    int64_t n_scalars = 0;
     std::string name;
 };
 
@@ -81,12 +85,24 @@ at::Tensor allocate(const Alloc& a, int device) {
 
 bool aligned(const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 31u) == 0; }
 
-void launch(const Launch& l, const std::vector<at::Tensor>& table, int device) {
+void launch(const Launch& l, const std::vector<at::Tensor>& table, const std::vector<double>& scalars,
+            int device) {
     std::string args = l.args;
     for (size_t i = 0; i < l.slot.size(); ++i) {
         void* p = table[l.slot[i]].data_ptr();
         std::memcpy(&args[8 * i], &p, sizeof(p));
     }
+    for (size_t j = 0; j < l.s_off.size(); ++j) {
+        const double v = scalars[l.s_idx[j]];
+        if (l.s_f64[j]) {
+            std::memcpy(&args[l.s_off[j]], &v, sizeof(v));
+        } else {
+            const float f = static_cast<float>(v);
+            std::memcpy(&args[l.s_off[j]], &f, sizeof(f));
+        }
+    }
+    // the function handle belongs to the module loaded on the plan's device: launch with it current
+    c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
     hipStream_t stream = c10::hip::getCurrentHIPStream(device).stream();
     int rc = psad_launch(l.fn, l.grid, 1, 1, l.block, 1, 1, 0, stream, args.data(), args.size());
     TORCH_CHECK(rc == 0, "psad: hipModuleLaunchKernel failed: ", psad_error_string(rc), " (code ", rc, ")");
@@ -94,7 +110,7 @@ void launch(const Launch& l, const std::vector<at::Tensor>& table, int device) {
 
 struct StencilFunction : public torch::autograd::Function<StencilFunction> {
     static torch::autograd::variable_list forward(torch::autograd::AutogradContext* ctx, int64_t id,
-                                                  at::TensorList inputs) {
+                                                  at::TensorList inputs, std::vector<double> scalars) {
         const Plan& p = plan_at(id);
         std::vector<at::Tensor> table(inputs.begin(), inputs.end());
         std::vector<at::Tensor> outs;
@@ -102,11 +118,12 @@ struct StencilFunction : public torch::autograd::Function<StencilFunction> {
             outs.push_back(allocate(a, p.device));
             table.push_back(outs.back());
         }
-        launch(p.fwd, table, p.device);
+        launch(p.fwd, table, scalars, p.device);
         std::vector<at::Tensor> saved;
         for (auto i : p.saved) saved.push_back(table[i]);
         ctx->save_for_backward(saved);
         ctx->saved_data["plan"] = id;
+        ctx->saved_data["scalars"] = scalars;          // the forward's values, as the Python op's ctx.scalars
         return outs;
     }
 
@@ -126,15 +143,17 @@ struct StencilFunction : public torch::autograd::Function<StencilFunction> {
             outs.push_back(allocate(a, p.device));
             table.push_back(outs.back());
         }
-        launch(p.bwd, table, p.device);
-        torch::autograd::variable_list result(1 + p.grad_of_input.size());   // [plan id] + inputs
+        launch(p.bwd, table, ctx->saved_data["scalars"].toDoubleVector(), p.device);
+        // one slot per forward argument, in order: plan id, each input of the list, the scalars
+        torch::autograd::variable_list result(2 + p.grad_of_input.size());
         for (size_t i = 0; i < p.grad_of_input.size(); ++i)
             if (p.grad_of_input[i] >= 0) result[1 + i] = table[p.grad_of_input[i]];
         return result;
     }
 };
 
-Launch make_launch(uint64_t fn, int64_t grid, int64_t block, const py::bytes& args, std::vector<int64_t> slot) {
+Launch make_launch(uint64_t fn, int64_t grid, int64_t block, const py::bytes& args, std::vector<int64_t> slot,
+                   std::vector<std::vector<int64_t>> scal, int64_t n_scalars) {
     Launch l;
     l.fn = reinterpret_cast<void*>(fn);
     l.grid = static_cast<unsigned>(grid);
@@ -142,6 +161,16 @@ Launch make_launch(uint64_t fn, int64_t grid, int64_t block, const py::bytes& ar
     l.args = std::string(args);
     TORCH_CHECK(l.args.size() >= 8 * slot.size(), "psad: argument template shorter than its pointer slots");
     l.slot = std::move(slot);
+    for (const auto& sc : scal) {       // (byte offset, is f64, index into the call's scalars)
+        TORCH_CHECK(sc.size() == 3, "psad: scalar slot spec is (offset, is_f64, index)");
+        const int64_t width = sc[1] ? 8 : 4;
+        TORCH_CHECK(sc[0] >= static_cast<int64_t>(8 * l.slot.size()) &&
+                        sc[0] + width <= static_cast<int64_t>(l.args.size()) && sc[2] >= 0 && sc[2] < n_scalars,
+                    "psad: scalar slot out of range");
+        l.s_off.push_back(sc[0]);
+        l.s_f64.push_back(sc[1]);
+        l.s_idx.push_back(sc[2]);
+    }
     return l;
 }
 
@@ -158,10 +187,11 @@ int64_t register_plan(const std::string& name, int64_t device, std::vector<std::
                       std::vector<int64_t> in_dtype, std::vector<std::vector<int64_t>> fwd_shape,
                       std::vector<int64_t> fwd_dtype, std::vector<bool> fwd_zero, uint64_t fwd_fn, int64_t fwd_grid,
                       int64_t fwd_block, py::bytes fwd_args, std::vector<int64_t> fwd_slot,
-                      std::vector<int64_t> saved, std::vector<std::vector<int64_t>> bwd_shape,
+                      std::vector<std::vector<int64_t>> fwd_scal, std::vector<int64_t> saved, std::vector<std::vector<int64_t>> bwd_shape,
                       std::vector<int64_t> bwd_dtype, std::vector<bool> bwd_zero, uint64_t bwd_fn, int64_t bwd_grid,
                       int64_t bwd_block, py::bytes bwd_args, std::vector<int64_t> bwd_slot,
-                      std::vector<int64_t> grad_of_input) {
+                      std::vector<std::vector<int64_t>> bwd_scal, std::vector<int64_t> grad_of_input,
+                      int64_t n_scalars) {
     auto p = std::make_unique<Plan>();
     p->name = name;
     p->device = static_cast<int>(device);
@@ -170,10 +200,11 @@ int64_t register_plan(const std::string& name, int64_t device, std::vector<std::
     p->in_shape = std::move(in_shape);
     for (auto d : in_dtype) p->in_dtype.push_back(static_cast<at::ScalarType>(d));
     p->fwd_out = make_allocs(fwd_shape, fwd_dtype, fwd_zero);
-    p->fwd = make_launch(fwd_fn, fwd_grid, fwd_block, fwd_args, std::move(fwd_slot));
+    p->n_scalars = n_scalars;
+    p->fwd = make_launch(fwd_fn, fwd_grid, fwd_block, fwd_args, std::move(fwd_slot), fwd_scal, n_scalars);
     p->saved = std::move(saved);
     p->bwd_out = make_allocs(bwd_shape, bwd_dtype, bwd_zero);
-    p->bwd = make_launch(bwd_fn, bwd_grid, bwd_block, bwd_args, std::move(bwd_slot));
+    p->bwd = make_launch(bwd_fn, bwd_grid, bwd_block, bwd_args, std::move(bwd_slot), bwd_scal, n_scalars);
     p->grad_of_input = std::move(grad_of_input);
     const int64_t n_fwd = static_cast<int64_t>(p->in_shape.size() + p->fwd_out.size());
     for (auto i : p->fwd.slot) TORCH_CHECK(i >= 0 && i < n_fwd, "psad: forward slot out of range");
@@ -187,16 +218,16 @@ int64_t register_plan(const std::string& name, int64_t device, std::vector<std::
 }
 
 // Forward through the plan, or None when the call does not match it.
-py::object apply(int64_t id, const std::vector<at::Tensor>& inputs) {
+py::object apply(int64_t id, const std::vector<at::Tensor>& inputs, const std::vector<double>& scalars) {
     const Plan& p = plan_at(id);
-    if (inputs.size() != p.in_shape.size()) return py::none();
+    if (inputs.size() != p.in_shape.size() || static_cast<int64_t>(scalars.size()) != p.n_scalars) return py::none();
     for (size_t i = 0; i < inputs.size(); ++i) {
         const at::Tensor& t = inputs[i];
         if (!t.defined() || !t.is_cuda() || t.get_device() != p.device || t.scalar_type() != p.in_dtype[i] ||
             t.sizes() != at::IntArrayRef(p.in_shape[i]) || !t.is_contiguous() || !aligned(t))
             return py::none();
     }
-    auto outs = StencilFunction::apply(id, at::TensorList(inputs));
+    auto outs = StencilFunction::apply(id, at::TensorList(inputs), scalars);
     return py::cast(outs);
 }
 

@@ -274,6 +274,11 @@ class AutoDiffLatticeBoltzmannStep:
         ``torch_native`` backend ignores the loops and differentiates one kernel launch)."""
         if str(backend).lower() not in ('torch_native', 'torch'):
             raise NotImplementedError(f"backend '{backend}': only the torch backends are built")
+        extra_inputs = [f for f in (input_field_to_tensor_dict or {}) if f not in (self.pdf_field, self.pdf_field.name)]
+        if extra_inputs or self._additional_fields:
+            # the kernels would need those fields bound per step (and their adjoints accumulated): not built
+            raise NotImplementedError('timestep op over update rules with additional input fields '
+                                      f'({[getattr(f, "name", f) for f in extra_inputs or self._additional_fields]})')
         torch = _torch()
         step = self
         T = int(num_time_steps)
@@ -294,7 +299,11 @@ class AutoDiffLatticeBoltzmannStep:
                     out = step._alloc(zero=False)
                     step._fwd(states[-1], out, {})
                     states.append(out)
-                ctx.records = states[:-1]
+                # state 0 may be the caller's tensor: keep it through save_for_backward, so that an in-place
+                # change between forward and backward raises (version counter) instead of skewing the adjoint
+                ctx.input_is_state0 = states[0].data_ptr() == pdfs.data_ptr()
+                ctx.save_for_backward(pdfs if ctx.input_is_state0 else None)
+                ctx.records = states[1:-1] if ctx.input_is_state0 else states[:-1]
                 return states[-1]
 
             @staticmethod
@@ -306,10 +315,12 @@ class AutoDiffLatticeBoltzmannStep:
                     ctx.records = None
                     return torch.from_numpy(step.adjoint_pdf_array.copy())
                 g = step._as_layout(grad)
+                records = ([step._as_layout(ctx.saved_tensors[0].detach())] if ctx.input_is_state0 else []) + \
+                    list(ctx.records)
                 cur, spare = g, None                # cur: adjoint of state t + 1 (never written when it is g)
                 for t in reversed(range(T)):
                     nxt = spare if spare is not None else step._alloc(zero=False)
-                    step._bwd(ctx.records[t], cur, nxt, {}, {})
+                    step._bwd(records[t], cur, nxt, {}, {})
                     spare = cur if cur is not g else None
                     cur = nxt
                 ctx.records = None

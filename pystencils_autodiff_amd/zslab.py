@@ -197,6 +197,10 @@ class ZSlabOp:
                 raise ValueError('z-slab decomposition needs 2-D or 3-D fields')
             if any(f.is_soa for f in k.ir.fields):
                 raise NotImplementedError('z-slab decomposition of fzyx (SoA) vector fields')
+            if k.ir.periodic:
+                # a periodic lattice needs a wrap-around exchange between the first and last rank (and the
+                # kernels' own wrapped reads disabled along z): not built
+                raise NotImplementedError("z-slab decomposition of boundary_handling='periodic' kernels")
         self._span = {} if z_offset is None or global_z is None else None
         self._fixed_span = None if self._span is not None else (int(z_offset), int(global_z))
         self._bufs = {}

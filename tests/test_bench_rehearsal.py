@@ -25,12 +25,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize('nproc', [2])
-def test_bench_two_ranks_end_to_end(nproc):
+@pytest.mark.parametrize('nproc,workload', [(2, 'diffusion7_f32'), (2, 'stencil27_f16')])
+def test_bench_two_ranks_end_to_end(nproc, workload):
     env = dict(os.environ, PSAD_DIST_BACKEND='gloo', HSA_ENABLE_IPC_MODE_LEGACY='0')
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={nproc}',
            '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
-           os.path.join(ROOT, 'bench.py'), '--gpus', str(nproc), '--edge', '128', '--steps', '3', '--warmup', '1']
+           os.path.join(ROOT, 'bench.py'), '--gpus', str(nproc), '--edge', '128', '--steps', '3', '--warmup', '1',
+           '--workload', workload, '--cpu-seconds', '1']
     t0 = time.perf_counter()
     proc = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     wall = time.perf_counter() - t0
@@ -43,4 +44,9 @@ def test_bench_two_ranks_end_to_end(nproc):
     assert res['steps'] == 3 and res['value'] > 0
     assert res['ms_per_step'] * res['steps'] / 1e3 <= wall
     assert res['value'] == pytest.approx(128 ** 3 * 3 / (res['ms_per_step'] * 3 / 1e3) / 1e6, rel=1e-3)
-    assert res['cpu_baseline'] is None          # rank 0 times the CPU only at N=1
+    assert res['config']['name'] == workload
+    assert res['metric'].endswith('128^3') and ('27-point fp16' in res['metric']) == (workload == 'stencil27_f16')
+    assert res['roofline']['bytes_per_launch'] == (8 if workload == 'diffusion7_f32' else 4) * 64 * 128 * 128
+    # rank 0 times the CPU path after the timed loop at every N (north_star: "in the same run")
+    cpu = res['cpu_baseline']
+    assert cpu is not None and cpu['value'] > 0 and cpu['cores'] == 1 and cpu['kind'] == 'port', cpu

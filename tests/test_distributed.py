@@ -312,3 +312,106 @@ def test_rccl_open_failure_is_agreed_by_every_rank(tmp_path):
         pytest.skip(f'libpsad_hip.so not built: {exc}')
     mp.spawn(_rccl_agreement_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
     assert [open(tmp_path / f'rccl_{r}.txt').read() for r in range(2)] == ['unavailable', 'unavailable']
+
+
+# --- BASELINE configs 4 and 5 in their 8-way z-slab form, full size, 8 ranks sharing one GPU -------------------
+
+def _hash_unit(idx, seed, xp):
+    """A counter-based hash of the global cell index → [0, 1) (24 bits), identical in torch (on the GPU, per
+    slab) and numpy (the oracle's 3-plane neighbourhoods): no rank ever holds the global field."""
+    h = idx * 2654435761 + seed * 40503
+    h = (h ^ (h >> 16)) & 0x7FFFFFFF
+    h = h * 0x45D9F3B
+    h = (h ^ (h >> 16)) & 0x7FFFFFFF
+    h = h * 0x45D9F3B
+    h = (h ^ (h >> 16)) & 0xFFFFFF
+    return h.to(xp.float64) / float(1 << 24) if hasattr(h, 'to') else h.astype(xp.float64) / float(1 << 24)
+
+
+def _synth_planes(z0, z1, Y, X, seed, dtype, signed):
+    """numpy: planes [z0, z1) of the synthetic field, rounded to the storage dtype (float64 values)."""
+    idx = np.arange(z0 * Y * X, z1 * Y * X, dtype=np.int64)
+    v = _hash_unit(idx, seed, np)
+    v = 2 * v - 1 if signed else v
+    return v.astype(dtype).astype(np.float64).reshape(z1 - z0, Y, X)
+
+
+def _full_size_worker(rank, world, port, builder_name, edge, result_dir):
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    import pystencils_autodiff_amd as pa
+    from pystencils_autodiff_amd import workloads as W
+    from pystencils_autodiff_amd.zslab import ZSlabOp, slab_bounds
+    dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        dt = torch.float16 if builder_name == 'stencil_27pt' else torch.float32
+        lo, hi = slab_bounds(edge, world, rank)
+        idx = torch.arange(lo * edge * edge, hi * edge * edge, dtype=torch.int64, device='cuda')
+        ul = _hash_unit(idx, 1, torch).to(dt).view(hi - lo, edge, edge)
+        dl = (2 * _hash_unit(idx, 2, torch) - 1).to(dt).view(hi - lo, edge, edge)
+        del idx
+        op = pa.AutoDiffOp(getattr(W, builder_name)(), boundary_handling='zeros')
+        z = ZSlabOp(op, use_cuda=True)
+        z._halo = _GlooHalo()                 # RcclHalo's contract, carried over gloo (RCCL: one rank per GPU)
+        z.warm_exchange(u=ul, diffout=dl)
+        fn = z.autograd_function()
+        uu = ul.clone().requires_grad_(True)
+        (o,) = fn.apply(uu)
+        o.backward(dl)
+        torch.cuda.synchronize()
+        du = uu.grad
+        for name, t in (('out', o.detach()), ('du', du)):
+            np.save(os.path.join(result_dir, f'{name}_{rank}.npy'),
+                    torch.stack([t[0], t[-1]]).float().cpu().numpy())
+        # the global adjoint identity <A u, d> = <u, A^T d> over every cell of every slab
+        dots = torch.stack([(o.detach().double() * dl.double()).sum(), (ul.double() * du.double()).sum(),
+                            o.detach().double().abs().sum(), torch.isfinite(o.detach()).all().double(),
+                            torch.isfinite(du).all().double()]).cpu()
+        dist.all_reduce(dots)
+        if rank == 0:
+            with open(os.path.join(result_dir, 'dots.json'), 'w') as fh:
+                json.dump([float(v) for v in dots], fh)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('builder_name,edge', [('diffusion_7pt', 1024), ('stencil_27pt', 768)],
+                         ids=['config4_7pt_f32_1024', 'config5_27pt_f16_768'])
+def test_zslab_full_size_eight_ranks_emulated(builder_name, edge, tmp_path):
+    """BASELINE configs 4 and 5 as configured: the full 1024³ fp32 7-point / 768³ fp16 27-point domain split
+    into 8 z-slabs (128 / 96 planes), 8 ranks sharing one GPU, each driving ``ZSlabOp.autograd_function()``
+    apply + backward with the RCCL sweep (faces on the halo stream, interior launch, two-range face launch),
+    the exchange carried by ``_GlooHalo``. Every rank's first and last planes of the output and of the
+    gradient — both global faces and all 14 slab-boundary planes — vs the float64 oracle on their 3-plane
+    neighbourhoods, and the global adjoint identity over all cells."""
+    import json
+    world = 8
+    from oracle import stencils as S
+    from pystencils_autodiff_amd.zslab import slab_bounds
+    from tests.conftest import assert_close_rel
+    mp.spawn(_full_size_worker, args=(world, _free_port(), builder_name, edge, str(tmp_path)), nprocs=world,
+             join=True)
+    f16 = builder_name == 'stencil_27pt'
+    dt = np.float16 if f16 else np.float32
+    taps = S.taps_27pt() if f16 else S.taps_diffusion_7pt()
+    tol = 1e-3 if f16 else 1e-6
+
+    def ref_plane(p, seed, signed, tp):
+        a, b = max(0, p - 1), min(edge, p + 2)
+        block = np.zeros((3, edge, edge))
+        block[a - (p - 1):b - (p - 1)] = _synth_planes(a, b, edge, edge, seed, dt, signed)
+        return S.linear_stencil(block, tp)[1]
+    for r in range(world):
+        lo, hi = slab_bounds(edge, world, r)
+        assert hi - lo == edge // world
+        out, du = np.load(tmp_path / f'out_{r}.npy'), np.load(tmp_path / f'du_{r}.npy')
+        for k, p in enumerate((lo, hi - 1)):
+            assert_close_rel(out[k], ref_plane(p, 1, False, taps), tol, f'rank {r} out plane {p}')
+            assert_close_rel(du[k], ref_plane(p, 2, True, S.flip(taps)), tol, f'rank {r} diffu plane {p}')
+    ad, ua, mass, fin_o, fin_d = json.load(open(tmp_path / 'dots.json'))
+    assert fin_o == world and fin_d == world
+    assert mass > 0
+    assert abs(ad - ua) <= (5e-3 if f16 else 1e-5) * max(abs(ad), abs(ua)), (ad, ua)

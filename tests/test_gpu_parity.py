@@ -608,6 +608,33 @@ def test_row_pitch_vector_width_vs_oracle(case):
             assert_close_rel(t.cpu().numpy(), ref[n], TOL[dt], f'{name} {which} {n} {shape}')
 
 
+@pytest.mark.parametrize('case', [('27pt_f16', W.stencil_27pt, np.float16, (6, 20, 136)),
+                                  ('7pt_f32', W.diffusion_7pt, np.float32, (5, 18, 132))], ids=lambda c: c[0])
+def test_one_kernel_alternating_pointer_alignment(case):
+    """ONE compiled kernel called with views at element offsets whose byte alignment is 16 (not 32), then 2 or 4,
+    then 16 again, then 64: each call must take a plan for its own alignment class (a 16-byte LDS-DMA plan
+    reused for a 2-byte-aligned view returns wrong data) — outputs vs the float64 oracle."""
+    name, builder, dt, shape = case
+    op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
+    k = op.forward_ast_gpu.compile()
+    es = np.dtype(dt).itemsize
+    n = int(np.prod(shape))
+    tdt = getattr(torch, np.dtype(dt).name)
+    rng = np.random.default_rng(11)
+    for off_bytes in (16, 2 if es == 2 else 4, 16, 64, 8):
+        u = rng.uniform(-1, 1, shape).astype(dt)
+        ref = OE.evaluate(op.forward_assignments, {'u': u}, boundary_handling='zeros')['out']
+        base = torch.empty(n + 64, dtype=tdt, device='cuda')
+        ebase = (-base.data_ptr() % 256) // es            # elements to a 256-byte boundary
+        tu = base[ebase + off_bytes // es: ebase + off_bytes // es + n].view(shape)
+        tu.copy_(torch.from_numpy(u))
+        assert tu.data_ptr() % 256 == off_bytes % 256
+        out = torch.full(shape, float('nan'), dtype=tdt, device='cuda')
+        k(u=tu, out=out)
+        torch.cuda.synchronize()
+        assert_close_rel(out.cpu().numpy(), ref, TOL[dt], f'{name} offset {off_bytes} B')
+
+
 @pytest.mark.parametrize('shape', [(10, 70, 264), (33, 97, 520), (130, 64, 256)])
 @pytest.mark.parametrize('builder', [lambda: W.asym_7pt(dtype='float16'), lambda: W.diffusion_7pt(dtype='float16')],
                          ids=['asym_f16', '7pt_f16'])

@@ -130,7 +130,10 @@ def test_native_misaligned_input_falls_back():
 
 
 @pytest.mark.gpu
-def test_native_scalar_class_kwargs_one_plan_per_value():
+def test_native_scalar_class_kwargs_patched_per_call():
+    """Scalars are patched into the plan's argument buffers per call: changing ``class_kwargs`` reuses the plan
+    (no plan per value), and the backward uses the forward's values even if they change in between."""
+    from pystencils_autodiff_amd.backends._torch_native import native_module
     z, y, x = ps.fields("z, y, x: float32[20,40]")
     a = sp.Symbol('a')
     _, fn = _make(ps.AssignmentCollection({z[0, 0]: x[0, 0] * sp.log(a * x[0, 0] * y[0, 0])}), None, True)
@@ -138,14 +141,24 @@ def test_native_scalar_class_kwargs_one_plan_per_value():
     with pytest.raises(TypeError, match='class_kwargs'):
         fn.apply(*ins)
     g = torch.ones(20, 40, device='cuda')
-    for av in (5.0, 2.0, 5.0):
+    n0 = None
+    for av in (5.0, 2.0, 5.0, 0.75):
         fn.class_kwargs['a'] = av
         outs, res = _run(fn, ins, [g])
         assert _is_native(outs[0])
+        n0 = native_module().num_plans() if n0 is None else n0
+        assert native_module().num_plans() == n0
         xn, yn = (t.detach().double() for t in ins)
         torch.testing.assert_close(res[0].double(), xn * torch.log(av * xn * yn), rtol=1e-6, atol=1e-6)
         torch.testing.assert_close(res[1].double(), torch.log(av * xn * yn) + 1, rtol=1e-6, atol=1e-6)
         torch.testing.assert_close(res[2].double(), xn / yn, rtol=1e-6, atol=1e-6)
+    # a value changed between forward and backward: the adjoint still uses the forward's value
+    fn.class_kwargs['a'] = 3.0
+    (o,) = fn.apply(*ins)
+    fn.class_kwargs['a'] = 7.0
+    o.backward(g)
+    xn, yn = (t.detach().double() for t in ins)
+    torch.testing.assert_close(ins[0].grad.double(), torch.log(3.0 * xn * yn) + 1, rtol=1e-6, atol=1e-6)
 
 
 @pytest.mark.gpu
@@ -228,17 +241,20 @@ def test_native_extension_loads_and_validates_plans():
     n0 = m.num_plans()
     args = b'\0' * 32
     ok = dict(name='t', device=0, in_shape=[[4, 4]], in_dtype=[6], fwd_shape=[[4, 4]], fwd_dtype=[6],
-              fwd_zero=[False], fwd_fn=1, fwd_grid=1, fwd_block=256, fwd_args=args, fwd_slot=[0, 1], saved=[],
-              bwd_shape=[[4, 4]], bwd_dtype=[6], bwd_zero=[False], bwd_fn=1, bwd_grid=1, bwd_block=256,
-              bwd_args=args, bwd_slot=[0, 1], grad_of_input=[1])
+              fwd_zero=[False], fwd_fn=1, fwd_grid=1, fwd_block=256, fwd_args=args, fwd_slot=[0, 1],
+              fwd_scal=[[16, 0, 0]], saved=[], bwd_shape=[[4, 4]], bwd_dtype=[6], bwd_zero=[False], bwd_fn=1,
+              bwd_grid=1, bwd_block=256, bwd_args=args, bwd_slot=[0, 1], bwd_scal=[[24, 1, 0]], grad_of_input=[1],
+              n_scalars=1)
     pid = m.register_plan(*ok.values())
     assert pid == n0 and m.num_plans() == n0 + 1
     for key, bad in (('fwd_slot', [0, 2]), ('saved', [5]), ('bwd_slot', [0, 3]), ('grad_of_input', [7]),
-                     ('fwd_args', b'\0' * 8)):
+                     ('fwd_args', b'\0' * 8), ('fwd_scal', [[8, 0, 0]]), ('bwd_scal', [[28, 1, 0]]),
+                     ('bwd_scal', [[24, 1, 1]]), ('fwd_scal', [[16, 0]])):
         kw = dict(ok, **{key: bad})
         with pytest.raises(RuntimeError):
             m.register_plan(*kw.values())
     assert m.num_plans() == n0 + 1
     x = torch.zeros(4, 4)                         # a CPU tensor never matches a plan: None, no launch
-    assert m.apply(pid, [x]) is None
-    assert m.apply(pid, []) is None
+    assert m.apply(pid, [x], [1.0]) is None
+    assert m.apply(pid, [], [1.0]) is None
+    assert m.apply(pid, [torch.zeros(4, 4)], []) is None      # scalar count differs from the plan
