@@ -86,3 +86,45 @@ def equilibrium(rho, u, stencil='D2Q9', compressible=False, xp=None):
         poly = 3 * cu + 4.5 * cu * cu - 1.5 * usq
         out.append(float(w[i]) * rho * (1 + poly) if compressible else float(w[i]) * (rho + poly))
     return xp.stack(out, -1) if xp.__name__ != 'torch' else xp.stack(out, dim=-1)
+
+
+def inverse(stencil):
+    dirs, _ = SETS[stencil]
+    return [dirs.index(tuple(-c for c in d)) for d in dirs]
+
+
+def _roll_all(xp, a, c):
+    for ax, s in enumerate(c):
+        if s:
+            a = _roll(xp, a, s, ax)
+    return a
+
+
+def stream_walls(f, stencil, wall, xp):
+    """Pull streaming with half-way bounce-back at no-slip obstacle cells (``wall``: bool array over the domain):
+    ``f_i(x) = f_ī(x)`` where ``x − c_i`` is an obstacle, else ``f_i(x − c_i)`` (periodic) — lbmpy's ``NoSlip``
+    (``src_ī(x + c_i) := src_i(x)`` written into the obstacle cell, then the pull; ``adjoint_boundaryconditions.py``
+    restates its adjoint)."""
+    dirs, _ = SETS[stencil]
+    inv = inverse(stencil)
+    comps = []
+    for i, c in enumerate(dirs):
+        pulled = _roll_all(xp, f[..., i], c)
+        nb_wall = _roll_all(xp, wall, c)
+        comps.append(xp.where(nb_wall, f[..., inv[i]], pulled))
+    return xp.stack(comps, -1) if xp.__name__ != 'torch' else xp.stack(comps, dim=-1)
+
+
+def step_walls(f, omega, wall, stencil='D2Q9', compressible=False, xp=None):
+    """One stream-pull-collide step with no-slip obstacles; obstacle cells keep their state."""
+    if xp is None:
+        import numpy as xp
+    new = collide(stream_walls(f, stencil, wall, xp), omega, stencil, compressible, xp)
+    keep = wall[..., None] if xp.__name__ != 'torch' else wall.unsqueeze(-1)
+    return xp.where(keep, f, new)
+
+
+def run_walls(f, omega, wall, steps, stencil='D2Q9', compressible=False, xp=None):
+    for _ in range(steps):
+        f = step_walls(f, omega, wall, stencil, compressible, xp)
+    return f

@@ -51,7 +51,7 @@ def build_torch_ext(force=False, verbose=False):
            f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}",
            *[f'-I{p}' for p in cpp_extension.include_paths()], f"-I{sysconfig.get_paths()['include']}",
            '-I/opt/rocm/include', f"-I{os.path.join(ROOT, 'include')}", TORCH_SRC, '-o', TORCH_OUT + '.tmp',
-           f'-L{tlib}', '-lc10', '-lc10_hip', '-ltorch', '-ltorch_cpu', '-ltorch_python', f'-L{HERE}', '-lpsad_hip',
+           f'-L{tlib}', '-lc10', '-lc10_hip', '-ltorch', '-ltorch_cpu', '-ltorch_python', '-l:libamdhip64.so', f'-L{HERE}', '-lpsad_hip',
            f'-Wl,-rpath,$ORIGIN:{tlib}']
     if verbose:
         print(' '.join(cmd))

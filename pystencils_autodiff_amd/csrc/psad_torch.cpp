@@ -21,6 +21,7 @@
 
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime_api.h>
 
 #include <atomic>
 #include <cstdint>
@@ -152,6 +153,130 @@ struct StencilFunction : public torch::autograd::Function<StencilFunction> {
     }
 };
 
+// ---- z-slab sweeps (zslab.py): the RCCL face exchange and the interior / face launches of one rank ----------
+//
+// ZSlabOp's sweep in Python issues, per sweep: an event on the compute stream and a wait for it on the halo
+// stream, one RCCL group (psad_halo_exchange) on the halo stream, the interior launch on the compute stream, an
+// event on the halo stream and a wait for it on the compute stream, then the face launch(es). For small slabs
+// (the 8-GPU 96×768² fp16 27-point slab computes a sweep in ~50 µs) the Python argument preparation around
+// those calls was what the GPU waited on. A slab plan resolves all of it once per input signature: the
+// launches' argument templates (field pointers patched per call, the receive buffers' halo pointers baked in),
+// the exchange's receive buffers, byte counts and peers; a sweep is then these HIP / RCCL calls and nothing else.
+// The send side needs no record_stream: the compute stream waits for the halo stream before the face launch,
+// so any later reuse of an input's memory is ordered after the exchange has read it.
+
+struct Exchange {
+    void* comm = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_faces = nullptr, ev_halos = nullptr;
+    std::vector<int64_t> slot;            // table index of each exchanged field
+    std::vector<int64_t> last_off;        // byte offset of its last RZ planes
+    std::vector<void*> recv_lo, recv_hi;  // receive buffers (nullptr: no neighbour on that side)
+    std::vector<size_t> bytes;
+    int peer_lo = -1, peer_hi = -1;
+    bool loopback = false;                // one-rank communicator: both faces to itself (periodic z)
+};
+
+struct Sweep {
+    Exchange ex;
+    bool has_inner = false;
+    Launch inner;
+    std::vector<Launch> faces;
+};
+
+struct SlabPlan {
+    int device = 0;
+    std::vector<std::vector<int64_t>> in_shape;
+    std::vector<at::ScalarType> in_dtype;
+    std::vector<Alloc> fwd_out, bwd_out;
+    Sweep fwd, bwd;
+    std::vector<int64_t> saved, grad_of_input;
+    int64_t n_scalars = 0;
+    std::string name;
+};
+
+std::vector<std::unique_ptr<SlabPlan>> g_slab_plans;
+
+const SlabPlan& slab_plan_at(int64_t id) {
+    std::lock_guard<std::mutex> lock(g_mutex);
+    TORCH_CHECK(id >= 0 && id < static_cast<int64_t>(g_slab_plans.size()), "psad: unknown slab plan ", id);
+    return *g_slab_plans[id];
+}
+
+void hip_ok(hipError_t e, const char* what) {
+    TORCH_CHECK(e == hipSuccess, "psad: ", what, " failed: ", hipGetErrorString(e));
+}
+
+void run_sweep(const Sweep& w, const std::vector<at::Tensor>& table, const std::vector<double>& scalars, int device) {
+    c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
+    hipStream_t cur = c10::hip::getCurrentHIPStream(device).stream();
+    const Exchange& ex = w.ex;
+    const size_t n = ex.slot.size();
+    if (n) {
+        hip_ok(hipEventRecord(ex.ev_faces, cur), "hipEventRecord");           // the faces are final
+        hip_ok(hipStreamWaitEvent(ex.stream, ex.ev_faces, 0), "hipStreamWaitEvent");
+        std::vector<const void*> send_lo(n), send_hi(n);
+        for (size_t i = 0; i < n; ++i) {
+            char* base = static_cast<char*>(table[ex.slot[i]].data_ptr());
+            send_lo[i] = base;
+            send_hi[i] = base + ex.last_off[i];
+            // RCCL pairs a peer's sends and receives in issue order: on a loopback communicator the lower halo
+            // receives the far (upper) face, as with real neighbours — a periodic z boundary
+            if (ex.loopback) std::swap(send_lo[i], send_hi[i]);
+        }
+        int rc = psad_halo_exchange(ex.comm, static_cast<int>(n), send_lo.data(), ex.recv_lo.data(), send_hi.data(),
+                                    ex.recv_hi.data(), ex.bytes.data(), ex.peer_lo, ex.peer_hi, ex.stream);
+        TORCH_CHECK(rc == 0, "psad: RCCL halo exchange failed: ", psad_rccl_error_string(rc), " (code ", rc, ")");
+    }
+    if (w.has_inner) launch(w.inner, table, scalars, device);                // interior overlaps the exchange
+    if (n) {
+        hip_ok(hipEventRecord(ex.ev_halos, ex.stream), "hipEventRecord");
+        hip_ok(hipStreamWaitEvent(cur, ex.ev_halos, 0), "hipStreamWaitEvent");
+    }
+    for (const auto& f : w.faces) launch(f, table, scalars, device);
+}
+
+struct SlabFunction : public torch::autograd::Function<SlabFunction> {
+    static torch::autograd::variable_list forward(torch::autograd::AutogradContext* ctx, int64_t id,
+                                                  at::TensorList inputs, std::vector<double> scalars) {
+        const SlabPlan& p = slab_plan_at(id);
+        std::vector<at::Tensor> table(inputs.begin(), inputs.end());
+        std::vector<at::Tensor> outs;
+        for (const auto& a : p.fwd_out) {
+            outs.push_back(allocate(a, p.device));
+            table.push_back(outs.back());
+        }
+        run_sweep(p.fwd, table, scalars, p.device);
+        std::vector<at::Tensor> saved;
+        for (auto i : p.saved) saved.push_back(table[i]);
+        ctx->save_for_backward(saved);
+        ctx->saved_data["plan"] = id;
+        ctx->saved_data["scalars"] = scalars;
+        return outs;
+    }
+
+    static torch::autograd::variable_list backward(torch::autograd::AutogradContext* ctx,
+                                                   torch::autograd::variable_list grads) {
+        const SlabPlan& p = slab_plan_at(ctx->saved_data["plan"].toInt());
+        std::vector<at::Tensor> table = ctx->get_saved_variables();
+        for (auto& g : grads) {
+            at::Tensor t = g.is_contiguous() ? g : g.contiguous();
+            if (!aligned(t)) t = t.clone();
+            table.push_back(t);
+        }
+        std::vector<at::Tensor> outs;
+        for (const auto& a : p.bwd_out) {
+            outs.push_back(allocate(a, p.device));
+            table.push_back(outs.back());
+        }
+        run_sweep(p.bwd, table, ctx->saved_data["scalars"].toDoubleVector(), p.device);
+        torch::autograd::variable_list result(2 + p.grad_of_input.size());   // plan id, inputs..., scalars
+        for (size_t i = 0; i < p.grad_of_input.size(); ++i)
+            if (p.grad_of_input[i] >= 0) result[1 + i] = table[p.grad_of_input[i]];
+        return result;
+    }
+};
+
 Launch make_launch(uint64_t fn, int64_t grid, int64_t block, const py::bytes& args, std::vector<int64_t> slot,
                    std::vector<std::vector<int64_t>> scal, int64_t n_scalars) {
     Launch l;
@@ -217,6 +342,99 @@ int64_t register_plan(const std::string& name, int64_t device, std::vector<std::
     return static_cast<int64_t>(g_plans.size()) - 1;
 }
 
+
+// (fn, grid, block, args, slot, scal) → Launch
+Launch launch_from(const py::tuple& t, int64_t n_scalars) {
+    TORCH_CHECK(t.size() == 6, "psad: launch spec is (fn, grid, block, args, slot, scal)");
+    return make_launch(t[0].cast<uint64_t>(), t[1].cast<int64_t>(), t[2].cast<int64_t>(), t[3].cast<py::bytes>(),
+                       t[4].cast<std::vector<int64_t>>(), t[5].cast<std::vector<std::vector<int64_t>>>(), n_scalars);
+}
+
+// inner (launch spec or None), faces [launch spec], exchange (slot, last_off, recv_lo, recv_hi, bytes, peer_lo,
+// peer_hi, loopback), comm, halo stream
+Sweep sweep_from(const py::object& inner, const py::list& faces, const py::tuple& ex, uint64_t comm, uint64_t stream,
+                 int64_t n_scalars, int64_t n_table) {
+    Sweep w;
+    if (!inner.is_none()) {
+        w.has_inner = true;
+        w.inner = launch_from(inner.cast<py::tuple>(), n_scalars);
+    }
+    for (const auto& f : faces) w.faces.push_back(launch_from(f.cast<py::tuple>(), n_scalars));
+    TORCH_CHECK(ex.size() == 8, "psad: exchange spec has 8 entries");
+    w.ex.slot = ex[0].cast<std::vector<int64_t>>();
+    w.ex.last_off = ex[1].cast<std::vector<int64_t>>();
+    for (auto v : ex[2].cast<std::vector<uint64_t>>()) w.ex.recv_lo.push_back(reinterpret_cast<void*>(v));
+    for (auto v : ex[3].cast<std::vector<uint64_t>>()) w.ex.recv_hi.push_back(reinterpret_cast<void*>(v));
+    for (auto v : ex[4].cast<std::vector<int64_t>>()) w.ex.bytes.push_back(static_cast<size_t>(v));
+    w.ex.peer_lo = ex[5].cast<int>();
+    w.ex.peer_hi = ex[6].cast<int>();
+    w.ex.loopback = ex[7].cast<bool>();
+    const size_t n = w.ex.slot.size();
+    TORCH_CHECK(w.ex.last_off.size() == n && w.ex.recv_lo.size() == n && w.ex.recv_hi.size() == n &&
+                    w.ex.bytes.size() == n, "psad: exchange spec lengths differ");
+    for (size_t i = 0; i < n; ++i) {
+        TORCH_CHECK(w.ex.slot[i] >= 0 && w.ex.slot[i] < n_table && w.ex.last_off[i] >= 0, "psad: exchange slot");
+        TORCH_CHECK((w.ex.peer_lo < 0 || w.ex.recv_lo[i]) && (w.ex.peer_hi < 0 || w.ex.recv_hi[i]),
+                    "psad: a receive buffer is missing for a neighbour");
+    }
+    for (const auto& l : w.faces)
+        for (auto i : l.slot) TORCH_CHECK(i >= 0 && i < n_table, "psad: face slot out of range");
+    if (w.has_inner)
+        for (auto i : w.inner.slot) TORCH_CHECK(i >= 0 && i < n_table, "psad: interior slot out of range");
+    if (n) {
+        w.ex.comm = reinterpret_cast<void*>(comm);
+        w.ex.stream = reinterpret_cast<hipStream_t>(stream);
+        TORCH_CHECK(w.ex.comm != nullptr, "psad: exchange without a communicator");
+        hip_ok(hipEventCreateWithFlags(&w.ex.ev_faces, hipEventDisableTiming), "hipEventCreateWithFlags");
+        hip_ok(hipEventCreateWithFlags(&w.ex.ev_halos, hipEventDisableTiming), "hipEventCreateWithFlags");
+    }
+    return w;
+}
+
+int64_t register_slab_plan(const std::string& name, int64_t device, std::vector<std::vector<int64_t>> in_shape,
+                           std::vector<int64_t> in_dtype, std::vector<std::vector<int64_t>> fwd_shape,
+                           std::vector<int64_t> fwd_dtype, std::vector<bool> fwd_zero, py::object fwd_inner,
+                           py::list fwd_faces, py::tuple fwd_ex, std::vector<int64_t> saved,
+                           std::vector<std::vector<int64_t>> bwd_shape, std::vector<int64_t> bwd_dtype,
+                           std::vector<bool> bwd_zero, py::object bwd_inner, py::list bwd_faces, py::tuple bwd_ex,
+                           std::vector<int64_t> grad_of_input, int64_t n_scalars, uint64_t comm, uint64_t stream) {
+    auto p = std::make_unique<SlabPlan>();
+    p->name = name;
+    p->device = static_cast<int>(device);
+    TORCH_CHECK(in_shape.size() == in_dtype.size() && grad_of_input.size() == in_shape.size(),
+                "psad: input spec mismatch");
+    p->in_shape = std::move(in_shape);
+    for (auto d : in_dtype) p->in_dtype.push_back(static_cast<at::ScalarType>(d));
+    p->fwd_out = make_allocs(fwd_shape, fwd_dtype, fwd_zero);
+    p->bwd_out = make_allocs(bwd_shape, bwd_dtype, bwd_zero);
+    p->n_scalars = n_scalars;
+    p->saved = std::move(saved);
+    p->grad_of_input = std::move(grad_of_input);
+    const int64_t n_fwd = static_cast<int64_t>(p->in_shape.size() + p->fwd_out.size());
+    for (auto i : p->saved) TORCH_CHECK(i >= 0 && i < n_fwd, "psad: saved index out of range");
+    const int64_t n_bwd = static_cast<int64_t>(p->saved.size() + p->fwd_out.size() + p->bwd_out.size());
+    for (auto i : p->grad_of_input) TORCH_CHECK(i >= -1 && i < n_bwd, "psad: gradient index out of range");
+    c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
+    p->fwd = sweep_from(fwd_inner, fwd_faces, fwd_ex, comm, stream, n_scalars, n_fwd);
+    p->bwd = sweep_from(bwd_inner, bwd_faces, bwd_ex, comm, stream, n_scalars, n_bwd);
+    std::lock_guard<std::mutex> lock(g_mutex);
+    g_slab_plans.push_back(std::move(p));
+    return static_cast<int64_t>(g_slab_plans.size()) - 1;
+}
+
+py::object apply_slab(int64_t id, const std::vector<at::Tensor>& inputs, const std::vector<double>& scalars) {
+    const SlabPlan& p = slab_plan_at(id);
+    if (inputs.size() != p.in_shape.size() || static_cast<int64_t>(scalars.size()) != p.n_scalars) return py::none();
+    for (size_t i = 0; i < inputs.size(); ++i) {
+        const at::Tensor& t = inputs[i];
+        if (!t.defined() || !t.is_cuda() || t.get_device() != p.device || t.scalar_type() != p.in_dtype[i] ||
+            t.sizes() != at::IntArrayRef(p.in_shape[i]) || !t.is_contiguous() || !aligned(t))
+            return py::none();
+    }
+    auto outs = SlabFunction::apply(id, at::TensorList(inputs), scalars);
+    return py::cast(outs);
+}
+
 // Forward through the plan, or None when the call does not match it.
 py::object apply(int64_t id, const std::vector<at::Tensor>& inputs, const std::vector<double>& scalars) {
     const Plan& p = plan_at(id);
@@ -237,6 +455,12 @@ PYBIND11_MODULE(_psad_torch, m) {
     m.doc() = "native autograd node of the torch_native stencil op (see psad_torch.cpp)";
     m.def("register_plan", &register_plan);
     m.def("apply", &apply);
+    m.def("register_slab_plan", &register_slab_plan);
+    m.def("apply_slab", &apply_slab);
+    m.def("num_slab_plans", []() {
+        std::lock_guard<std::mutex> lock(g_mutex);
+        return static_cast<int64_t>(g_slab_plans.size());
+    });
     m.def("set_debug_poison", [](bool on) { g_poison.store(on); },
           "fill the outputs allocated uninitialised with NaN (tests: a kernel that leaves cells unwritten shows)");
     m.def("num_plans", []() {

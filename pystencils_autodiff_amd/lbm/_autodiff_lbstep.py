@@ -22,15 +22,23 @@ Deliberate deviations, each because the reference's behaviour is not a gradient:
 * the backward of T steps needs each step's src state (the collision Jacobian depends on it): the forward
   records them (``record=True`` / the timestep op: T + 1 arrays, written in turn, no copies); the
   reference's ``run_backward`` re-uses whatever the arrays hold.
-Only periodic lattices are built (lbmpy's boundary handling / ``AdjointBoundaryCondition``,
-``adjoint_boundaryconditions.py``, needs lbmpy's flag fields).
+
+Rules made by ``create_lb_update_rule`` run on the lattice schedule (``_lattice_kernels``: one forward and one
+adjoint kernel written for the lattice, any pdf strides, the op's internal states in the row-interleaved
+``[z][y][q][x]`` layout) — which also carries no-slip walls (``set_boundary_including_adjoint``,
+``_autodiff_lbstep.py:162-187``; half-way bounce-back fused into the pull, obstacle cells keep their state).
+Other rules run on the ``AutoDiffOp`` kernels (periodic, no walls).
 """
+import os
+
 import numpy as np
 import sympy as sp
 
 from .. import ps
 from ..autodiff import AutoDiffOp
+from ._lattice_kernels import LatticeKernels, neighbour_mask, row_interleaved_empty
 from ._method import LBStencil
+from .boundaries import AdjointBoundaryCondition, AdjointNoSlip, BoundaryHandling, NoSlip
 
 __all__ = ['AutoDiffLatticeBoltzmannStep', 'PdfFieldNotDetectedException', 'SimulationResultsTensors']
 
@@ -130,6 +138,18 @@ class AutoDiffLatticeBoltzmannStep:
         self._device = device
         self._arrays = {}
         self._records = None
+        # the lattice schedule for the rules of create_lb_update_rule (SRT, stream_pull_collide); walls need it
+        rr = getattr(update_rule, 'relaxation_rate', None)
+        self._omega_of = (lambda: float(self.kernel_params[rr.name])) if isinstance(rr, sp.Symbol) else \
+            ((lambda v=rr: float(v)) if rr is not None else None)
+        # (PSAD_LBM_LATTICE=0: the AutoDiffOp kernels instead — tests of that path, A/B probes)
+        self._lattice = {} if (getattr(update_rule, 'stencil', None) is not None and not time_constant_fields
+                               and os.environ.get('PSAD_LBM_LATTICE', '1') != '0'
+                               and not self._additional_fields and self._omega_of is not None
+                               and np.dtype(src.dtype.numpy_dtype) in (np.float32, np.float64)) else None
+        self._boundary = BoundaryHandling(self.domain_size, on_change=self._flags_changed)
+        self._adjoint_boundary_conditions = {}
+        self._flag_dev = None
 
     # -- reference-named properties ----------------------------------------------------------------
     @property
@@ -190,6 +210,23 @@ class AutoDiffLatticeBoltzmannStep:
         out.copy_(t)
         return out
 
+    def _internal_state(self):
+        """A state only the time-step op sees: the row-interleaved layout (lattice schedule)."""
+        torch = _torch()
+        dev = self._device or torch.device('cuda', torch.cuda.current_device())
+        return row_interleaved_empty(self.domain_size, int(self.pdf_field.index_shape[0]),
+                                     getattr(torch, np.dtype(self.pdf_field.dtype.numpy_dtype).name), dev)
+
+    def _alloc_strides(self):
+        if getattr(self, '_alloc_st', None) is None:
+            self._alloc_st = tuple(self._array(self._pdf_arr_name).stride())
+        return self._alloc_st
+
+    def _lattice_input_ok(self, t):
+        """A tensor the lattice kernels take as it is: ``[*domain, q]`` of the pdf dtype on the step's device."""
+        ref = self._array(self._pdf_arr_name)
+        return tuple(t.shape) == tuple(ref.shape) and t.dtype == ref.dtype and t.device == ref.device
+
     def _array(self, name):
         if name not in self._arrays:
             self._arrays[name] = self._alloc()
@@ -204,6 +241,60 @@ class AutoDiffLatticeBoltzmannStep:
         self._array(self._pdf_arr_name)[...] = pdfs
         self._records = None
 
+    # -- boundaries (``_autodiff_lbstep.py:162-187``) --------------------------------------------------
+    @property
+    def boundary_handling(self):
+        """The obstacle flags (``BoundaryHandling.set_boundary``); forward and adjoint read the same flags."""
+        return self._boundary
+
+    @property
+    def backward_boundary_handling(self):
+        return self._boundary
+
+    def set_boundary_including_adjoint(self, boundary_condition, slice_obj=None, mask_callback=None, mask_array=None,
+                                       adjoint_boundary_condition=None):
+        """Set ``boundary_condition`` (``NoSlip``) on the selected cells for the forward AND the adjoint steps
+        (the reference's signature; the adjoint condition defaults to ``AdjointBoundaryCondition(bc)``)."""
+        if not isinstance(boundary_condition, NoSlip):
+            raise NotImplementedError(f'boundary {boundary_condition!r}: only NoSlip walls are built')
+        if self._lattice is None:
+            raise NotImplementedError('walls need the lattice schedule (a create_lb_update_rule rule without '
+                                      'time-constant or additional fields)')
+        if adjoint_boundary_condition is None:
+            adjoint_boundary_condition = self._adjoint_boundary_conditions.setdefault(
+                boundary_condition, AdjointBoundaryCondition(boundary_condition,
+                                                             time_constant_fields=self._autodiff.time_constant_fields,
+                                                             constant_fields=self._autodiff.constant_fields))
+        elif not isinstance(adjoint_boundary_condition, (AdjointNoSlip, AdjointBoundaryCondition)):
+            raise NotImplementedError(f'adjoint boundary {adjoint_boundary_condition!r}')
+        self._boundary.set_boundary(boundary_condition, slice_obj, mask_callback=mask_callback, mask_array=mask_array)
+
+    def _flags_changed(self):
+        self._flag_dev = None
+        self._records = None
+
+    def _flag_arg(self):
+        """The cells' neighbour masks for the wall kernels (computed once per flag change), None without walls."""
+        if not self._boundary.has_walls:
+            return None
+        if self._flag_dev is None:
+            if self._gpu:
+                torch = _torch()
+                dev = self._device or torch.device('cuda', torch.cuda.current_device())
+                self._flag_dev = neighbour_mask(torch.from_numpy(self._boundary.flags.copy()).to(dev), self.method,
+                                                torch)
+            else:
+                self._flag_dev = neighbour_mask(self._boundary.flags, self.method, np)
+        return self._flag_dev
+
+    def _lattice_kernels(self):
+        walls = self._boundary.has_walls
+        k = self._lattice.get(walls)
+        if k is None:
+            k = self._lattice[walls] = LatticeKernels(self.method, getattr(self._update_rule, 'compressible', False),
+                                                      self.pdf_field.dtype.numpy_dtype, walls, self._target)
+        return k
+
     # -- kernels -----------------------------------------------------------------------------------
     def _kernels(self):
         op = self._autodiff
@@ -212,10 +303,14 @@ class AutoDiffLatticeBoltzmannStep:
         return op.forward_ast_cpu.compile(), op.backward_ast_cpu.compile()
 
     def _fwd(self, src, dst, extra):
+        if self._lattice is not None:
+            return self._lattice_kernels().forward(src, dst, self._omega_of(), self._flag_arg())
         kf, _ = self._kernels()
         kf(**{self._pdf_arr_name: src, self._tmp_arr_name: dst}, **extra, **self.kernel_params)
 
     def _bwd(self, src, diffdst, diffsrc, extra, extra_adj):
+        if self._lattice is not None:
+            return self._lattice_kernels().adjoint(src, diffdst, diffsrc, self._omega_of(), self._flag_arg())
         _, kb = self._kernels()
         kb(**{self._pdf_arr_name: src, 'diff' + self._tmp_arr_name: diffdst, 'diff' + self._pdf_arr_name: diffsrc},
            **extra, **extra_adj, **self.kernel_params)
@@ -292,11 +387,15 @@ class AutoDiffLatticeBoltzmannStep:
                     ctx.records = step._records
                     step._records = None
                     return torch.from_numpy(step.pdf_array.copy())
-                # states on fresh arrays in the field's layout: the input is the first state when it has
-                # that layout already (``empty_pdfs``), the output is the last — no copies
-                states = [step._as_layout(pdfs.detach())]
-                for _ in range(T):
-                    out = step._alloc(zero=False)
+                # states on fresh arrays: the input is the first state (the lattice kernels read any strides;
+                # the AutoDiffOp kernels need the field's layout — ``empty_pdfs`` — or get a copy), the output, in
+                # the field's layout, the last; the lattice schedule keeps the states between in the
+                # row-interleaved layout (no copies either way)
+                lattice = step._lattice is not None
+                x0 = pdfs.detach()
+                states = [x0 if lattice and step._lattice_input_ok(x0) else step._as_layout(x0)]
+                for t in range(T):
+                    out = step._alloc(zero=False) if (t == T - 1 or not lattice) else step._internal_state()
                     step._fwd(states[-1], out, {})
                     states.append(out)
                 # state 0 may be the caller's tensor: keep it through save_for_backward, so that an in-place
@@ -314,12 +413,19 @@ class AutoDiffLatticeBoltzmannStep:
                     step.run_backward(T)
                     ctx.records = None
                     return torch.from_numpy(step.adjoint_pdf_array.copy())
-                g = step._as_layout(grad)
-                records = ([step._as_layout(ctx.saved_tensors[0].detach())] if ctx.input_is_state0 else []) + \
-                    list(ctx.records)
+                lattice = step._lattice is not None
+                g = grad if lattice and step._lattice_input_ok(grad) else step._as_layout(grad)
+                x0 = ctx.saved_tensors[0].detach() if ctx.input_is_state0 else None
+                records = ([x0 if lattice and step._lattice_input_ok(x0) else step._as_layout(x0)]
+                           if ctx.input_is_state0 else []) + list(ctx.records)
                 cur, spare = g, None                # cur: adjoint of state t + 1 (never written when it is g)
                 for t in reversed(range(T)):
-                    nxt = spare if spare is not None else step._alloc(zero=False)
+                    if spare is not None:
+                        nxt = spare
+                    else:
+                        nxt = step._alloc(zero=False) if (t == 0 or not lattice) else step._internal_state()
+                    if lattice and t == 0 and nxt.stride() != step._alloc_strides():
+                        nxt = step._alloc(zero=False)       # the gradient leaves in the field's layout
                     step._bwd(records[t], cur, nxt, {}, {})
                     spare = cur if cur is not g else None
                     cur = nxt
@@ -329,6 +435,38 @@ class AutoDiffLatticeBoltzmannStep:
         LbmTimesteps.num_time_steps = T
         LbmTimesteps.lb_step = self
         return LbmTimesteps
+
+    def _pdf_io_field(self):
+        """The pdf field of the macroscopic ops, in the step's pdf layout (fzyx pdfs enter without a copy)."""
+        return ps.fields(f"pdfs({self.method.Q}): {np.dtype(self.pdf_field.dtype.numpy_dtype).name}"
+                         f"[{len(self.domain_size)}D]", layout='fzyx' if self.pdf_field.is_soa else None)
+
+    def create_end_to_end_op(self, num_time_steps, velocity_input_tensor, density_input_tensor,
+                             additional_fields_to_tensor_map=None, force_input_tensor=None, backend='torch_native',
+                             num_times_steps_without_save=0, **kernel_compilation_kwargs):
+        """Equilibrium from (ρ, u) → ``num_time_steps`` steps → (ρ, u), differentiable end to end
+        (``_autodiff_lbstep.py:310-334``, there TensorFlow only): the setter op, the time-step ops in groups of
+        ``num_times_steps_without_save + 1`` steps, the getter op, evaluated on the given tensors (torch
+        autograd records the chain). Returns ``SimulationResultsTensors``."""
+        if str(backend).lower() not in ('torch_native', 'torch'):
+            raise NotImplementedError(f"backend '{backend}': only the torch backends are built")
+        if force_input_tensor is not None:
+            raise NotImplementedError('force models are not built (SRT without forcing)')
+        if additional_fields_to_tensor_map:
+            raise NotImplementedError('additional fields of the update rule are not built')
+        setter = self._e2e_ops.get('setter') if hasattr(self, '_e2e_ops') else None
+        if setter is None:
+            self._e2e_ops = {'setter': self.create_macroscopic_setter_op(backend, **kernel_compilation_kwargs),
+                             'getter': self.create_macroscopic_getter_op(backend, **kernel_compilation_kwargs)}
+        ops = self._e2e_ops
+        group = int(num_times_steps_without_save) + 1
+        step_op = self.create_timestep_op(group, backend=backend)
+        (input_pdf,) = ops['setter'].apply(density_input_tensor, velocity_input_tensor)
+        out = input_pdf
+        for _ in range(int(num_time_steps) // group):
+            out = step_op.apply(out)
+        rho, vel = ops['getter'].apply(out)
+        return SimulationResultsTensors(input_pdf, out, rho, vel)
 
     def _macroscopic_fields(self):
         dt = self.pdf_field.dtype.numpy_dtype
@@ -340,8 +478,7 @@ class AutoDiffLatticeBoltzmannStep:
         ``(rho, vel)``."""
         from ._method import macroscopic_getter
         rho, vel = self._macroscopic_fields()
-        pdf = ps.fields(f"pdfs({self.method.Q}): {np.dtype(self.pdf_field.dtype.numpy_dtype).name}"
-                        f"[{len(self.domain_size)}D]")
+        pdf = self._pdf_io_field()
         ac = macroscopic_getter(self.method, pdf, rho, vel, getattr(self._update_rule, 'compressible', False))
         op = AutoDiffOp(ac, 'LBM_GetMacroscopicValues', diff_mode='transposed', **kernel_compilation_kwargs)
         return op.create_tensorflow_op(use_cuda=self._gpu, backend=backend)
@@ -350,8 +487,7 @@ class AutoDiffLatticeBoltzmannStep:
         """pdfs = feq(ρ, u) as a differentiable op (``_autodiff_lbstep.py:282-308``): ``Op.apply(rho, vel)``."""
         from ._method import equilibrium_setter
         rho, vel = self._macroscopic_fields()
-        pdf = ps.fields(f"pdfs({self.method.Q}): {np.dtype(self.pdf_field.dtype.numpy_dtype).name}"
-                        f"[{len(self.domain_size)}D]")
+        pdf = self._pdf_io_field()
         ac = equilibrium_setter(self.method, pdf, rho, vel, getattr(self._update_rule, 'compressible', False))
         op = AutoDiffOp(ac, 'LBM_SetMacroscopicValues', diff_mode='transposed', **kernel_compilation_kwargs)
         return op.create_tensorflow_op(use_cuda=self._gpu, backend=backend)

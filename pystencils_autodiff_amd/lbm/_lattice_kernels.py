@@ -1,0 +1,495 @@
+"""The lattice Boltzmann schedule: stream-pull-collide SRT forward and adjoint kernels, written for the lattice.
+
+``AutoDiffLatticeBoltzmannStep`` drives rules made by ``create_lb_update_rule`` (lbmpy's SRT
+``stream_pull_collide`` kernel [ext], ``/root/reference/src/pystencils_autodiff/lbm/_autodiff_lbstep.py:189-247,
+372-398``) through these kernels instead of the general one-thread-per-cell lowering of the rule's
+``AssignmentCollection``: the general lowering reads and writes each pdf component as its own field, in the
+layout of the caller's tensors, with every cell's 2·Q streams in Q separate component planes.
+
+What this schedule does differently:
+
+* **Layouts by strides.** A pdf array is addressed as ``q·s_q + z·s_z + y·s_y + x·s_x``: the caller's fzyx
+  (lbmpy's default, one plane per component) or AoS arrays are read and written in place. The time-step op's
+  intermediate states, which only the op sees, use the row-interleaved layout ``[z][y][q][x]``: the Q
+  components of a lattice row are one contiguous block (Q·X elements), so a wave's 2·Q accesses per row land
+  in ~10 neighbouring row blocks instead of 2·Q planes a whole field apart.
+* **Walls.** An optional flag array (``uint8``, one per cell, C order, 1 = no-slip obstacle) turns on lbmpy's
+  half-way bounce-back fused into the pull: ``f_i(x) = src_ī(x)`` where ``x − c_i`` is an obstacle
+  (``lbmpy.boundaries.NoSlip`` [ext] writes ``src_ī(x + c_i) := src_i(x)`` into the obstacle cell before the
+  pull, ``adjoint_boundaryconditions.py:49-72`` moves the adjoint back); obstacle cells keep their state
+  (``dst = src`` there — lbmpy's values in obstacle cells are not part of the flow).
+* **Adjoint in scatter form through the collision's structure** (``_method.create_lb_adjoint_rule``):
+  ``v_j = (1 − ω) g_j + ω (A + Σ_a B_a ∂u_a/∂f_j)`` with two moment-like sums, stored to the cell the forward
+  pulled ``f_j`` from — ``(x − c_j, j)``, or ``(x, ī)`` for a bounced ``f_j``. Every (component, cell) of
+  the result is written exactly once (for fluid ``x``: by ``x + c_k`` if that cell is fluid, else by ``x``
+  itself; obstacle cells by themselves), so the output needs no zero fill and no atomics.
+
+One source is printed for both targets: a HIP kernel (one thread per cell, wave64 along x) compiled by hiprtc,
+and a C loop nest (``use_cuda=False`` / ``target='cpu'``) compiled by gcc.
+"""
+import ctypes
+import os
+import struct
+
+import numpy as np
+
+__all__ = ['LatticeKernels', 'lattice_strides', 'row_interleaved_empty', 'neighbour_mask']
+
+
+def _c(v):
+    """A rational / float constant as a C literal of the compute type."""
+    return repr(float(v))
+
+
+SELF_BIT = 30      # bit of a cell's neighbour mask: the cell itself is an obstacle (bits 0..Q-1: x − c_i is one)
+
+
+def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
+    """Source of the forward (``lbm_fwd``) and adjoint (``lbm_adj``) kernels.
+
+    ``addr='buf'`` (HIP): every pdf array is one buffer resource (its bytes below 2³²); a component's plane
+    offset ``q·s_q`` rides in the instruction's scalar offset and each distinct neighbour cell's byte offset is
+    ONE 32-bit VGPR shared by all components that pull from it — no 64-bit address arithmetic per access.
+    ``'ptr'``: plain pointers (the C target, and arrays of 4 GiB and more). ``walls``: a ``uint32`` neighbour
+    mask per cell (bit i: ``x − c_i`` is an obstacle; bit ``SELF_BIT``: ``x`` is one), one load per cell."""
+    D, Q = stencil.D, stencil.Q
+    dirs = [tuple(d) for d in stencil.directions]
+    w = [float(x) for x in stencil.weights]
+    inv = [stencil.inverse_direction_index(i) for i in range(Q)]
+    axes = ['z', 'y', 'x'][3 - D:]          # spatial axes, axis 0 slowest; x fastest
+    ct = ctype
+    hip = target == 'hip'
+    buf = hip and addr == 'buf'
+    esize = 8 if ctype == 'double' else 4
+    L = []
+    fn = '__device__ static inline' if hip else 'static inline'
+    if not hip:
+        L.append('#include <stdint.h>\ntypedef long long i64;')
+    L.append(f'typedef {ctype} T;\ntypedef {idx} IDX;')
+    if hip:
+        L.append('typedef unsigned u32x2 __attribute__((ext_vector_type(2)));')
+
+    def c_(v):
+        return f'({ct}){_c(v)}'
+
+    def key(d):
+        return '_'.join({0: '0', 1: 'm', -1: 'p'}[c] for c in d)      # pull: x − c → m(inus) / p(lus)
+
+    keys = sorted({key(d) for d in dirs})
+
+    def coord(k, a):
+        c = k.split('_')[axes.index(a)]
+        return a if c == '0' else f'{a}{c}'
+
+    def neighbour_offsets(L, prefix):
+        """One element (ptr) or byte (buf) offset per distinct neighbour cell of tensor ``prefix``."""
+        for k in keys:
+            e = ' + '.join(f'(IDX){coord(k, a)} * {prefix}_{a}' for a in axes)
+            if buf:
+                L.append(f'  const unsigned {prefix}o_{k} = (unsigned)({e}) * {esize}u;')
+            else:
+                L.append(f'  const IDX {prefix}o_{k} = {e};')
+
+    def soff(prefix, comp):
+        return f'{comp} * {prefix}_qb' if buf else None
+
+    def load(prefix, arr, comp, off):
+        if buf:
+            bits = 'b64' if esize == 8 else 'b32'
+            ty = 'u32x2' if esize == 8 else 'unsigned'
+            return (f'({ct})__builtin_bit_cast(T, ({ty})__builtin_amdgcn_raw_buffer_load_{bits}('
+                    f'rs_{prefix}, {off}, {soff(prefix, comp)}, 0))')
+        return f'({ct}){arr}[(IDX){comp} * {prefix}_q + {off}]'
+
+    def store(prefix, arr, comp, off, val):
+        if buf:
+            bits = 'b64' if esize == 8 else 'b32'
+            ty = 'u32x2' if esize == 8 else 'unsigned'
+            return (f'__builtin_amdgcn_raw_buffer_store_{bits}(__builtin_bit_cast({ty}, (T)({val})), rs_{prefix}, '
+                    f'{off}, {soff(prefix, comp)}, 0);')
+        return f'{arr}[(IDX){comp} * {prefix}_q + {off}] = (T)({val});'
+
+    def wrap_lines(L):
+        for a in axes:
+            N = a.upper()
+            L.append(f'  const int {a}m = {a} == 0 ? {N} - 1 : {a} - 1, {a}p = {a} == {N} - 1 ? 0 : {a} + 1;')
+
+    def rsrc(L, prefix, arr):
+        if buf:
+            L.append(f'  const __amdgpu_buffer_rsrc_t rs_{prefix} = __builtin_amdgcn_make_buffer_rsrc((void*){arr}, '
+                     f'(short)0, (int){prefix}_bytes, 0x00020000);')
+            L.append(f'  const int {prefix}_qb = (int){prefix}_q * {esize};')
+
+    centre = '_'.join('0' for _ in axes)
+
+    def pull_loads(L, prefix, arr):
+        for i in range(Q):
+            k = key(dirs[i])
+            if walls and any(dirs[i]):
+                if buf:
+                    L.append(f'  const bool bb{i} = (msk >> {i}) & 1u;')
+                    L.append(f'  const {ct} f{i} = bb{i} ? {load(prefix, arr, inv[i], f"{prefix}o_{centre}")} : '
+                             f'{load(prefix, arr, i, f"{prefix}o_{k}")};')
+                else:
+                    L.append(f'  const {ct} f{i} = {arr}[(msk >> {i}) & 1u ? (IDX){inv[i]} * {prefix}_q + '
+                             f'{prefix}o_{centre} : (IDX){i} * {prefix}_q + {prefix}o_{k}];')
+            else:
+                L.append(f'  const {ct} f{i} = {load(prefix, arr, i, f"{prefix}o_{k}")};')
+
+    def moments(L):
+        L.append(f'  const {ct} rho = ' + ' + '.join(f'f{i}' for i in range(Q)) + ';')
+        for a in range(D):
+            pos = [f'f{i}' for i in range(Q) if dirs[i][a] == 1]
+            neg = [f'f{i}' for i in range(Q) if dirs[i][a] == -1]
+            L.append(f'  const {ct} m{a} = (' + ' + '.join(pos) + ') - (' + ' + '.join(neg) + ');')
+        if compressible:
+            L.append(f'  const {ct} irho = ({ct})1 / rho;')
+        for a in range(D):
+            L.append(f'  const {ct} u{a} = m{a}' + (' * irho;' if compressible else ';'))
+        L.append(f'  const {ct} usq = ' + ' + '.join(f'u{a} * u{a}' for a in range(D)) + ';')
+
+    def cu_expr(i):
+        t = [('+ ' if dirs[i][a] > 0 else '- ') + f'u{a}' for a in range(D) if dirs[i][a]]
+        if not t:
+            return f'({ct})0'
+        s_ = ' '.join(t)
+        return s_[2:] if s_.startswith('+ ') else '(' + s_ + ')'
+
+    mask_param = 'const unsigned* __restrict__ nbmask'
+    sig_fwd = (f'const T* __restrict__ src, T* __restrict__ dst, {mask_param}, const int Z, const int Y, const int X, '
+               'const IDX s_q, const IDX s_z, const IDX s_y, const IDX s_x, '
+               'const IDX d_q, const IDX d_z, const IDX d_y, const IDX d_x, '
+               f'const long long s_bytes, const long long d_bytes, const {ct} omega')
+    sig_adj = (f'const T* __restrict__ src, const T* __restrict__ g, T* __restrict__ out, {mask_param}, '
+               'const int Z, const int Y, const int X, '
+               'const IDX s_q, const IDX s_z, const IDX s_y, const IDX s_x, '
+               'const IDX g_q, const IDX g_z, const IDX g_y, const IDX g_x, '
+               'const IDX o_q, const IDX o_z, const IDX o_y, const IDX o_x, '
+               f'const long long s_bytes, const long long g_bytes, const long long o_bytes, const {ct} omega')
+    cell = '((IDX)z * Y + y) * X + x' if D == 3 else '(IDX)y * X + x'
+
+    # ---- forward
+    L.append(f'{fn} void lbm_fwd_cell({sig_fwd}, const int z, const int y, const int x)\n{{')
+    L.append('  (void)Z; (void)s_bytes; (void)d_bytes;')
+    rsrc(L, 's', 'src')
+    rsrc(L, 'd', 'dst')
+    wrap_lines(L)
+    neighbour_offsets(L, 's')
+    L.append(f'  const IDX dc = ' + ' + '.join(f'(IDX){a} * d_{a}' for a in axes) + ';')
+    if buf:
+        L.append(f'  const unsigned dcb = (unsigned)dc * {esize}u;')
+    dcoff = 'dcb' if buf else 'dc'
+    if walls:
+        L.append(f'  const unsigned msk = nbmask[{cell}];')
+        L.append(f'  if (msk >> {SELF_BIT}) {{')
+        for i in range(Q):
+            L.append('    ' + store('d', 'dst', i, dcoff, load('s', 'src', i, f'so_{centre}')))
+        L.append('    return;\n  }')
+    pull_loads(L, 's', 'src')
+    moments(L)
+    for i in range(Q):
+        L.append(f'  {{ const {ct} cu = {cu_expr(i)};')
+        L.append(f'    const {ct} poly = cu * (({ct})3 + ({ct})4.5 * cu) - ({ct})1.5 * usq;')
+        feq = f'{c_(w[i])} * rho * (({ct})1 + poly)' if compressible else f'{c_(w[i])} * (rho + poly)'
+        L.append('    ' + store('d', 'dst', i, dcoff, f'f{i} + omega * ({feq} - f{i})') + ' }')
+    L.append('}')
+
+    # ---- adjoint (scatter to where the forward pulled from)
+    L.append(f'{fn} void lbm_adj_cell({sig_adj}, const int z, const int y, const int x)\n{{')
+    L.append('  (void)Z; (void)s_bytes; (void)g_bytes; (void)o_bytes;')
+    rsrc(L, 's', 'src')
+    rsrc(L, 'g', 'g')
+    rsrc(L, 'o', 'out')
+    wrap_lines(L)
+    neighbour_offsets(L, 's')
+    neighbour_offsets(L, 'o')
+    L.append(f'  const IDX gc = ' + ' + '.join(f'(IDX){a} * g_{a}' for a in axes) + ';')
+    if buf:
+        L.append(f'  const unsigned gcb = (unsigned)gc * {esize}u;')
+    gcoff = 'gcb' if buf else 'gc'
+    if walls:
+        L.append(f'  const unsigned msk = nbmask[{cell}];')
+        L.append(f'  if (msk >> {SELF_BIT}) {{')
+        for i in range(Q):
+            L.append('    ' + store('o', 'out', i, f'oo_{centre}', load('g', 'g', i, gcoff)))
+        L.append('    return;\n  }')
+    for i in range(Q):
+        L.append(f'  const {ct} g{i} = {load("g", "g", i, gcoff)};')
+    pull_loads(L, 's', 'src')
+    moments(L)
+    L.append(f'  {ct} S = 0, A = 0;')
+    for a in range(D):
+        L.append(f'  {ct} B{a} = 0;')
+    for i in range(Q):
+        L.append(f'  {{ const {ct} cu = {cu_expr(i)};')
+        L.append(f'    const {ct} gw = g{i} * {c_(w[i])};')
+        L.append('    S += gw;')
+        if compressible:
+            L.append(f'    A += gw * (({ct})1 + cu * (({ct})3 + ({ct})4.5 * cu) - ({ct})1.5 * usq);')
+        if any(dirs[i]):
+            L.append(f'    const {ct} t = gw * (({ct})3 + ({ct})9 * cu);')
+            for a in range(D):
+                if dirs[i][a]:
+                    L.append(f'    B{a} {"+" if dirs[i][a] > 0 else "-"}= t;')
+        L.append('  }')
+    if not compressible:
+        L.append('  A = S;')
+    for a in range(D):
+        L.append(f'  B{a} -= ({ct})3 * u{a} * S;')
+        if compressible:
+            L.append(f'  B{a} *= rho;')
+    if compressible:
+        L.append(f'  const {ct} Bu = ' + ' + '.join(f'B{a} * u{a}' for a in range(D)) + ';')
+    for j in range(Q):
+        cb = [('+ ' if dirs[j][a] > 0 else '- ') + f'B{a}' for a in range(D) if dirs[j][a]]
+        cbs = ' '.join(cb)
+        cbs = (cbs[2:] if cbs.startswith('+ ') else cbs) if cb else f'({ct})0'
+        du = f'(({cbs}) - Bu) * irho' if compressible else f'({cbs})'
+        L.append(f'  {{ const {ct} v = (({ct})1 - omega) * g{j} + omega * (A + {du});')
+        k = key(dirs[j])
+        if walls and any(dirs[j]):
+            if buf:
+                L.append(f'    if ((msk >> {j}) & 1u) {store("o", "out", inv[j], f"oo_{centre}", "v")}')
+                L.append(f'    else {store("o", "out", j, f"oo_{k}", "v")} }}')
+            else:
+                L.append(f'    out[(msk >> {j}) & 1u ? (IDX){inv[j]} * o_q + oo_{centre} : (IDX){j} * o_q + oo_{k}] '
+                         f'= (T)v; }}')
+        else:
+            L.append('    ' + store('o', 'out', j, f'oo_{k}', 'v') + ' }')
+    L.append('}')
+
+    # ---- entry points
+    args_f = 'src, dst, nbmask, Z, Y, X, s_q, s_z, s_y, s_x, d_q, d_z, d_y, d_x, s_bytes, d_bytes, omega'
+    args_a = ('src, g, out, nbmask, Z, Y, X, s_q, s_z, s_y, s_x, g_q, g_z, g_y, g_x, o_q, o_z, o_y, o_x, s_bytes, '
+              'g_bytes, o_bytes, omega')
+    if hip:
+        for nm, sig, args in (('lbm_fwd', sig_fwd, args_f), ('lbm_adj', sig_adj, args_a)):
+            L.append(f'extern "C" __global__ void __launch_bounds__(256) {nm}({sig})\n{{')
+            L.append('  const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y, z = blockIdx.z;')
+            L.append('  if (x >= X || y >= Y) return;')
+            L.append(f'  {nm}_cell({args}, z, y, x);\n}}')
+    else:
+        for nm, kind in (('lbm_fwd', 'f'), ('lbm_adj', 'a')):
+            # the CPU kernels' ctypes signature (backends.cpu_kernel.compile_c): pointers, extents, strides, -, scalars
+            L.append(f'void {nm}(void** P, const i64* N, const i64* S, const i64* B_, const double* Dv)\n{{')
+            L.append('  (void)B_; const int Z = (int)N[0], Y = (int)N[1], X = (int)N[2];')
+            L.append(f'  const {ct} omega = ({ct})Dv[0];')
+            if kind == 'f':
+                L.append('  const T* src = (const T*)P[0]; T* dst = (T*)P[1]; const unsigned* nbmask = '
+                         '(const unsigned*)P[2];')
+                L.append('  const IDX s_q = S[0], s_z = S[1], s_y = S[2], s_x = S[3], d_q = S[4], d_z = S[5], '
+                         'd_y = S[6], d_x = S[7];')
+                L.append('  const long long s_bytes = 0, d_bytes = 0;')
+                call = f'lbm_fwd_cell({args_f}, z, y, x);'
+            else:
+                L.append('  const T* src = (const T*)P[0]; const T* g = (const T*)P[1]; T* out = (T*)P[2]; '
+                         'const unsigned* nbmask = (const unsigned*)P[3];')
+                L.append('  const IDX s_q = S[0], s_z = S[1], s_y = S[2], s_x = S[3], g_q = S[4], g_z = S[5], '
+                         'g_y = S[6], g_x = S[7], o_q = S[8], o_z = S[9], o_y = S[10], o_x = S[11];')
+                L.append('  const long long s_bytes = 0, g_bytes = 0, o_bytes = 0;')
+                call = f'lbm_adj_cell({args_a}, z, y, x);'
+            L.append('  #pragma omp parallel for collapse(2) schedule(static)')
+            L.append('  for (int z = 0; z < Z; ++z)\n    for (int y = 0; y < Y; ++y)\n      for (int x = 0; x < X; ++x)')
+            L.append(f'        {call}\n}}')
+    return '\n'.join(L) + '\n'
+
+
+def neighbour_mask(flags, stencil, xp):
+    """``uint32`` per cell: bit i set where ``x − c_i`` is an obstacle (periodic), bit ``SELF_BIT`` where ``x`` is
+    one (``flags``: obstacle flags over the domain, numpy or torch)."""
+    is_torch = xp.__name__ == 'torch'
+    f = flags.to(xp.int32) if is_torch else flags.astype(np.int64)
+    m = f * 0
+    for i, c in enumerate(stencil.directions):
+        if not any(c):
+            continue
+        r = f
+        for ax, sh in enumerate(c):
+            if sh:
+                r = xp.roll(r, shifts=sh, dims=ax) if is_torch else np.roll(r, sh, axis=ax)
+        m = m | (r << i)
+    m = m | (f << SELF_BIT)
+    return m.to(xp.int32).contiguous() if is_torch else np.ascontiguousarray(m.astype(np.uint32))
+
+
+def lattice_strides(t, D):
+    """``(s_q, s_z, s_y, s_x)`` in elements of a pdf tensor ``[*spatial, q]`` (2-D: ``s_z`` = 0)."""
+    st = [int(s) for s in (t.stride() if hasattr(t, 'stride') and callable(t.stride) else
+                           [s // t.itemsize for s in t.strides])]
+    sp_ = st[:D]
+    if D == 2:
+        sp_ = [0] + sp_
+    return (st[D],) + tuple(sp_)
+
+
+def row_interleaved_empty(domain, Q, dtype, device):
+    """An uninitialised pdf tensor ``[*domain, Q]`` in the row-interleaved layout ``[z][y][q][x]`` (each lattice
+    row's Q components one contiguous block) — the time-step op's internal states."""
+    import torch
+    dims = list(domain)
+    base = torch.empty(dims[:-1] + [Q, dims[-1]], dtype=dtype, device=device)
+    return base.transpose(-1, -2)
+
+
+class LatticeKernels:
+    """Compiled forward / adjoint lattice kernels of one (stencil, compressible, dtype, walls, target). ``mask``
+    arguments are the cells' neighbour masks (``neighbour_mask``), ``None`` without walls."""
+
+    def __init__(self, stencil, compressible, dtype, walls, target):
+        self.stencil = stencil
+        self.compressible = bool(compressible)
+        self.dtype = np.dtype(dtype)
+        if self.dtype not in (np.float32, np.float64):
+            raise NotImplementedError(f'lattice kernels for {self.dtype} pdfs')
+        self.ct = 'double' if self.dtype == np.float64 else 'float'
+        self.walls = bool(walls)
+        self.target = target
+        self._fns = {}
+
+    def source(self, idx='int', addr='buf'):
+        if self.target != 'gpu':
+            return _emit(self.stencil, self.compressible, self.ct, self.walls, 'c', 'i64', 'ptr')
+        return _emit(self.stencil, self.compressible, self.ct, self.walls, 'hip', idx, addr)
+
+    # -- GPU ---------------------------------------------------------------------------------------
+    def _gpu_fn(self, which, idx, addr, device):
+        key = (which, idx, addr, device)
+        fn = self._fns.get(key)
+        if fn is None:
+            from ..backends import hip_runtime as rt
+            code = rt.compile_hip(self.source(idx, addr), name='psad_lbm.hip')
+            fn = self._fns[key] = rt.load_function(code, f'lbm_{which}', device)
+        return fn
+
+    def build(self):
+        from ..backends import hip_runtime as rt
+        if self.target == 'gpu':
+            return [rt.compile_hip(self.source('int', a), name='psad_lbm.hip') for a in ('buf', 'ptr')]
+        return self._cpu_fn('fwd')
+
+    def _check(self, tensors, mask):
+        D, Q = self.stencil.D, self.stencil.Q
+        shape = tuple(tensors[0].shape)
+        for t in tensors:
+            if tuple(t.shape) != shape or len(shape) != D + 1 or int(shape[D]) != Q:
+                raise ValueError(f'pdf tensors must be [*domain, {Q}] of one shape, got {tuple(t.shape)}')
+            if t.dtype != tensors[0].dtype or not t.is_cuda or t.device != tensors[0].device:
+                raise ValueError('pdf tensors must share dtype and device')
+        if self.walls != (mask is not None):
+            raise ValueError('the wall kernels need the neighbour mask (and the periodic ones none)')
+        if mask is not None and (tuple(mask.shape) != shape[:D] or not mask.is_contiguous()
+                                 or mask.dtype.itemsize != 4 or mask.device != tensors[0].device):
+            raise ValueError(f'neighbour mask of shape {tuple(mask.shape)} does not match the domain {shape[:D]}')
+        if min(shape[:D]) < 2:
+            raise ValueError('the periodic lattice needs at least 2 cells per axis')
+
+    @staticmethod
+    def _reach(t):
+        """Elements from the tensor's base to its last element (+1)."""
+        return sum(abs(int(s)) * (int(n) - 1) for s, n in zip(t.stride(), t.shape)) + 1
+
+    def _mode(self, tensors):
+        reach = max(self._reach(t) for t in tensors)
+        idx = 'int' if reach < 2 ** 31 - 1 else 'long long'
+        esz = tensors[0].element_size()
+        addr = 'buf' if reach * esz < 2 ** 31 and all(min(t.stride()) >= 0 for t in tensors) else 'ptr'
+        if os.environ.get('PSAD_LBM_ADDR') == 'ptr':       # A/B of the addressing modes (probes)
+            addr = 'ptr'
+        return idx, addr
+
+    def _common(self, tensors, mask):
+        self._check(tensors, mask)
+        idx, addr = self._mode(tensors)
+        fn_args = []
+        for t in tensors:
+            fn_args += list(lattice_strides(t, self.stencil.D))
+        return idx, addr, fn_args
+
+    def forward(self, src, dst, omega, mask=None, stream=None):
+        """``dst = stream-pull-collide(src)`` (torch tensors ``[*domain, q]``, any strides)."""
+        if self.target != 'gpu':
+            return self._cpu('fwd', [src, dst], omega, mask)
+        import torch
+        idx, addr, strides = self._common([src, dst], mask)
+        fn = self._gpu_fn('fwd', idx, addr, src.device.index)
+        Z, Y, X = self._extent(src)
+        code = 'i' if idx == 'int' else 'q'
+        args = _pack('QQQiii' + code * 8 + 'qq' + ('d' if self.ct == 'double' else 'f'),
+                     src.data_ptr(), dst.data_ptr(), mask.data_ptr() if mask is not None else 0, Z, Y, X, *strides,
+                     self._reach(src) * src.element_size(), self._reach(dst) * dst.element_size(), float(omega))
+        self._launch(fn, (X, Y, Z), args, src.device.index, stream, torch)
+
+    def adjoint(self, src, g, out, omega, mask=None, stream=None):
+        """``out = (∂ step / ∂ src)ᵀ g`` at the state ``src``."""
+        if self.target != 'gpu':
+            return self._cpu('adj', [src, g, out], omega, mask)
+        import torch
+        idx, addr, strides = self._common([src, g, out], mask)
+        fn = self._gpu_fn('adj', idx, addr, src.device.index)
+        Z, Y, X = self._extent(src)
+        code = 'i' if idx == 'int' else 'q'
+        args = _pack('QQQQiii' + code * 12 + 'qqq' + ('d' if self.ct == 'double' else 'f'),
+                     src.data_ptr(), g.data_ptr(), out.data_ptr(), mask.data_ptr() if mask is not None else 0,
+                     Z, Y, X, *strides, *[self._reach(t) * t.element_size() for t in (src, g, out)], float(omega))
+        self._launch(fn, (X, Y, Z), args, src.device.index, stream, torch)
+
+    def _extent(self, t):
+        shape = [int(n) for n in t.shape[:self.stencil.D]]
+        return [1] + shape if self.stencil.D == 2 else shape
+
+    @staticmethod
+    def _launch(fn, xyz, args, device, stream, torch):
+        from ..backends import hip_runtime as rt
+        X, Y, Z = xyz
+        if stream is None:
+            stream = torch._C._cuda_getCurrentRawStream(device)
+        rt.launch(fn, (-(-X // 64), -(-Y // 4), Z), (64, 4, 1), args, stream)
+
+    # -- CPU ---------------------------------------------------------------------------------------
+    def _cpu_fn(self, which):
+        fn = self._fns.get(which)
+        if fn is None:
+            from ..backends.cpu_kernel import compile_c
+            fn = self._fns[which] = compile_c(self.source(), f'lbm_{which}', openmp=True)
+        return fn
+
+    def _cpu(self, which, arrays, omega, mask):
+        arrays = [np.asarray(a) for a in arrays]
+        for a in arrays:
+            if a.dtype != self.dtype:
+                raise TypeError(f'pdf arrays must be {self.dtype}, got {a.dtype}')
+        D = self.stencil.D
+        shape = tuple(arrays[0].shape)
+        for a in arrays:
+            if tuple(a.shape) != shape or int(shape[D]) != self.stencil.Q:
+                raise ValueError('pdf arrays must be [*domain, q] of one shape')
+        if self.walls != (mask is not None):
+            raise ValueError('the wall kernels need the neighbour mask (and the periodic ones none)')
+        m = None
+        if mask is not None:
+            m = np.ascontiguousarray(mask, dtype=np.uint32)
+            if m.shape != shape[:D]:
+                raise ValueError('neighbour mask does not match the domain')
+        fn = self._cpu_fn(which)
+        ptrs = [a.ctypes.data for a in arrays] + [m.ctypes.data if m is not None else 0]
+        strides = []
+        for a in arrays:
+            strides += list(lattice_strides(a, D))
+        ext = list(shape[:D]) if D == 3 else [1] + list(shape[:D])
+        P = (ctypes.c_void_p * len(ptrs))(*ptrs)
+        N = (ctypes.c_longlong * 3)(*ext)
+        S = (ctypes.c_longlong * len(strides))(*strides)
+        B = (ctypes.c_longlong * 1)(0)
+        Dv = (ctypes.c_double * 1)(float(omega))
+        fn(P, N, S, B, Dv)
+
+
+def _pack(fmt, *vals):
+    """Kernel arguments at natural alignment (``HIP_LAUNCH_PARAM_BUFFER``)."""
+    out, off = b'', 0
+    for c, v in zip(fmt, vals):
+        size = struct.calcsize(c)
+        pad = (-off) % size
+        out += b'\0' * pad + struct.pack('<' + c, v)
+        off += pad + size
+    return out + b'\0' * ((-off) % 8)

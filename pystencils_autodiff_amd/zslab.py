@@ -385,16 +385,7 @@ class ZSlabOp:
                 raise ValueError(f"slab of {t.shape[0]} planes is thinner than the stencil radius {rz}")
             if not t.is_contiguous():
                 raise ValueError(f"slab of '{name}' must be contiguous for the RCCL face exchange")
-            key = ('rccl', name, rz, t.dtype, t.shape, t.device)      # per radius: fwd and bwd may differ
-            bufs = self._bufs.get(key)
-            if bufs is None:
-                shape = (rz,) + tuple(t.shape[1:])
-                plane = t[0].numel() * t.element_size()
-                bufs = (torch.empty(shape, dtype=t.dtype, device=t.device) if peer_lo >= 0 else None,
-                        torch.empty(shape, dtype=t.dtype, device=t.device) if peer_hi >= 0 else None,
-                        rz * plane, (t.shape[0] - rz) * plane)
-                self._bufs[key] = bufs
-            lo, hi, nbytes, last_off = bufs
+            lo, hi, nbytes, last_off = self._recv_bufs(halo, name, rz, tuple(t.shape), t.dtype, t.device)
             first = t.data_ptr()
             last = first + last_off
             if halo.loopback:
@@ -406,6 +397,25 @@ class ZSlabOp:
             t.record_stream(halo.stream)
             halos[name] = (lo, hi)
         return planes, halos
+
+    def _recv_bufs(self, halo, name, rz, shape, dtype, device):
+        """The receive buffers of field ``name``'s halos (cached per field, radius, dtype, shape, device: the
+        forward and the adjoint sweep may read a field at different radii), its face bytes and the byte offset
+        of its last ``rz`` planes."""
+        peer_lo, peer_hi = self._peers(halo)
+        key = ('rccl', name, rz, dtype, tuple(shape), device)
+        bufs = self._bufs.get(key)
+        if bufs is None:
+            hshape = (rz,) + tuple(shape[1:])
+            esize = torch.empty((), dtype=dtype).element_size()
+            plane = esize
+            for n in shape[1:]:
+                plane *= int(n)
+            bufs = (torch.empty(hshape, dtype=dtype, device=device) if peer_lo >= 0 else None,
+                    torch.empty(hshape, dtype=dtype, device=device) if peer_hi >= 0 else None,
+                    rz * plane, (int(shape[0]) - rz) * plane)
+            self._bufs[key] = bufs
+        return bufs
 
     def warm_exchange(self, **slabs):
         """One face exchange of the given slabs (``name=tensor``, stencil field names) with no compute:
@@ -518,5 +528,194 @@ class ZSlabOp:
                 zop.bwd(**kw)
                 return tuple(res.get(adj[f.name]) for f in fwd_inputs[:ctx.n_inputs])
 
+        native = _NativeSlab(self, fwd_inputs, fwd_outputs, fwd_read, bwd_outputs, bwd_read, adj, tdtype)
+        function_apply = torch.autograd.Function.apply.__func__
+
+        def apply(cls, *args, **kwargs):
+            """``apply(*slabs)``: through the native slab node (``_psad_torch``: the whole sweep — RCCL group,
+            stream events, interior and face launches — without Python) when the call fits its plan, else the
+            Python Function above (same launches, same results)."""
+            if not kwargs:
+                outs = native(args, cls.class_kwargs)
+                if outs is not None:
+                    return outs
+            return function_apply(cls, *args, **kwargs)
+        ZSlabFunction.apply = classmethod(apply)
         ZSlabFunction.__name__ = f"{op.op_name}_zslab"
         return ZSlabFunction
+
+
+class _NativeSlab:
+    """The slab Function's forward and backward sweeps as one C++ autograd node (``_psad_torch.apply_slab``,
+    ``csrc/psad_torch.cpp`` "z-slab sweeps"). A plan per input signature (shapes, dtypes, device) holds, for
+    each sweep, the interior and face launches (argument templates resolved by the kernels' own ``prepare``
+    on stand-in pointers, the receive buffers' halo pointers baked in) and the RCCL exchange (receive
+    buffers, bytes, peers, the communicator and halo stream of :class:`RcclHalo`). Calls it cannot express take
+    the Python Function: no RCCL communicator (gloo, the emulated-rank tests' stand-in), an interior-only
+    (``boundary_handling=None``) kernel, a stencil radius of 0, inputs that are not contiguous 32-byte-aligned
+    device tensors."""
+
+    def __init__(self, zop, fwd_inputs, fwd_outputs, fwd_read, bwd_outputs, bwd_read, adj, tdtype):
+        self.zop = zop
+        self.fwd_inputs, self.fwd_outputs = fwd_inputs, fwd_outputs
+        self.fwd_read, self.bwd_outputs, self.bwd_read = fwd_read, bwd_outputs, bwd_read
+        self.adj, self.tdtype = adj, tdtype
+        self.plans = {}
+        self.keep = []                      # receive buffers the plans point at
+
+    def __call__(self, args, class_kwargs):
+        from .backends._torch_native import native_module
+        zop = self.zop
+        halo = zop._halo
+        if not isinstance(halo, RcclHalo) or native_module() is None or os.environ.get('PSAD_NATIVE_SLAB', '1') == '0':
+            return None
+        if len(args) != len(self.fwd_inputs) or not args or not all(isinstance(a, torch.Tensor) for a in args):
+            return None
+        names = sorted({s.name for k in zop.kernels.values() for s in k.ir.scalars})
+        try:
+            scal = [float(class_kwargs[n]) for n in names]
+        except (KeyError, TypeError, ValueError):
+            return None
+        a0 = args[0]
+        key = (tuple(a0.shape), a0.dtype, a0.device)
+        pid = self.plans.get(key)
+        if pid is None:
+            try:
+                pid = self._build(args, names, halo)
+            except (TypeError, ValueError):
+                pid = None
+            self.plans[key] = -1 if pid is None else pid
+        if pid is None or pid < 0:
+            return None
+        outs = native_module().apply_slab(pid, list(args), scal)
+        return None if outs is None else tuple(outs)
+
+    def _build(self, args, scalar_names, halo):
+        import struct
+
+        from .backends._torch_native import _SCALAR_TYPE, native_module
+        from .backends.hip_kernel import _Plane
+        zop = self.zop
+        fk, bk = zop.kernels['forward'], zop.kernels['backward']
+        for k in (fk, bk):
+            if not (k.ir.zeros or k.ir.ghost_layers == 0):
+                return None                 # interior-only kernels: border fills and global z limits
+        for a in args:
+            if not a.is_cuda or not a.is_contiguous() or a.data_ptr() % 32 or a.device != args[0].device or \
+                    str(a.dtype).replace('torch.', '') not in _SCALAR_TYPE or tuple(a.shape) != tuple(args[0].shape):
+                return None
+        dev = args[0].device
+        shape = tuple(int(n) for n in args[0].shape)
+        zl = shape[0]
+        seeds, fake = {}, [0]
+
+        def stand_in(dtype):
+            if dtype not in seeds:
+                seeds[dtype] = torch.empty(1, dtype=dtype, device=dev)
+            st, acc = [], 1
+            for n in reversed(shape):
+                st.insert(0, acc)
+                acc *= n
+            fake[0] += 1
+            return _Plane(seeds[dtype], fake[0] << 40, shape, tuple(st))
+
+        scal = {n: 1.0 for n in scalar_names}
+
+        def sweep(which, kw, table):
+            k = zop.kernels[which]
+            _, stencil, rz = zop._meta.get(which) or (None, k.ir.stencil_fields,
+                                                      max([zop._radius(k, f) for f in k.ir.stencil_fields] + [0]))
+            if rz == 0:
+                return None
+            compiled = k.compile()
+            inner, faces = zop._launches(zl, rz, (0, zl))
+            halos, ex_slot, ex_off, rlo, rhi, nbytes = {}, [], [], [], [], []
+            for f in stencil:
+                if f.name not in kw:
+                    return None
+                lo, hi, nb, last = zop._recv_bufs(halo, f.name, rz, shape, self.tdtype(f), dev)
+                self.keep.append((lo, hi))
+                halos[f.name] = (lo, hi)
+                ex_slot.append(table.index(f.name))
+                ex_off.append(last)
+                rlo.append(lo.data_ptr() if lo is not None else 0)
+                rhi.append(hi.data_ptr() if hi is not None else 0)
+                nbytes.append(nb)
+
+            def resolve(**extra):
+                prep = compiled.prepare(**kw, **scal, **extra)
+                if prep is None:
+                    return None
+                fn, grid, block, packed, xb, _ = prep
+                fnames = [f[0] for f in compiled._field_specs()]
+                if grid == 0 or xb or any(n not in table for n in fnames):
+                    return None
+                if list(struct.unpack_from(f'<{len(fnames)}Q', packed)) != [kw[n].data_ptr() for n in fnames]:
+                    return None
+                sn = [sc.name for sc in compiled.ir.scalars]
+                slots = [[off, int(f64), scalar_names.index(n)]
+                         for (off, f64), n in zip(compiled.last_plan.scalar_slots(len(sn)), sn)]
+                return (int(fn), int(grid), int(block), bytes(packed), [table.index(n) for n in fnames], slots)
+            inner_l = resolve(z_range=inner) if inner else None
+            if inner and inner_l is None:
+                return None
+            if len(faces) == 2 and faces[0][1] - faces[0][0] == faces[1][1] - faces[1][0]:
+                face_l = [resolve(halos=halos, z_range=tuple(faces))]
+            else:
+                face_l = [resolve(halos=halos, z_range=f) for f in faces]
+            if any(f is None for f in face_l):
+                return None
+            peer_lo, peer_hi = zop._peers(halo)
+            ex = (ex_slot, ex_off, rlo, rhi, nbytes, peer_lo, peer_hi, bool(halo.loopback))
+            return inner_l, face_l, ex
+
+        def allocs(outs, read, kw):
+            shapes, dtypes, zero, names = [], [], [], []
+            for f in outs:
+                dt = self.tdtype(f)
+                if str(dt).replace('torch.', '') not in _SCALAR_TYPE:
+                    return None
+                kw[f.name] = stand_in(dt)
+                shapes.append(list(shape))
+                dtypes.append(_SCALAR_TYPE[str(dt).replace('torch.', '')])
+                zero.append(f.name in read)
+                names.append(f.name)
+            return shapes, dtypes, zero, names
+        fwd_names = {f.name for f in fk.ir.fields}
+        kw = {}
+        in_names = [f.name for f in self.fwd_inputs]
+        for name, a in zip(in_names, args):
+            kw[name] = stand_in(a.dtype)
+        fo = allocs(self.fwd_outputs, self.fwd_read, kw)
+        if fo is None:
+            return None
+        fwd_table = in_names + fo[3]
+        fkw = {n: v for n, v in kw.items() if n in fwd_names}
+        fs = sweep('forward', fkw, fwd_table)
+        if fs is None:
+            return None
+        bwd_names = {f.name for f in bk.ir.fields}
+        saved = [n for n in in_names + fo[3] if n in bwd_names]
+        bkw = {n: kw[n] for n in saved}
+        grad_names = []
+        for i, f in enumerate(self.fwd_outputs):
+            a = self.adj[f.name]
+            grad_names.append(a if a in bwd_names else f'\0grad{i}')
+            if a in bwd_names:
+                bkw[a] = stand_in(self.tdtype(f))
+        bo_fields = [next(g for g in bk.ir.fields if g.name == n) for n in self.bwd_outputs]
+        bo = allocs(bo_fields, self.bwd_read, bkw)
+        if bo is None:
+            return None
+        bwd_table = saved + grad_names + bo[3]
+        bs = sweep('backward', {n: v for n, v in bkw.items() if n in bwd_names}, bwd_table)
+        if bs is None:
+            return None
+        grad_of_input = [bwd_table.index(self.adj[n], len(saved) + len(grad_names))
+                         if self.adj.get(n) in bo[3] else -1 for n in in_names]
+        return native_module().register_slab_plan(
+            'zslab', dev.index, [list(a.shape) for a in args],
+            [_SCALAR_TYPE[str(a.dtype).replace('torch.', '')] for a in args],
+            fo[0], fo[1], fo[2], fs[0], fs[1], fs[2], [fwd_table.index(n) for n in saved],
+            bo[0], bo[1], bo[2], bs[0], bs[1], bs[2], grad_of_input, len(scalar_names),
+            int(halo.comm.value), int(halo._stream_handle))

@@ -48,9 +48,14 @@ def main():
         print(f'{name:24s} {wl} {zl}x{n}^2: {wall:.4f} ms/step wall, {host:.4f} ms/step host enqueue, '
               f'implied N={n // zl} {n}^3 rate {n**3 / (wall * 1e-3) / 1e6:,.0f} Mcells/s')
     torch.autograd.set_multithreading_enabled(False)
-    wall, host = timed(zfn, u, d)
-    print(f'zslab, autograd 1 thread  : {wall:.4f} ms/step wall, {host:.4f} ms/step host enqueue, '
-          f'implied N={n // zl} {n}^3 rate {n**3 / (wall * 1e-3) / 1e6:,.0f} Mcells/s')
+    import os
+    for native in ('1', '0', '1', '0'):
+        # the slab Function through the native node (csrc/psad_torch.cpp "z-slab sweeps") or the Python sweeps
+        os.environ['PSAD_NATIVE_SLAB'] = native
+        wall, host = timed(zfn, u, d)
+        print(f'zslab {"native" if native == "1" else "python"}, autograd 1 thread: {wall:.4f} ms/step wall, '
+              f'{host:.4f} ms/step host enqueue, implied N={n // zl} {n}^3 rate '
+              f'{n**3 / (wall * 1e-3) / 1e6:,.0f} Mcells/s', flush=True)
     zop.close()
 
 

@@ -415,3 +415,56 @@ def test_zslab_full_size_eight_ranks_emulated(builder_name, edge, tmp_path):
     assert fin_o == world and fin_d == world
     assert mass > 0
     assert abs(ad - ua) <= (5e-3 if f16 else 1e-5) * max(abs(ad), abs(ua)), (ad, ua)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('builder_name,shape', [('asym_7pt', (12, 40, 70)), ('diffusion_7pt', (2, 9, 64)),
+                                                ('stencil_27pt', (9, 24, 80)), ('stencil_27pt', (96, 64, 256))])
+def test_zslab_native_node_loopback(builder_name, shape, monkeypatch):
+    """The slab Function through the native node (``_psad_torch.apply_slab``: RCCL group, stream events, interior
+    and face launches in C++) on a loopback communicator: the periodic-z oracle, and bitwise the Python Function's
+    sweeps (``PSAD_NATIVE_SLAB=0``) on the same inputs; a second call reuses the plan."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import pystencils_autodiff_amd as pa
+    from oracle import stencils as S
+    from pystencils_autodiff_amd import _psad_torch
+    from pystencils_autodiff_amd import workloads as W
+    from pystencils_autodiff_amd.zslab import RcclHalo, ZSlabOp
+    from tests.conftest import assert_close_rel
+    op = pa.AutoDiffOp(getattr(W, builder_name)(), boundary_handling='zeros')
+    taps = {'diffusion_7pt': S.taps_diffusion_7pt(), 'asym_7pt': S.taps_asym_7pt(),
+            'stencil_27pt': S.taps_27pt()}[builder_name]
+    dt = np.float16 if builder_name == 'stencil_27pt' else np.float32
+    tol = 1e-3 if dt == np.float16 else 1e-6
+    rng = np.random.default_rng(6)
+    u = rng.uniform(0, 1, shape).astype(dt)
+    d = rng.uniform(-1, 1, shape).astype(dt)
+    z = ZSlabOp(op, use_cuda=True)
+    z._halo = RcclHalo(loopback=True)
+    try:
+        tu, td = torch.from_numpy(u).cuda(), torch.from_numpy(d).cuda()
+        z.warm_exchange(u=tu, diffout=td)
+        fn = z.autograd_function()
+        n0 = _psad_torch.num_slab_plans()
+        res = []
+        for native in ('1', '1', '0'):
+            monkeypatch.setenv('PSAD_NATIVE_SLAB', native)
+            uu = tu.clone().requires_grad_(True)
+            (o,) = fn.apply(uu)
+            assert ('SlabFunction' in o.grad_fn.name()) == (native == '1'), o.grad_fn.name()
+            o.backward(td)
+            torch.cuda.synchronize()
+            res.append((o.detach().clone(), uu.grad.clone()))
+        assert _psad_torch.num_slab_plans() == n0 + 1
+        assert torch.equal(res[0][0], res[2][0]) and torch.equal(res[0][1], res[2][1])
+        assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+        def periodic(a, tp):
+            a64 = a.astype(np.float64)
+            ext = np.concatenate([a64[-1:], a64, a64[:1]])
+            return S.linear_stencil(ext, tp)[1:-1]
+        assert_close_rel(res[0][0].cpu().numpy(), periodic(u, taps), tol, 'out')
+        assert_close_rel(res[0][1].cpu().numpy(), periodic(d, S.flip(taps)), tol, 'diffu')
+    finally:
+        z.close()

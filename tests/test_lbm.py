@@ -109,9 +109,13 @@ GPU_CASES = [('D2Q9', (40, 33), False, 'fzyx', 'float64'), ('D2Q9', (37, 64), Tr
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('schedule', ['lattice', 'autodiffop'])
 @pytest.mark.parametrize('stencil,shape,compressible,layout,dtype', GPU_CASES)
-def test_lbm_steps_gpu_vs_oracle(stencil, shape, compressible, layout, dtype):
+def test_lbm_steps_gpu_vs_oracle(stencil, shape, compressible, layout, dtype, schedule, monkeypatch):
+    """T steps and T adjoint steps on the owned arrays, through the lattice schedule and through the rule's
+    AutoDiffOp kernels (PSAD_LBM_LATTICE=0), against the oracle and torch's reverse mode through it."""
     import torch
+    monkeypatch.setenv('PSAD_LBM_LATTICE', '1' if schedule == 'lattice' else '0')
     rule = lbm.create_lb_update_rule(stencil, compressible=compressible, layout=layout, data_type=dtype)
     step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.3, target='gpu')
     f0 = _init(stencil, shape, compressible)
@@ -128,8 +132,9 @@ def test_lbm_steps_gpu_vs_oracle(stencil, shape, compressible, layout, dtype):
     step.run_backward(T)
     gg = step.adjoint_pdf_array.double().cpu().numpy()
     assert np.abs(gg - gref).max() <= tol * 10 * np.abs(gref).max()
+    assert (step._lattice is not None) == (schedule == 'lattice')
     kf = step.autodiff_op.forward_ast_gpu.compile()
-    if layout == 'fzyx':
+    if layout == 'fzyx' and schedule == 'autodiffop':
         assert kf.last_variant[0] == 'generic'       # SoA components: one-thread-per-cell streaming schedule
 
 
@@ -227,3 +232,169 @@ def test_periodic_boundary_gpu():
     rhs = float((x.detach() * x.grad).sum())
     assert abs(lhs - rhs) < 1e-11 * float(g.abs().sum())
     assert op.forward_ast_gpu.compile().last_variant[0] == 'generic'
+
+
+# --------------------------------------------------------------------------------------------------------
+# walls (NoSlip, set_boundary_including_adjoint) and the end-to-end op (_autodiff_lbstep.py:162-187, 310-334)
+# --------------------------------------------------------------------------------------------------------
+def _channel(shape, obstacle=True):
+    """A channel: walls on the first and last rows of axis 1, plus a small obstacle (bool mask)."""
+    wall = np.zeros(shape, bool)
+    wall[:, 0] = True
+    wall[:, -1] = True
+    if obstacle:
+        c = tuple(n // 3 for n in shape)
+        wall[tuple(slice(k, k + 2) for k in c)] = True
+    return wall
+
+
+def _set_channel(step, shape, obstacle=True):
+    step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[:, 0])
+    step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[:, -1])
+    if obstacle:
+        c = [n // 3 for n in shape]
+        # the obstacle through a mask callback over cell midpoints (axis 0 first), lbmpy's convention
+        step.set_boundary_including_adjoint(
+            lbm.NoSlip('obstacle'), mask_callback=lambda *m: np.logical_and.reduce(
+                [(mi > ci) & (mi < ci + 2) for mi, ci in zip(m, c)]))
+
+
+@pytest.mark.parametrize('stencil,shape,compressible,layout', [('D2Q9', (12, 9), True, 'fzyx'),
+                                                              ('D2Q9', (10, 8), False, 'numpy'),
+                                                              ('D3Q19', (7, 8, 6), False, 'fzyx')])
+def test_lbm_walls_cpu_vs_oracle(stencil, shape, compressible, layout):
+    """No-slip channel with an obstacle: T forward steps vs the array-roll + bounce-back restatement, the
+    adjoint of T steps vs torch's reverse mode through it, the flags equal the mask the API was given."""
+    import torch
+    rule = lbm.create_lb_update_rule(stencil, compressible=compressible, layout=layout)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.2, target='cpu')
+    _set_channel(step, shape)
+    wall = _channel(shape)
+    assert np.array_equal(step.boundary_handling.flags.astype(bool), wall)
+    f0 = _init(stencil, shape, compressible, seed=7)
+    T = 4
+    step.set_pdfs(f0)
+    step.run(T, record=True)
+    ft = torch.tensor(f0, requires_grad=True)
+    ref = OL.run_walls(ft, 1.2, torch.tensor(wall), T, stencil, compressible, xp=torch)
+    assert np.abs(step.pdf_array - ref.detach().numpy()).max() <= 1e-13 * np.abs(f0).max()
+    g = np.random.default_rng(8).standard_normal(f0.shape)
+    (gref,) = torch.autograd.grad(ref, ft, torch.tensor(g))
+    step.set_adjoint_pdfs(g)
+    step.run_backward(T)
+    assert np.abs(step.adjoint_pdf_array - gref.numpy()).max() <= 1e-12 * np.abs(gref.numpy()).max()
+
+
+def test_lbm_walls_api():
+    rule = lbm.create_lb_update_rule('D2Q9')
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=(6, 5), relaxation_rate=1.0, target='cpu')
+    assert step.backward_boundary_handling is step.boundary_handling
+    step.set_boundary_including_adjoint(lbm.NoSlip(), mask_array=np.eye(6, 5, dtype=bool))
+    assert np.array_equal(step.boundary_handling.flags, np.eye(6, 5, dtype=np.uint8))
+    step.boundary_handling.set_boundary('domain', lbm.make_slice[2:, :])
+    assert step.boundary_handling.flags.sum() == 2
+    step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[4, 1:3],
+                                        adjoint_boundary_condition=lbm.AdjointNoSlip())
+    assert step.boundary_handling.flags[4, 1:3].all() and step.boundary_handling.flags.sum() == 4
+    with pytest.raises(NotImplementedError):
+        step.set_boundary_including_adjoint('UBB')
+    with pytest.raises(NotImplementedError):
+        lbm.AdjointBoundaryCondition(object())
+    assert lbm.AdjointBoundaryCondition(lbm.NoSlip()) == lbm.AdjointBoundaryCondition(lbm.NoSlip())
+
+
+def test_lbm_end_to_end_op_cpu():
+    """rho, u → equilibrium → T steps (channel walls) → rho, u: values vs the oracle chain, gradients of a
+    scalar loss w.r.t. rho and u vs torch's reverse mode through the oracle chain."""
+    import torch
+    shape, T = (10, 8), 4
+    rule = lbm.create_lb_update_rule('D2Q9', compressible=True)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.4, target='cpu')
+    _set_channel(step, shape, obstacle=False)
+    rng = np.random.default_rng(12)
+    rho0 = 1 + 0.05 * rng.standard_normal(shape)
+    u0 = 0.03 * rng.standard_normal(shape + (2,))
+    rho = torch.tensor(rho0, requires_grad=True)
+    vel = torch.tensor(u0, requires_grad=True)
+    res = step.create_end_to_end_op(T, vel, rho, num_times_steps_without_save=1)
+    w = torch.tensor(rng.standard_normal(shape + (2,)))
+    loss = (res.output_velocity_tensor * w).sum() + (res.output_density_tensor ** 2).sum()
+    loss.backward()
+    rt, vt = torch.tensor(rho0, requires_grad=True), torch.tensor(u0, requires_grad=True)
+    f = OL.equilibrium(rt, vt, 'D2Q9', True, xp=torch)
+    f = OL.run_walls(f, 1.4, torch.tensor(_channel(shape, False)), T, 'D2Q9', True, xp=torch)
+    r_ref = f.sum(-1)
+    dirs = OL.D2Q9[0]
+    v_ref = torch.stack([sum(c[a] * f[..., i] for i, c in enumerate(dirs)) / r_ref for a in range(2)], -1)
+    l_ref = (v_ref * w).sum() + (r_ref ** 2).sum()
+    l_ref.backward()
+    assert abs(float(loss) - float(l_ref)) <= 1e-12 * abs(float(l_ref))
+    assert torch.allclose(rho.grad, rt.grad, rtol=0, atol=1e-11 * float(rt.grad.abs().max()))
+    assert torch.allclose(vel.grad, vt.grad, rtol=0, atol=1e-11 * float(vt.grad.abs().max()))
+    assert res.input_pdf_tensor.shape == shape + (9,)
+
+
+# --- GPU: the lattice schedule ---------------------------------------------------------------------------
+LATTICE_GPU_CASES = [('D2Q9', (64, 48), True, 'fzyx', 'float32', True), ('D2Q9', (37, 70), False, 'numpy', 'float64', True),
+                     ('D3Q19', (20, 17, 70), False, 'fzyx', 'float32', True),
+                     ('D3Q19', (16, 12, 24), True, 'fzyx', 'float64', False),
+                     ('D3Q27', (10, 9, 66), True, 'fzyx', 'float64', True)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('stencil,shape,compressible,layout,dtype,walls', LATTICE_GPU_CASES)
+def test_lbm_lattice_schedule_gpu_vs_oracle(stencil, shape, compressible, layout, dtype, walls):
+    """The timestep op on the lattice schedule (walls or periodic, fzyx / AoS pdfs, fp32 / fp64): forward vs the
+    oracle, the adjoint vs torch's reverse mode through it; the op's internal states are row-interleaved
+    (their layout never reaches the caller: output and gradient come back in the field's layout)."""
+    import torch
+    if stencil == 'D3Q27':
+        pytest.importorskip('torch')
+        OL.SETS.setdefault('D3Q27', (lbm.LBStencil('D3Q27').directions,
+                                     [__import__('fractions').Fraction(str(w)) for w in lbm.LBStencil('D3Q27').weights]))
+    rule = lbm.create_lb_update_rule(stencil, compressible=compressible, layout=layout, data_type=dtype)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.3, target='gpu')
+    wall = _channel(shape) if walls else np.zeros(shape, bool)
+    if walls:
+        _set_channel(step, shape)
+    Op = step.create_timestep_op(5)
+    f0 = _init(stencil, shape, compressible, seed=4) if stencil != 'D3Q27' else \
+        OL.equilibrium(np.ones(shape), np.zeros(shape + (3,)), 'D3Q27', compressible) + \
+        0.01 * np.random.default_rng(4).standard_normal(shape + (27,))
+    tdt = getattr(torch, dtype)
+    x = torch.tensor(f0, dtype=tdt, device='cuda', requires_grad=True)
+    out = Op.apply(x)
+    assert out.stride() == step.empty_pdfs().stride()
+    ft = torch.tensor(f0, requires_grad=True, device='cuda')
+    ref = OL.run_walls(ft, 1.3, torch.tensor(wall, device='cuda'), 5, stencil, compressible, xp=torch)
+    tol = 1e-12 if dtype == 'float64' else 1e-5
+    assert float((out.double() - ref).abs().max()) <= tol * float(ref.abs().max())
+    g = torch.tensor(np.random.default_rng(5).standard_normal(f0.shape), device='cuda')
+    out.backward(g.to(tdt))
+    (gref,) = torch.autograd.grad(ref, ft, g)
+    assert x.grad.stride() == step.empty_pdfs().stride() or layout == 'numpy'
+    assert float((x.grad.double() - gref).abs().max()) <= 10 * tol * float(gref.abs().max())
+
+
+@pytest.mark.gpu
+def test_lbm_end_to_end_op_gpu():
+    import torch
+    shape, T = (96, 64), 6
+    rule = lbm.create_lb_update_rule('D2Q9', compressible=True, data_type='float64')
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.6, target='gpu')
+    _set_channel(step, shape)
+    rng = np.random.default_rng(13)
+    rho0, u0 = 1 + 0.05 * rng.standard_normal(shape), 0.03 * rng.standard_normal(shape + (2,))
+    rho = torch.tensor(rho0, requires_grad=True, device='cuda')
+    vel = torch.tensor(u0, requires_grad=True, device='cuda')
+    res = step.create_end_to_end_op(T, vel, rho, num_times_steps_without_save=2)
+    loss = (res.output_velocity_tensor[..., 0] ** 2).sum() + res.output_density_tensor.sum()
+    loss.backward()
+    rt, vt = torch.tensor(rho0, requires_grad=True, device='cuda'), torch.tensor(u0, requires_grad=True, device='cuda')
+    f = OL.equilibrium(rt, vt, 'D2Q9', True, xp=torch)
+    f = OL.run_walls(f, 1.6, torch.tensor(_channel(shape), device='cuda'), T, 'D2Q9', True, xp=torch)
+    r_ref = f.sum(-1)
+    ux = sum(c[0] * f[..., i] for i, c in enumerate(OL.D2Q9[0])) / r_ref
+    (ux ** 2).sum().add(r_ref.sum()).backward()
+    assert torch.allclose(rho.grad, rt.grad, rtol=0, atol=1e-10 * float(rt.grad.abs().max()))
+    assert torch.allclose(vel.grad, vt.grad, rtol=0, atol=1e-10 * float(vt.grad.abs().max()))
