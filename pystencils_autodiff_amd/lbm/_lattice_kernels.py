@@ -263,11 +263,19 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
     args_a = ('src, g, out, nbmask, Z, Y, X, s_q, s_z, s_y, s_x, g_q, g_z, g_y, g_x, o_q, o_z, o_y, o_x, s_bytes, '
               'g_bytes, o_bytes, omega')
     if hip:
+        # a block = 64 x-adjacent cells of 4 lattice rows, ``rb`` times over consecutive row groups (rows counted
+        # over (z, y)): the wave's setup (kernel arguments, descriptors, scalar offsets) serves rb cells per lane
         for nm, sig, args in (('lbm_fwd', sig_fwd, args_f), ('lbm_adj', sig_adj, args_a)):
-            L.append(f'extern "C" __global__ void __launch_bounds__(256) {nm}({sig})\n{{')
-            L.append('  const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y, z = blockIdx.z;')
-            L.append('  if (x >= X || y >= Y) return;')
-            L.append(f'  {nm}_cell({args}, z, y, x);\n}}')
+            L.append(f'extern "C" __global__ void __launch_bounds__(256) {nm}({sig}, const int rb)\n{{')
+            L.append('  const int x = blockIdx.x * 64 + threadIdx.x;')
+            L.append('  if (x >= X) return;')
+            L.append('  const int rows = Y * Z;')
+            L.append('  for (int it = 0; it < rb; ++it) {')
+            L.append('    const int r = (blockIdx.y * rb + it) * 4 + threadIdx.y;')
+            L.append('    if (r >= rows) break;')
+            L.append('    const int z = r / Y, y = r - z * Y;')
+            L.append(f'    {nm}_cell({args}, z, y, x);')
+            L.append('  }\n}')
     else:
         for nm, kind in (('lbm_fwd', 'f'), ('lbm_adj', 'a')):
             # the CPU kernels' ctypes signature (backends.cpu_kernel.compile_c): pointers, extents, strides, -, scalars
@@ -414,10 +422,11 @@ class LatticeKernels:
         fn = self._gpu_fn('fwd', idx, addr, src.device.index)
         Z, Y, X = self._extent(src)
         code = 'i' if idx == 'int' else 'q'
-        args = _pack('QQQiii' + code * 8 + 'qq' + ('d' if self.ct == 'double' else 'f'),
+        rb, gy = self._rows_per_block(X, Y, Z)
+        args = _pack('QQQiii' + code * 8 + 'qq' + ('d' if self.ct == 'double' else 'f') + 'i',
                      src.data_ptr(), dst.data_ptr(), mask.data_ptr() if mask is not None else 0, Z, Y, X, *strides,
-                     self._reach(src) * src.element_size(), self._reach(dst) * dst.element_size(), float(omega))
-        self._launch(fn, (X, Y, Z), args, src.device.index, stream, torch)
+                     self._reach(src) * src.element_size(), self._reach(dst) * dst.element_size(), float(omega), rb)
+        self._launch(fn, X, gy, args, src.device.index, stream, torch)
 
     def adjoint(self, src, g, out, omega, mask=None, stream=None):
         """``out = (∂ step / ∂ src)ᵀ g`` at the state ``src``."""
@@ -428,22 +437,31 @@ class LatticeKernels:
         fn = self._gpu_fn('adj', idx, addr, src.device.index)
         Z, Y, X = self._extent(src)
         code = 'i' if idx == 'int' else 'q'
-        args = _pack('QQQQiii' + code * 12 + 'qqq' + ('d' if self.ct == 'double' else 'f'),
+        rb, gy = self._rows_per_block(X, Y, Z)
+        args = _pack('QQQQiii' + code * 12 + 'qqq' + ('d' if self.ct == 'double' else 'f') + 'i',
                      src.data_ptr(), g.data_ptr(), out.data_ptr(), mask.data_ptr() if mask is not None else 0,
-                     Z, Y, X, *strides, *[self._reach(t) * t.element_size() for t in (src, g, out)], float(omega))
-        self._launch(fn, (X, Y, Z), args, src.device.index, stream, torch)
+                     Z, Y, X, *strides, *[self._reach(t) * t.element_size() for t in (src, g, out)], float(omega), rb)
+        self._launch(fn, X, gy, args, src.device.index, stream, torch)
 
     def _extent(self, t):
         shape = [int(n) for n in t.shape[:self.stencil.D]]
         return [1] + shape if self.stencil.D == 2 else shape
 
     @staticmethod
-    def _launch(fn, xyz, args, device, stream, torch):
+    def _rows_per_block(X, Y, Z):
+        """Row groups (4 rows) per block and the grid's y extent: ~8192 blocks (32 per CU), at most 16 groups."""
+        groups = -(-(Y * Z) // 4)
+        xb = -(-X // 64)
+        rb = int(os.environ.get('PSAD_LBM_RB', 0)) or max(1, min(16, -(-groups * xb // 8192)))
+        return rb, -(-groups // rb)
+
+    @staticmethod
+    def _launch(fn, X, gy, args, device, stream, torch):
         from ..backends import hip_runtime as rt
-        X, Y, Z = xyz
         if stream is None:
             stream = torch._C._cuda_getCurrentRawStream(device)
-        rt.launch(fn, (-(-X // 64), -(-Y // 4), Z), (64, 4, 1), args, stream)
+        # (PSAD_LBM_LDS: dynamic LDS per block, i.e. fewer resident blocks per CU — occupancy A/B in the probes)
+        rt.launch(fn, (-(-X // 64), gy), (64, 4, 1), args, stream, int(os.environ.get('PSAD_LBM_LDS', 0)))
 
     # -- CPU ---------------------------------------------------------------------------------------
     def _cpu_fn(self, which):

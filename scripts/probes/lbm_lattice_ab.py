@@ -61,11 +61,13 @@ def main():
         wall[:, 0] = 1
         wall[:, -1] = 1
         mask = neighbour_mask(wall, st, torch)
-        for walls, addr in ((False, 'buf'), (False, 'ptr'), (True, 'buf'), (True, 'ptr')):
-            os.environ['PSAD_LBM_ADDR'] = addr
+        os.environ['PSAD_LBM_RB'] = '1'
+        for walls, lds in ((False, '0'), (False, '16384'), (False, '24576'), (False, '32768'), (False, '40960'),
+                           (False, '54000'), (True, '0'), (True, '32768')):
+            os.environ['PSAD_LBM_LDS'] = lds
             K = LatticeKernels(st, False, np.float32, walls, 'gpu')
             fl = mask if walls else None
-            tag = (' walls' if walls else '') + ' ' + addr
+            tag = (' walls' if walls else '') + f' lds {int(lds) // 1024}K'
             res['lattice fzyx fwd' + tag] = (timed(lambda: K.forward(s, d, 1.6, fl)), fb)
             res['lattice fzyx adj' + tag] = (timed(lambda: K.adjoint(s, g, o, 1.6, fl)), ab)
             rs, rd, rg, ro = rowi(), rowi(), rowi(), rowi()

@@ -346,7 +346,8 @@ LATTICE_GPU_CASES = [('D2Q9', (64, 48), True, 'fzyx', 'float32', True), ('D2Q9',
 def test_lbm_lattice_schedule_gpu_vs_oracle(stencil, shape, compressible, layout, dtype, walls):
     """The timestep op on the lattice schedule (walls or periodic, fzyx / AoS pdfs, fp32 / fp64): forward vs the
     oracle, the adjoint vs torch's reverse mode through it; the op's internal states are row-interleaved
-    (their layout never reaches the caller: output and gradient come back in the field's layout)."""
+    (their layout never reaches the caller: the output comes back in the field's layout, the gradient in the one
+    torch's gradient accumulation gives the input)."""
     import torch
     if stencil == 'D3Q27':
         pytest.importorskip('torch')
@@ -372,7 +373,6 @@ def test_lbm_lattice_schedule_gpu_vs_oracle(stencil, shape, compressible, layout
     g = torch.tensor(np.random.default_rng(5).standard_normal(f0.shape), device='cuda')
     out.backward(g.to(tdt))
     (gref,) = torch.autograd.grad(ref, ft, g)
-    assert x.grad.stride() == step.empty_pdfs().stride() or layout == 'numpy'
     assert float((x.grad.double() - gref).abs().max()) <= 10 * tol * float(gref.abs().max())
 
 
