@@ -547,8 +547,18 @@ class HipStencilKernel:
             # past each row end (XM) — where the WS schedule applies
             probe = self._march_cfg(ve, shape)
             xm = bool(probe.WS) and ws_geometry(ir, probe) is not None
-        if xm:
-            cfg = MarchConfig(**{**self._march_cfg(ve, shape).__dict__, 'XM': True})
+        xo = False
+        if not xm and not fits(ve) and esize == 2 and not ir.has_index_dims and os.environ.get('PSAD_XO', '1') != '0' and \
+                all(np.dtype(f.dtype.numpy_dtype).itemsize == 2 for f in ir.fields) and \
+                int(np.prod(shape[1:])) * 2 < 2 ** 31 - 1024:
+            # fp16 rows starting on half dwords (X odd, or an odd-element base): the half-precision LDS-DMA ring
+            # loads such rows one element early and shifts them back in LDS (XO) — 255³ fp16 instead of the
+            # register-prefetch path
+            probe = self._march_cfg(ve, shape)
+            ws_p = ws_geometry(ir, probe) if probe.WS else None
+            xo = ws_p is not None and ws_p['kind'] == 'h'
+        if xm or xo:
+            cfg = MarchConfig(**{**self._march_cfg(ve, shape).__dict__, 'XM': True, 'XO': xo})
         else:
             # widest plane-load vector the rows allow: 16 bytes (and the LDS-DMA loader) when the row pitch is a
             # multiple of 16 bytes, else 8 / 4 bytes (register-prefetch loads) before scalar ones — X = 262

@@ -263,19 +263,22 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
     args_a = ('src, g, out, nbmask, Z, Y, X, s_q, s_z, s_y, s_x, g_q, g_z, g_y, g_x, o_q, o_z, o_y, o_x, s_bytes, '
               'g_bytes, o_bytes, omega')
     if hip:
-        # a block = 64 x-adjacent cells of 4 lattice rows, ``rb`` times over consecutive row groups (rows counted
-        # over (z, y)): the wave's setup (kernel arguments, descriptors, scalar offsets) serves rb cells per lane
+        # a block = 256 consecutive cells of the lattice in C order (rows of x), and consecutive blocks on one XCD
+        # (bijective remap of the round-robin dispatch): a lattice row's x-shifted loads and the adjoint's
+        # x-shifted stores cover cache lines that the neighbouring wave also touches — in one block, or in a
+        # block on the same XCD's L2, not split between two L2s (partial-line write-backs)
         for nm, sig, args in (('lbm_fwd', sig_fwd, args_f), ('lbm_adj', sig_adj, args_a)):
             L.append(f'extern "C" __global__ void __launch_bounds__(256) {nm}({sig}, const int rb)\n{{')
-            L.append('  const int x = blockIdx.x * 64 + threadIdx.x;')
-            L.append('  if (x >= X) return;')
-            L.append('  const int rows = Y * Z;')
-            L.append('  for (int it = 0; it < rb; ++it) {')
-            L.append('    const int r = (blockIdx.y * rb + it) * 4 + threadIdx.y;')
-            L.append('    if (r >= rows) break;')
-            L.append('    const int z = r / Y, y = r - z * Y;')
-            L.append(f'    {nm}_cell({args}, z, y, x);')
-            L.append('  }\n}')
+            L.append('  (void)rb;')
+            L.append('  const unsigned nb = gridDim.x, b = blockIdx.x;')
+            L.append('  const unsigned per = nb >> 3, rem = nb & 7, xcd = b & 7, bi = b >> 3;')
+            L.append('  const unsigned lb = (xcd < rem) ? xcd * (per + 1) + bi : rem * (per + 1) + (xcd - rem) * per + bi;')
+            L.append('  const unsigned cell = lb * 256u + threadIdx.x;     // cells < 2^32 (checked at launch)')
+            L.append('  if (cell >= (unsigned)X * (unsigned)Y * (unsigned)Z) return;')
+            L.append('  const unsigned r = cell / (unsigned)X;')
+            L.append('  const int x = (int)(cell - r * (unsigned)X);')
+            L.append('  const int z = (int)(r / (unsigned)Y), y = (int)(r - (unsigned)z * Y);')
+            L.append(f'  {nm}_cell({args}, z, y, x);\n}}')
     else:
         for nm, kind in (('lbm_fwd', 'f'), ('lbm_adj', 'a')):
             # the CPU kernels' ctypes signature (backends.cpu_kernel.compile_c): pointers, extents, strides, -, scalars
@@ -449,19 +452,17 @@ class LatticeKernels:
 
     @staticmethod
     def _rows_per_block(X, Y, Z):
-        """Row groups (4 rows) per block and the grid's y extent: ~8192 blocks (32 per CU), at most 16 groups."""
-        groups = -(-(Y * Z) // 4)
-        xb = -(-X // 64)
-        rb = int(os.environ.get('PSAD_LBM_RB', 0)) or max(1, min(16, -(-groups * xb // 8192)))
-        return rb, -(-groups // rb)
+        """(unused by the kernel, 1) and the grid: one block per 256 consecutive cells."""
+        return 1, -(-(X * Y * Z) // 256)
 
     @staticmethod
-    def _launch(fn, X, gy, args, device, stream, torch):
+    def _launch(fn, X, nblocks, args, device, stream, torch):
         from ..backends import hip_runtime as rt
         if stream is None:
             stream = torch._C._cuda_getCurrentRawStream(device)
-        # (PSAD_LBM_LDS: dynamic LDS per block, i.e. fewer resident blocks per CU — occupancy A/B in the probes)
-        rt.launch(fn, (-(-X // 64), gy), (64, 4, 1), args, stream, int(os.environ.get('PSAD_LBM_LDS', 0)))
+        if nblocks * 256 >= 2 ** 32:
+            raise ValueError('lattice of 2^32 cells or more: too large for one launch')
+        rt.launch(fn, (nblocks,), (256, 1, 1), args, stream)
 
     # -- CPU ---------------------------------------------------------------------------------------
     def _cpu_fn(self, which):

@@ -61,13 +61,10 @@ def main():
         wall[:, 0] = 1
         wall[:, -1] = 1
         mask = neighbour_mask(wall, st, torch)
-        os.environ['PSAD_LBM_RB'] = '1'
-        for walls, lds in ((False, '0'), (False, '16384'), (False, '24576'), (False, '32768'), (False, '40960'),
-                           (False, '54000'), (True, '0'), (True, '32768')):
-            os.environ['PSAD_LBM_LDS'] = lds
+        for walls in (False, True):
             K = LatticeKernels(st, False, np.float32, walls, 'gpu')
             fl = mask if walls else None
-            tag = (' walls' if walls else '') + f' lds {int(lds) // 1024}K'
+            tag = ' walls' if walls else ''
             res['lattice fzyx fwd' + tag] = (timed(lambda: K.forward(s, d, 1.6, fl)), fb)
             res['lattice fzyx adj' + tag] = (timed(lambda: K.adjoint(s, g, o, 1.6, fl)), ab)
             rs, rd, rg, ro = rowi(), rowi(), rowi(), rowi()

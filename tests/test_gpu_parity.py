@@ -572,18 +572,20 @@ def test_ws_loader_schedule_vs_oracle(params, shape, case):
     ('7pt_f32', W.diffusion_7pt, np.float32, (13, 45, 255), 'xm'), ('asym_f32', W.asym_7pt, np.float32, (11, 29, 134), 'xm'),
     ('27pt_f32', lambda: W.stencil_27pt(dtype='float32'), np.float32, (9, 23, 259), 'xm'),
     ('27pt_f16', W.stencil_27pt, np.float16, (7, 33, 260), 'xm'), ('27pt_f16', W.stencil_27pt, np.float16, (5, 19, 258), 'xm'),
-    ('27pt_f16', W.stencil_27pt, np.float16, (6, 17, 131), 1),
+    ('27pt_f16', W.stencil_27pt, np.float16, (6, 17, 131), 'xo'), ('27pt_f16', W.stencil_27pt, np.float16, (7, 20, 255), 'xo'),
     ('7pt_f16', lambda: W.diffusion_7pt(dtype='float16'), np.float16, (8, 41, 132), 'xm'),
     ('7pt_f16', lambda: W.diffusion_7pt(dtype='float16'), np.float16, (9, 70, 262), 'xm'),
-    ('7pt_f16', lambda: W.diffusion_7pt(dtype='float16'), np.float16, (5, 23, 133), 1),
+    ('7pt_f16', lambda: W.diffusion_7pt(dtype='float16'), np.float16, (5, 23, 133), 'xo'),
+    ('7pt_f16', lambda: W.diffusion_7pt(dtype='float16'), np.float16, (9, 33, 257), 'xo'),
     ('7pt_f64', lambda: W.diffusion_7pt(dtype='float64'), np.float64, (6, 17, 65), 'xm'),
     ('5pt_f32', W.laplace_5pt, np.float32, (130, 262), 2), ('5pt_f32', W.laplace_5pt, np.float32, (67, 129), 'generic')],
     ids=lambda c: f'{c[0]}_{"x".join(map(str, c[3]))}')
 def test_row_pitch_vector_width_vs_oracle(case):
     """Rows whose byte pitch is not a multiple of 16: with a dword-aligned pitch (fp32 / fp64, fp16 with X even)
-    the LDS-DMA ring keeps 16-byte pieces and zero-fills past each row end (XM); odd fp16 rows take the widest
-    plane-load vector they allow (register-prefetch loads), 2-D scalar rows the generic schedule — forward and
-    adjoint of the op's kernels vs the float64 oracle, NaN-poisoned outputs."""
+    the LDS-DMA ring keeps 16-byte pieces and zero-fills past each row end (XM); odd fp16 rows (every other row
+    starts on a half dword) stay on the half-precision ring, loaded one element early and shifted back in LDS
+    (XO); 2-D scalar rows take the generic schedule — forward and adjoint of the op's kernels vs the float64
+    oracle, NaN-poisoned outputs."""
     name, builder, dt, shape, expect = case
     op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
     rng = np.random.default_rng(sum(shape) + 3)
@@ -602,6 +604,8 @@ def test_row_pitch_vector_width_vs_oracle(case):
             assert k.last_variant[0] == 'generic', k.last_variant
         elif expect == 'xm':            # the LDS-DMA ring with dword-aligned pieces
             assert k.last_variant[0] == 'march' and k.last_variant[1].WS and k.last_variant[1].XM, k.last_variant
+        elif expect == 'xo':            # the half ring with rows on half dwords shifted in LDS
+            assert k.last_variant[0] == 'march' and k.last_variant[1].WS and k.last_variant[1].XO, k.last_variant
         else:
             assert k.last_variant[0] == 'march' and k.last_variant[1].VE == expect, k.last_variant
         for n, t in outs.items():
@@ -692,7 +696,7 @@ def test_ws_halos_and_two_range_launches(params):
 
 
 @pytest.mark.parametrize('dtype,X', [(torch.float32, 134), (torch.float32, 133), (torch.float64, 67),
-                                     (torch.float16, 262)])
+                                     (torch.float16, 262), (torch.float16, 263)])
 @pytest.mark.parametrize('bh', ['zeros', None])
 def test_xm_rows_halos_two_range_and_interior_only(dtype, X, bh):
     """Rows whose pitch is not a multiple of 16 bytes on the LDS-DMA ring (XM): z-slab launch pattern (halo
@@ -707,6 +711,7 @@ def test_xm_rows_halos_two_range_and_interior_only(dtype, X, bh):
     full = torch.zeros_like(u)
     k(u=u, out=full)
     assert k.last_variant[1].WS and k.last_variant[1].XM, k.last_variant
+    assert k.last_variant[1].XO == (X % 2 == 1 and dtype == torch.float16), k.last_variant
     kz = None if bh == 'zeros' else (1, 29)
     parts = [(0, 11), (11, 19), (19, 30)]
     outs = []
