@@ -32,7 +32,7 @@ def default_march_config(ir, ve, shape=None, tuning=None):
     ``PSAD_MARCH="CX=..,NR=.."``.
     """
     from .hip_emitter import lite_fields
-    cfg = dict(CX=4, WX=1, NR=8, NT_STORE=True, PD=1, FULL_RING=False, VIEW2D='yx', ZSUM=False, ZCT=0, PK=False,
+    cfg = dict(CX=4, WX=1, NR=8, NT_STORE=True, VIEW2D='yx', ZSUM=False, PK=False,
                ZMIN=32, ZMAX=64, BLK=512)
     probe = MarchConfig(VE=ve, **cfg)
     zsum_ok = zsum_plan(ir, probe) is not None
@@ -91,9 +91,12 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             k, v = kv.split('=')
             over[k.strip()] = v.strip() if k.strip() == 'VIEW2D' else int(v)
     for k, v in over.items():
-        if k in ('CX', 'WX', 'NR', 'PD', 'WAVES', 'LDS_PAD', 'ZCT', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'DMA_AUX'):
+        if k not in ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D',
+                     'ZC', 'BLOCKS'):
+            raise ValueError(f"unknown tile parameter '{k}' (gpu_indexing_params / PSAD_MARCH)")
+        if k in ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW'):
             cfg[k] = int(v)
-        elif k in ('NT_STORE', 'NT_LOAD', 'FULL_RING', 'ZSUM', 'PK', 'WS', 'AR', 'DPP'):
+        elif k in ('NT_STORE', 'ZSUM', 'PK', 'WS', 'AR'):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
         elif k == 'VIEW2D':
             cfg[k] = str(v)
@@ -498,9 +501,9 @@ class HipStencilKernel:
         # re-reads 2·RZ halo planes). 7-point 1024³, 128×32 tiles: 64-plane chunks 1.536 ms vs 128-plane
         # 1.570 ms (profiles/r01_tune_cx_ab_1024.log); 512³ and 128×1024² slabs land on 64 by the target
         target = int(self.kernel.tuning.get('BLOCKS', os.environ.get('PSAD_MARCH_BLOCKS', cfg.BLK)))
-        zc = self.kernel.tuning.get('ZC') or int(os.environ.get('PSAD_MARCH_ZC', 0)) or cfg.ZCT or \
+        zc = self.kernel.tuning.get('ZC') or int(os.environ.get('PSAD_MARCH_ZC', 0)) or \
             min(nz, max(cfg.ZMIN, min(cfg.ZMAX, math.ceil(nz * nt / target))))
-        explicit = self.kernel.tuning.get('ZC') or os.environ.get('PSAD_MARCH_ZC') or cfg.ZCT or \
+        explicit = self.kernel.tuning.get('ZC') or os.environ.get('PSAD_MARCH_ZC') or \
             'BLOCKS' in self.kernel.tuning or os.environ.get('PSAD_MARCH_BLOCKS')
         cus = _torch().cuda.get_device_properties(_torch().cuda.current_device()).multi_processor_count \
             if slots else 0

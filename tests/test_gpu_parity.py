@@ -278,13 +278,13 @@ def test_vector_field_generic_schedule():
 
 
 @pytest.mark.parametrize('params', [
-    dict(CX=4, NR=8, PD=2, NT_STORE=True), dict(CX=1, NR=1), dict(CX=2, WX=2, NR=3, PD=2),
-    dict(CX=2, NR=4, FULL_RING=True), dict(CX=4, NR=8, ZC=5), dict(CX=1, WX=4, NR=2, PD=2, ZC=3),
-    dict(CX=2, NR=3, NW=1, ZC=4), dict(CX=1, WX=2, NW=2, NR=2, PD=2),
+    dict(CX=4, NR=8, NT_STORE=True), dict(CX=1, NR=1), dict(CX=2, WX=2, NR=3),
+    dict(CX=4, NR=8, ZC=5), dict(CX=1, WX=4, NR=2, ZC=3),
+    dict(CX=2, NR=3, NW=1, ZC=4), dict(CX=1, WX=2, NW=2, NR=2),
 ])
 @pytest.mark.parametrize('builder', [W.diffusion_7pt, W.asym_7pt, W.stencil_27pt])
 def test_march_tunings_vs_oracle(params, builder):
-    """Every tile shape / pipeline depth / ring kind gives the oracle's result (ragged tiles, short chunks)."""
+    """Every tile shape / ring kind gives the oracle's result (ragged tiles, short chunks)."""
     from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
     op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
     is16 = builder is W.stencil_27pt
@@ -306,7 +306,7 @@ def test_march_tunings_vs_oracle(params, builder):
 
 
 @pytest.mark.parametrize('params', [dict(VIEW2D='yx'), dict(VIEW2D='zy'), dict(VIEW2D='yx', CX=1, NR=3),
-                                    dict(VIEW2D='zy', CX=2, WX=4, NR=1, PD=2, ZC=7)])
+                                    dict(VIEW2D='zy', CX=2, WX=4, NR=1, ZC=7)])
 @pytest.mark.parametrize('bh', ['zeros', None])
 def test_march_2d_views_vs_oracle(params, bh):
     from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
@@ -487,8 +487,7 @@ def _radius2_cases():
 
 
 @pytest.mark.parametrize('case', _radius2_cases(), ids=lambda c: c[0])
-@pytest.mark.parametrize('params', [dict(), dict(ZSUM=False), dict(ZSUM=False, FULL_RING=True),
-                                    dict(CX=1, NR=3, ZC=7), dict(ZSUM=False, PD=2, CX=2, NR=2)])
+@pytest.mark.parametrize('params', [dict(), dict(ZSUM=False), dict(CX=1, NR=3, ZC=7), dict(ZSUM=False, CX=2, NR=2)])
 @pytest.mark.parametrize('bh', ['zeros', None])
 def test_radius2_stencils_vs_oracle(case, params, bh):
     from pystencils_autodiff_amd.backends.hip_emitter import zsum_plan
