@@ -24,6 +24,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <limits>
@@ -86,8 +87,18 @@ at::Tensor allocate(const Alloc& a, int device) {
 
 bool aligned(const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 31u) == 0; }
 
+void launch_on(const Launch& l, const std::vector<at::Tensor>& table, const std::vector<double>& scalars,
+               hipStream_t stream);
+
 void launch(const Launch& l, const std::vector<at::Tensor>& table, const std::vector<double>& scalars,
             int device) {
+    // the function handle belongs to the module loaded on the plan's device: launch with it current
+    c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
+    launch_on(l, table, scalars, c10::hip::getCurrentHIPStream(device).stream());
+}
+
+void launch_on(const Launch& l, const std::vector<at::Tensor>& table, const std::vector<double>& scalars,
+               hipStream_t stream) {
     std::string args = l.args;
     for (size_t i = 0; i < l.slot.size(); ++i) {
         void* p = table[l.slot[i]].data_ptr();
@@ -102,9 +113,6 @@ void launch(const Launch& l, const std::vector<at::Tensor>& table, const std::ve
             std::memcpy(&args[l.s_off[j]], &f, sizeof(f));
         }
     }
-    // the function handle belongs to the module loaded on the plan's device: launch with it current
-    c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
-    hipStream_t stream = c10::hip::getCurrentHIPStream(device).stream();
     int rc = psad_launch(l.fn, l.grid, 1, 1, l.block, 1, 1, 0, stream, args.data(), args.size());
     TORCH_CHECK(rc == 0, "psad: hipModuleLaunchKernel failed: ", psad_error_string(rc), " (code ", rc, ")");
 }
@@ -182,6 +190,7 @@ struct Sweep {
     bool has_inner = false;
     Launch inner;
     std::vector<Launch> faces;
+    bool faces_on_halo = false;           // face launch(es) on the halo stream right behind the exchange
 };
 
 struct SlabPlan {
@@ -228,12 +237,15 @@ void run_sweep(const Sweep& w, const std::vector<at::Tensor>& table, const std::
                                     ex.recv_hi.data(), ex.bytes.data(), ex.peer_lo, ex.peer_hi, ex.stream);
         TORCH_CHECK(rc == 0, "psad: RCCL halo exchange failed: ", psad_rccl_error_string(rc), " (code ", rc, ")");
     }
+    if (n && w.faces_on_halo)                                                // faces beside the interior
+        for (const auto& f : w.faces) launch_on(f, table, scalars, ex.stream);
     if (w.has_inner) launch(w.inner, table, scalars, device);                // interior overlaps the exchange
     if (n) {
         hip_ok(hipEventRecord(ex.ev_halos, ex.stream), "hipEventRecord");
         hip_ok(hipStreamWaitEvent(cur, ex.ev_halos, 0), "hipStreamWaitEvent");
     }
-    for (const auto& f : w.faces) launch(f, table, scalars, device);
+    if (!(n && w.faces_on_halo))
+        for (const auto& f : w.faces) launch(f, table, scalars, device);
 }
 
 struct SlabFunction : public torch::autograd::Function<SlabFunction> {
@@ -369,6 +381,8 @@ Sweep sweep_from(const py::object& inner, const py::list& faces, const py::tuple
     w.ex.peer_lo = ex[5].cast<int>();
     w.ex.peer_hi = ex[6].cast<int>();
     w.ex.loopback = ex[7].cast<bool>();
+    const char* fo = std::getenv("PSAD_SLAB_FACES");      // 'halo': faces on the halo stream (A/B, probes)
+    w.faces_on_halo = fo != nullptr && std::string(fo) == "halo";
     const size_t n = w.ex.slot.size();
     TORCH_CHECK(w.ex.last_off.size() == n && w.ex.recv_lo.size() == n && w.ex.recv_hi.size() == n &&
                     w.ex.bytes.size() == n, "psad: exchange spec lengths differ");

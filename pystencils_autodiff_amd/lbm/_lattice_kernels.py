@@ -356,6 +356,7 @@ class LatticeKernels:
         self.walls = bool(walls)
         self.target = target
         self._fns = {}
+        self._plans = {}
 
     def source(self, idx='int', addr='buf'):
         if self.target != 'gpu':
@@ -416,10 +417,29 @@ class LatticeKernels:
             fn_args += list(lattice_strides(t, self.stencil.D))
         return idx, addr, fn_args
 
+    def _cached(self, which, tensors, mask, omega, stream):
+        """Launch from the argument template of an earlier call with the same shapes, strides, dtype, device,
+        walls and ω (only the pointers are patched): the time-step op launches T times per apply."""
+        key = (which, float(omega), mask is not None) + tuple((tuple(t.shape), tuple(t.stride()), t.dtype, t.device)
+                                                             for t in tensors)
+        plan = self._plans.get(key)
+        if plan is None:
+            return key, False
+        fn, nblocks, template, device = plan
+        buf = bytearray(template)
+        ptrs = [t.data_ptr() for t in tensors] + [mask.data_ptr() if mask is not None else 0]
+        struct.pack_into(f'<{len(ptrs)}Q', buf, 0, *ptrs)
+        import torch
+        self._launch(fn, None, nblocks, bytes(buf), device, stream, torch)
+        return key, True
+
     def forward(self, src, dst, omega, mask=None, stream=None):
         """``dst = stream-pull-collide(src)`` (torch tensors ``[*domain, q]``, any strides)."""
         if self.target != 'gpu':
             return self._cpu('fwd', [src, dst], omega, mask)
+        key, done = self._cached('fwd', [src, dst], mask, omega, stream)
+        if done:
+            return
         import torch
         idx, addr, strides = self._common([src, dst], mask)
         fn = self._gpu_fn('fwd', idx, addr, src.device.index)
@@ -429,12 +449,16 @@ class LatticeKernels:
         args = _pack('QQQiii' + code * 8 + 'qq' + ('d' if self.ct == 'double' else 'f') + 'i',
                      src.data_ptr(), dst.data_ptr(), mask.data_ptr() if mask is not None else 0, Z, Y, X, *strides,
                      self._reach(src) * src.element_size(), self._reach(dst) * dst.element_size(), float(omega), rb)
+        self._plans[key] = (fn, gy, args, src.device.index)
         self._launch(fn, X, gy, args, src.device.index, stream, torch)
 
     def adjoint(self, src, g, out, omega, mask=None, stream=None):
         """``out = (∂ step / ∂ src)ᵀ g`` at the state ``src``."""
         if self.target != 'gpu':
             return self._cpu('adj', [src, g, out], omega, mask)
+        key, done = self._cached('adj', [src, g, out], mask, omega, stream)
+        if done:
+            return
         import torch
         idx, addr, strides = self._common([src, g, out], mask)
         fn = self._gpu_fn('adj', idx, addr, src.device.index)
@@ -444,6 +468,7 @@ class LatticeKernels:
         args = _pack('QQQQiii' + code * 12 + 'qqq' + ('d' if self.ct == 'double' else 'f') + 'i',
                      src.data_ptr(), g.data_ptr(), out.data_ptr(), mask.data_ptr() if mask is not None else 0,
                      Z, Y, X, *strides, *[self._reach(t) * t.element_size() for t in (src, g, out)], float(omega), rb)
+        self._plans[key] = (fn, gy, args, src.device.index)
         self._launch(fn, X, gy, args, src.device.index, stream, torch)
 
     def _extent(self, t):

@@ -82,10 +82,12 @@ class BoundaryHandling:
         self.flags = np.zeros(self.domain_size, np.uint8)
         self._on_change = on_change
         self.conditions = {}
+        self._has_walls = False
 
     @property
     def has_walls(self):
-        return bool(self.flags.any())
+        """Any obstacle cell (kept up to date by ``set_boundary``: the kernels ask once per launch)."""
+        return self._has_walls
 
     def set_boundary(self, boundary_obj, slice_obj=None, mask_callback=None, mask_array=None, **_):
         """Mark cells as ``boundary_obj`` (``NoSlip``; ``AdjointNoSlip`` / ``AdjointBoundaryCondition(NoSlip)``
@@ -118,6 +120,7 @@ class BoundaryHandling:
         sub = self.flags[slice_obj]
         sub = np.where(mask.reshape(sub.shape), np.uint8(value), sub)
         self.flags[slice_obj] = sub
+        self._has_walls = bool(self.flags.any())
         if value:
             self.conditions[boundary_obj] = True
         if self._on_change is not None:

@@ -49,11 +49,16 @@ def main():
               f'implied N={n // zl} {n}^3 rate {n**3 / (wall * 1e-3) / 1e6:,.0f} Mcells/s')
     torch.autograd.set_multithreading_enabled(False)
     import os
-    for native in ('1', '0', '1', '0'):
-        # the slab Function through the native node (csrc/psad_torch.cpp "z-slab sweeps") or the Python sweeps
+    for native, faces in (('1', 'compute'), ('0', 'compute'), ('1', 'halo'), ('1', 'compute'), ('1', 'halo')):
+        # the slab Function through the native node (csrc/psad_torch.cpp "z-slab sweeps") or the Python sweeps;
+        # the native node's face launches on the compute stream after the interior, or on the halo stream
         os.environ['PSAD_NATIVE_SLAB'] = native
+        os.environ['PSAD_SLAB_FACES'] = faces
+        zop2 = ZSlabOp(op, use_cuda=True)          # a fresh plan per setting (the face placement is fixed at plan time)
+        zop2._halo = zop._halo
+        zfn = zop2.autograd_function()
         wall, host = timed(zfn, u, d)
-        print(f'zslab {"native" if native == "1" else "python"}, autograd 1 thread: {wall:.4f} ms/step wall, '
+        print(f'zslab {"native" if native == "1" else "python"} faces on {faces}, autograd 1 thread: {wall:.4f} ms/step wall, '
               f'{host:.4f} ms/step host enqueue, implied N={n // zl} {n}^3 rate '
               f'{n**3 / (wall * 1e-3) / 1e6:,.0f} Mcells/s', flush=True)
     zop.close()
