@@ -45,6 +45,10 @@ def parse():
     p.add_argument('--warmup', type=int, default=10)
     p.add_argument('--workload', default='diffusion7_f32', choices=sorted(WORKLOADS),
                    help='diffusion7_f32 (default, the headline) or stencil27_f16 (BASELINE config 5)')
+    p.add_argument('--secondary', default='stencil27_f16', choices=sorted(WORKLOADS) + ['none'],
+                   help='a second BASELINE workload timed in the same run, reported under "secondary" '
+                        '(default: config 5, stencil27_f16 768^3; none to skip)')
+    p.add_argument('--secondary-edge', type=int, default=None, help='cube edge of the secondary workload')
     p.add_argument('--edge', type=int, default=None,
                    help='cube edge (default: the workload\'s BASELINE size, 1024 / 768)')
     p.add_argument('--no-cpu-baseline', action='store_true')
@@ -133,33 +137,18 @@ def load_traffic(workload, kernel):
     return (k['total'] if k else None), entry.get('source')
 
 
-def main():
-    args = parse()
+def run_workload(name, edge, args, world, rank, distributed, extras):
+    """Warmup, then EXACTLY ``args.steps`` timed fwd+bwd steps of workload ``name`` through the drop-in path
+    (1 GPU: the op; N GPUs: this rank's z-slab through ``ZSlabOp.autograd_function()``), bracketed by barrier +
+    synchronize, max over ranks. Returns the figures of the JSON line."""
     import torch
     import torch.distributed as dist
-
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
-    distributed = world > 1
-    if args.gpus != world and distributed:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    local_rank = local_rank % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local_rank)
-    if distributed:
-        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        backend = os.environ.get('PSAD_DIST_BACKEND', 'nccl')   # nccl = RCCL; gloo only to rehearse on 1 GPU
-        if backend == 'nccl':
-            dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
-        else:
-            dist.init_process_group(backend)
 
     import pystencils_autodiff_amd as pa
     from pystencils_autodiff_amd import workloads as W
     from pystencils_autodiff_amd.zslab import ZSlabOp, slab_bounds
-
-    wl = WORKLOADS[args.workload]
-    n = args.edge or wl['edge']
+    wl = WORKLOADS[name]
+    n = edge or wl['edge']
     tdtype = getattr(torch, wl['dtype'])
     bytes_per_cell = wl['bytes']
     lo, hi = slab_bounds(n, world, rank)
@@ -245,7 +234,7 @@ def main():
     bytes_fwd = bytes_per_cell * zl * n * n
     achieved = bytes_fwd / (fwd_ms * 1e-3) / 1e9
     result_extra = {}
-    if not distributed:
+    if extras and not distributed:
         # the same step with torch's default engine (backward on its device thread; the op's backward is
         # the C++ node, so no Python runs there)
         torch.autograd.set_multithreading_enabled(True)
@@ -258,7 +247,7 @@ def main():
         torch.cuda.synchronize()
         result_extra['value_default_engine'] = round(cells_total * args.steps / (time.perf_counter() - t1) / 1e6, 1)
         torch.autograd.set_multithreading_enabled(False)
-    if args.kernel_only and not distributed:
+    if extras and args.kernel_only and not distributed:
         out = torch.empty_like(u)
         du = torch.empty_like(u)
         for _ in range(2):
@@ -273,6 +262,50 @@ def main():
         kt = time.perf_counter() - t1
         result_extra['kernel_only_mcells_s'] = round(cells_total * args.steps / kt / 1e6, 1)
 
+    zop_keep = zop if distributed else None
+    kname = fwd_k.source(fwd_k.last_variant)[1] if fwd_k.last_variant else fwd_k.name
+    out = dict(n=n, value=value, ms_per_step=ms_per_step, fwd_ms=fwd_ms, bwd_ms=bwd_ms, achieved=achieved,
+               bytes_fwd=bytes_fwd, kname=kname, cells=cells_total, extra=result_extra, zop=zop_keep)
+    del uu, u, d, fn, op
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    distributed = world > 1
+    if args.gpus != world and distributed:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    local_rank = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_rank)
+    if distributed:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        backend = os.environ.get('PSAD_DIST_BACKEND', 'nccl')   # nccl = RCCL; gloo only to rehearse on 1 GPU
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+        else:
+            dist.init_process_group(backend)
+
+    primary = run_workload(args.workload, args.edge, args, world, rank, distributed, extras=True)
+    secondary = None
+    if args.secondary != 'none' and args.secondary != args.workload:
+        # BASELINE config 5 measured in the same run (the driver's scaling runs call bench.py with its default
+        # workload only): same path, same timing rules, its own barrier + max-over-ranks clock
+        secondary = run_workload(args.secondary, args.secondary_edge, args, world, rank, distributed, extras=False)
+    n = primary['n']
+    wl = WORKLOADS[args.workload]
+    value, ms_per_step, fwd_ms, bwd_ms = (primary[k] for k in ('value', 'ms_per_step', 'fwd_ms', 'bwd_ms'))
+    achieved, bytes_fwd, kname, cells_total = (primary[k] for k in ('achieved', 'bytes_fwd', 'kname', 'cells'))
+    bytes_per_cell = wl['bytes']
+    result_extra = primary['extra']
+    zop = primary['zop']
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         # after the timed loop, at every N (north_star: the CPU path "in the same run"); the other ranks
@@ -285,7 +318,6 @@ def main():
         dist.barrier()
     if rank == 0:
         workload = f'{args.workload}_{n}^3'
-        kname = fwd_k.source(fwd_k.last_variant)[1] if fwd_k.last_variant else fwd_k.name
         traffic, traffic_src = load_traffic(workload, kname)
         res = {
             'metric': f'Mcells/s forward+backward, {wl["label"]} {n}^3',
@@ -317,10 +349,28 @@ def main():
                          'bytes_per_launch': bytes_fwd},
             'cpu_baseline': cpu,
         }
+        if secondary is not None:
+            w2 = WORKLOADS[args.secondary]
+            n2 = secondary['n']
+            res['secondary'] = {
+                'metric': f'Mcells/s forward+backward, {w2["label"]} {n2}^3', 'name': args.secondary,
+                'value': round(secondary['value'], 1), 'unit': 'Mcells/s', 'n_gpus': world, 'steps': args.steps,
+                'warmup': args.warmup, 'ms_per_step': round(secondary['ms_per_step'], 4),
+                'fwd_ms': round(secondary['fwd_ms'], 4), 'bwd_ms': round(secondary['bwd_ms'], 4),
+                'dtype': w2['dtype_tag'], 'cells': secondary['cells'],
+                'decomposition': f'z-slab x{world}' if world > 1 else 'single GPU',
+                'hbm_roofline_frac_step': round(2 * w2['bytes'] * secondary['cells'] / (secondary['ms_per_step'] * 1e-3)
+                                                / 1e9 / (HBM_PEAK_GBS * world), 4),
+                'roofline': {'bound': 'hbm', 'achieved': round(secondary['achieved'], 1), 'peak': HBM_PEAK_GBS,
+                             'unit': 'GB/s', 'frac': round(secondary['achieved'] / HBM_PEAK_GBS, 4),
+                             'kernel': f'{secondary["kname"]} (forward sweep)',
+                             'bytes_per_launch': secondary['bytes_fwd']}}
         res.update(result_extra)
         print(json.dumps(res))
     if distributed:
-        zop.close()
+        for r in (primary, secondary):
+            if r is not None and r['zop'] is not None:
+                r['zop'].close()
         dist.destroy_process_group()
 
 

@@ -266,9 +266,15 @@ class HipStencilKernel:
         fn, grid, block, packed, xb, device = prep
         if grid == 0:
             return xb
+        torch = _torch()
         if stream is None:
-            stream = _torch()._C._cuda_getCurrentRawStream(device)
-        rt.launch(fn, (grid,), (block,), packed, stream)
+            stream = torch._C._cuda_getCurrentRawStream(device)
+        if device != torch.cuda.current_device():
+            # the function handle belongs to the module loaded on the tensors' device: launch with it current
+            with torch.cuda.device(device):
+                rt.launch(fn, (grid,), (block,), packed, stream)
+        else:
+            rt.launch(fn, (grid,), (block,), packed, stream)
         return xb
 
     def prepare(self, halos=None, force_schedule=None, z_range=None, x_border=False, z_limits=None, **kwargs):

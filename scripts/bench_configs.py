@@ -180,7 +180,7 @@ def run_slab(name, builder, shape, dtype, full_cells, steps=20, warmup=3):
     sys.stdout.flush()
 
 
-def run_lbm(name, stencil, shape, dtype, T=10, reps=3, compressible=False):
+def run_lbm(name, stencil, shape, dtype, T=10, reps=3, compressible=False, walls=False):
     """Lattice Boltzmann time-step op (lbm.AutoDiffLatticeBoltzmannStep.create_timestep_op): T forward steps
     and the T adjoint steps, HIP events around Op.apply and backward. MLUPS = cells · T / time; algorithmic
     bytes per cell and step: forward 2q·s (read src, write dst), adjoint 3q·s (read diffdst and the recorded
@@ -190,6 +190,10 @@ def run_lbm(name, stencil, shape, dtype, T=10, reps=3, compressible=False):
     from pystencils_autodiff_amd import lbm
     rule = lbm.create_lb_update_rule(stencil, compressible=compressible, data_type=str(dtype).replace('torch.', ''))
     step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.5, target='gpu')
+    if walls:
+        # a channel: no-slip walls on the first and last rows of axis 1
+        step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[:, 0])
+        step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[:, -1])
     Op = step.create_timestep_op(T)
     q = rule.stencil.Q
     g = torch.Generator(device='cuda').manual_seed(0)
@@ -225,6 +229,7 @@ def run_lbm(name, stencil, shape, dtype, T=10, reps=3, compressible=False):
     es = torch.tensor([], dtype=dtype).element_size()
     f_ms, b_ms = sorted(fw)[len(fw) // 2], sorted(bw)[len(bw) // 2]
     res = {'config': name, 'shape': list(shape), 'dtype': str(dtype).replace('torch.', ''), 'time_steps': T,
+           'schedule': 'lattice' if step._lattice is not None else 'autodiffop', 'walls': bool(walls),
            'fwd_mlups': round(cells * T / (f_ms * 1e-3) / 1e6, 1), 'bwd_mlups': round(cells * T / (b_ms * 1e-3) / 1e6, 1),
            'fwd_ms': round(f_ms, 4), 'bwd_ms': round(b_ms, 4),
            'fwd_GBps': round(2 * q * es * cells * T / (f_ms * 1e-3) / 1e9, 1),
@@ -293,12 +298,14 @@ def main():
         if only and name not in only:
             continue
         run_slab(name, b, shape, dt, cells)
-    lbms = [('lbm_d2q9_f32_2048^2', 'D2Q9', (2048, 2048), torch.float32),
-            ('lbm_d3q19_f32_192^3', 'D3Q19', (192, 192, 192), torch.float32)]
-    for name, stencil, shape, dt in lbms:
+    lbms = [('lbm_d2q9_f32_2048^2', 'D2Q9', (2048, 2048), torch.float32, False),
+            ('lbm_d3q19_f32_192^3', 'D3Q19', (192, 192, 192), torch.float32, False),
+            ('lbm_d2q9_f32_2048^2_channel', 'D2Q9', (2048, 2048), torch.float32, True),
+            ('lbm_d3q19_f32_192^3_channel', 'D3Q19', (192, 192, 192), torch.float32, True)]
+    for name, stencil, shape, dt, walls in lbms:
         if only and name not in only:
             continue
-        run_lbm(name, stencil, shape, dt)
+        run_lbm(name, stencil, shape, dt, walls=walls)
 
 
 if __name__ == '__main__':

@@ -31,7 +31,7 @@ def test_bench_two_ranks_end_to_end(nproc, workload):
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={nproc}',
            '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
            os.path.join(ROOT, 'bench.py'), '--gpus', str(nproc), '--edge', '128', '--steps', '3', '--warmup', '1',
-           '--workload', workload, '--cpu-seconds', '1']
+           '--workload', workload, '--cpu-seconds', '1', '--secondary-edge', '96']
     t0 = time.perf_counter()
     proc = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     wall = time.perf_counter() - t0
@@ -48,5 +48,11 @@ def test_bench_two_ranks_end_to_end(nproc, workload):
     assert res['metric'].endswith('128^3') and ('27-point fp16' in res['metric']) == (workload == 'stencil27_f16')
     assert res['roofline']['bytes_per_launch'] == (8 if workload == 'diffusion7_f32' else 4) * 64 * 128 * 128
     # rank 0 times the CPU path after the timed loop at every N (north_star: "in the same run")
+    if workload == 'diffusion7_f32':            # config 5 timed in the same run (the driver's scaling runs)
+        sec = res['secondary']
+        assert sec['name'] == 'stencil27_f16' and sec['n_gpus'] == nproc and sec['value'] > 0
+        assert sec['decomposition'] == f'z-slab x{nproc}' and sec['cells'] == 96 ** 3
+    else:
+        assert 'secondary' not in res
     cpu = res['cpu_baseline']
     assert cpu is not None and cpu['value'] > 0 and cpu['cores'] == 1 and cpu['kind'] == 'port', cpu
