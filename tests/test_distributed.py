@@ -452,7 +452,7 @@ def test_zslab_native_node_loopback(builder_name, shape, monkeypatch):
             monkeypatch.setenv('PSAD_NATIVE_SLAB', native)
             uu = tu.clone().requires_grad_(True)
             (o,) = fn.apply(uu)
-            assert ('SlabFunction' in o.grad_fn.name()) == (native == '1'), o.grad_fn.name()
+            assert ('CppNode' in o.grad_fn.name()) == (native == '1'), o.grad_fn.name()
             o.backward(td)
             torch.cuda.synchronize()
             res.append((o.detach().clone(), uu.grad.clone()))
