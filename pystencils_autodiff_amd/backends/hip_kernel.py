@@ -567,7 +567,8 @@ class HipStencilKernel:
             ws_p = ws_geometry(ir, probe) if probe.WS else None
             xo = ws_p is not None and ws_p['kind'] == 'h'
         if xm or xo:
-            cfg = MarchConfig(**{**self._march_cfg(ve, shape).__dict__, 'XM': True, 'XO': xo})
+            cfg = MarchConfig(**{**self._march_cfg(ve, shape).__dict__, 'XM': True,
+                                 'XO': (1 if X % 2 else 2) if xo else 0})
         else:
             # widest plane-load vector the rows allow: 16 bytes (and the LDS-DMA loader) when the row pitch is a
             # multiple of 16 bytes, else 8 / 4 bytes (register-prefetch loads) before scalar ones — X = 262

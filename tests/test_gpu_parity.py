@@ -710,7 +710,7 @@ def test_xm_rows_halos_two_range_and_interior_only(dtype, X, bh):
     full = torch.zeros_like(u)
     k(u=u, out=full)
     assert k.last_variant[1].WS and k.last_variant[1].XM, k.last_variant
-    assert k.last_variant[1].XO == (X % 2 == 1 and dtype == torch.float16), k.last_variant
+    assert bool(k.last_variant[1].XO) == (X % 2 == 1 and dtype == torch.float16), k.last_variant
     kz = None if bh == 'zeros' else (1, 29)
     parts = [(0, 11), (11, 19), (19, 30)]
     outs = []
