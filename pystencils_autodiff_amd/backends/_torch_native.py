@@ -259,8 +259,12 @@ class _NativePath:
         except KeyError:
             return None
         a0 = args[0]
-        if not isinstance(a0, torch.Tensor):
-            return None
+        # per-call conditions (the C++ side checks them again): such a call takes the Python Function without
+        # marking its signature as one the plan cannot express
+        for a in args:
+            if not isinstance(a, torch.Tensor) or not a.is_cuda or not a.is_contiguous() or a.data_ptr() % 32 \
+                    or a.device != a0.device:
+                return None
         key = (tuple(a0.shape), a0.dtype, a0.device)
         pid = self.plans.get(key)
         if pid is None:

@@ -29,10 +29,10 @@ def main():
         v = sorted(a.elapsed_time(b) for a, b in ev)
         return v[len(v) // 2]
     for name, builder in (('27pt_f16', W.stencil_27pt), ('7pt_f16', lambda: W.diffusion_7pt(dtype='float16'))):
-        for n in (256, 255, 257, 511, 512):
+        for n in (256, 255, 257, 254, 258, 511, 512, 510):
             for xo in ('1', '0'):
                 if n % 2 == 0 and xo == '0':
-                    continue
+                    continue                      # (even rows: XM, dword-aligned, no realignment)
                 os.environ['PSAD_XO'] = xo
                 op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
                 k = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name=f'odd{xo}',
