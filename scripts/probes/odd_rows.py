@@ -42,7 +42,15 @@ def main():
                 ms = timed(lambda: k(u=u, out=out))
                 cfg = k.last_variant[1]
                 print(f'{name} {n}^3 XO={xo}: {ms:.4f} ms  {4 * n ** 3 / ms / 1e6:6.0f} GB/s  '
-                      f'(WS={cfg.WS} XM={cfg.XM} XO={cfg.XO} VE={cfg.VE})', flush=True)
+                      f'(WS={cfg.WS} XM={cfg.XM} XO={cfg.XO} VE={cfg.VE} NR={cfg.NR})', flush=True)
+                if os.environ.get('NR_SWEEP') and xo == '1':
+                    for nr in (2, 4):
+                        kt = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name=f'oddnr{nr}',
+                                           target='gpu', gpu_indexing_params={'NR': nr}).compile()
+                        ms = timed(lambda: kt(u=u, out=out))
+                        c2 = kt.last_variant[1]
+                        print(f'{name} {n}^3 NR={nr}: {ms:.4f} ms  {4 * n ** 3 / ms / 1e6:6.0f} GB/s  '
+                              f'(WS={c2.WS} XM={c2.XM} XO={c2.XO} TX={c2.TX} TY={c2.TY})', flush=True)
 
 
 if __name__ == '__main__':
