@@ -153,7 +153,8 @@ def run_workload(name, edge, args, world, rank, distributed, extras, warmup=None
     bytes_per_cell = wl['bytes']
     lo, hi = slab_bounds(n, world, rank)
     zl = hi - lo
-    op = pa.AutoDiffOp(getattr(W, wl['builder'])(), boundary_handling='zeros')
+    # the op named after the workload: its kernels (<name>_forward_gpu_zsum, ...) stay apart in rocprof traces
+    op = pa.AutoDiffOp(getattr(W, wl['builder'])(), name, boundary_handling='zeros')
     fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
     fwd_k = op.forward_ast_gpu.compile()
     bwd_k = op.backward_ast_gpu.compile()

@@ -26,6 +26,7 @@ def main():
     p.add_argument('--bytes', type=float)
     p.add_argument('--json')
     p.add_argument('--source', default='')
+    p.add_argument('--select', default='autodiffop', help='substring of the kernel names of the workload')
     a = p.parse_args()
     f = per_kernel(a.fetch, 'FETCH_SIZE')
     w = per_kernel(a.write, 'WRITE_SIZE')
@@ -36,7 +37,7 @@ def main():
         out[k] = {'read_bytes_corrected': rd, 'write_bytes': wr, 'total': rd + wr}
         print(f"{k[:60]:60s} read {rd / 1e9:8.3f} GB  write {wr / 1e9:8.3f} GB  total {(rd + wr) / 1e9:8.3f} GB")
     if a.json and a.workload:
-        sel = {k: v for k, v in out.items() if 'autodiffop' in k}
+        sel = {k: v for k, v in out.items() if a.select in k}
         entry = {'kernels': sel, 'algorithmic_bytes_per_launch': a.bytes, 'source': a.source,
                  'note': 'FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KB->bytes, mean per launch'}
         fwd = [v['total'] for k, v in sel.items() if 'forward' in k]
