@@ -356,6 +356,7 @@ def main():
         if secondary is not None:
             w2 = WORKLOADS[args.secondary]
             n2 = secondary['n']
+            traffic2, traffic2_src = load_traffic(f'{args.secondary}_{n2}^3', secondary['kname'])
             res['secondary'] = {
                 'metric': f'Mcells/s forward+backward, {w2["label"]} {n2}^3', 'name': args.secondary,
                 'value': round(secondary['value'], 1), 'unit': 'Mcells/s', 'n_gpus': world, 'steps': args.steps,
@@ -367,6 +368,7 @@ def main():
                                                 / 1e9 / (HBM_PEAK_GBS * world), 4),
                 'roofline': {'bound': 'hbm', 'achieved': round(secondary['achieved'], 1), 'peak': HBM_PEAK_GBS,
                              'unit': 'GB/s', 'frac': round(secondary['achieved'] / HBM_PEAK_GBS, 4),
+                             'traffic': traffic2, 'traffic_source': traffic2_src,
                              'kernel': f'{secondary["kname"]} (forward sweep)',
                              'bytes_per_launch': secondary['bytes_fwd']}}
         res.update(result_extra)
