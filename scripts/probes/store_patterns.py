@@ -71,6 +71,16 @@ extern "C" __global__ void __launch_bounds__(256) tile_copy8(const _Float16* s, 
 extern "C" __global__ void __launch_bounds__(256) tile_w8_nr4(const _Float16* s, _Float16* d, int N, int zc, int TXH) { tile_body<4, 0>(s, d, N, zc, TXH); }
 extern "C" __global__ void __launch_bounds__(256) tile_w16_nr4(const _Float16* s, _Float16* d, int N, int zc, int TXH) { tile_body<4, 1>(s, d, N, zc, TXH); }
 
+// 1-D strips marching z: block = (strip of 2048 consecutive halves of a plane, z chunk), 16 B per lane
+extern "C" __global__ void __launch_bounds__(256) strip_w16(_Float16* __restrict__ d, int N, int zc) {
+  const long long YX = (long long)N * N;
+  const int nstrip = (int)(YX / 2048);
+  const int s = blockIdx.x % nstrip, chunk = blockIdx.x / nstrip;
+  const int zb = chunk * zc, ze = min(zb + zc, N);
+  for (int z = zb; z < ze; ++z)
+    __builtin_nontemporal_store((f16x8)(_Float16)z, (f16x8*)(d + (long long)z * YX + (long long)s * 2048) + threadIdx.x);
+}
+
 extern "C" __global__ void __launch_bounds__(256) linear_w16(_Float16* __restrict__ d, long long n8) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i < n8) __builtin_nontemporal_store((f16x8)(_Float16)1, (f16x8*)d + i);
@@ -113,7 +123,7 @@ def main():
         args = struct.pack('<QQiii', src.data_ptr(), dst.data_ptr(), N, zc, txh) + b'\0' * 4
         return lambda: rt.launch(fn, (grid,), (256,), args, stream)
     res = []
-    for zc in (24, 96):
+    for zc in (1, 24, 96):
         for kname, nr in (('tile_w8', 2), ('tile_w16', 2), ('tile_w8_nr4', 4), ('tile_w16_nr4', 4)):
             for txh in (256, N):
                 if N % txh:
@@ -123,6 +133,12 @@ def main():
         for txh in (256, N):
             ms = timed(tile('tile_copy8', 2, zc, txh))
             res.append((f'tile_copy8     tile {txh}x8 zc {zc} (read p+1, write p)', ms, 2 * nbytes))
+    fs = rt.load_function(code, 'strip_w16', dev)
+    for zc in (1, 4, 24, 96):
+        nstrip = N * N // 2048
+        args = struct.pack('<Qii', dst.data_ptr(), N, zc)
+        res.append((f'strip_w16 (4 KB 1-D strips marching z) zc {zc}',
+                    timed(lambda: rt.launch(fs, (nstrip * -(-N // zc),), (256,), args, stream)), nbytes))
     fl = rt.load_function(code, 'linear_w16', dev)
     n8 = dst.numel() // 8
     args = struct.pack('<Qq', dst.data_ptr(), n8)
