@@ -258,3 +258,21 @@ def test_native_extension_loads_and_validates_plans():
     assert m.apply(pid, [x], [1.0]) is None
     assert m.apply(pid, [], [1.0]) is None
     assert m.apply(pid, [torch.zeros(4, 4)], []) is None      # scalar count differs from the plan
+
+
+@pytest.mark.gpu
+def test_native_node_on_non_default_device():
+    """Inputs on cuda:1 while cuda:0 is current: the plan's function handles belong to cuda:1's modules and the
+    launches (native node and Python Function) run under a device guard — results equal the same op on cuda:0."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip('one GPU visible')
+    _, fn = _make(W.asym_7pt(), 'zeros', True)
+    (u0,) = _inputs((11, 13, 70), torch.float32, 1)
+    d0 = torch.rand(11, 13, 70, device='cuda:0')
+    outs0, res0 = _run(fn, [u0], [d0])
+    u1 = u0.detach().to('cuda:1').requires_grad_(True)
+    d1 = d0.to('cuda:1')
+    with torch.cuda.device(0):
+        outs1, res1 = _run(fn, [u1], [d1])
+    assert outs1[0].device == torch.device('cuda', 1)
+    _same([r.to('cuda:0') if r is not None else None for r in res1], res0)
