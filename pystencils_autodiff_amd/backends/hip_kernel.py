@@ -32,6 +32,7 @@ def default_march_config(ir, ve, shape=None, tuning=None):
     ``PSAD_MARCH="CX=..,NR=.."``.
     """
     from .hip_emitter import lite_fields
+    star_ws = False
     cfg = dict(CX=4, WX=1, NR=8, NT_STORE=True, VIEW2D='yx', ZSUM=False, PK=False,
                ZMIN=32, ZMAX=64, BLK=512)
     probe = MarchConfig(VE=ve, **cfg)
@@ -68,6 +69,7 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             # the chunk model keeps 1024³ / 768³ / 512³ / the 8-GPU slabs where they were,
             # profiles/r02_tune_small_*.log)
             cfg.update(WS=True, CX=4, NR=8 if ws0['kind'] == 'h' else 4, D=4, ZMIN=8, ZMAX=128, BLK=256)
+            star_ws = True
     if ir.ndim == 2:
         cfg.update(CX=4, WX=1, NR=4, VIEW2D='yx', NT_STORE=False)   # 256×16 tiles (4096²: 0.024 ms, 5.6 TB/s)
     if ir.has_index_dims:
@@ -92,9 +94,9 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             over[k.strip()] = v.strip() if k.strip() == 'VIEW2D' else int(v)
     for k, v in over.items():
         if k not in ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D',
-                     'ZC', 'BLOCKS'):
+                     'ZC', 'BLOCKS', 'MAP'):
             raise ValueError(f"unknown tile parameter '{k}' (gpu_indexing_params / PSAD_MARCH)")
-        if k in ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW'):
+        if k in ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'MAP'):
             cfg[k] = int(v)
         elif k in ('NT_STORE', 'ZSUM', 'PK', 'WS', 'AR'):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
@@ -139,6 +141,15 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             cfg['NR'] //= 2
         else:
             cfg['CX'] //= 2
+    if star_ws and cfg.get('WS') and shape is not None and 'MAP' not in over:
+        ntx = -(-int(shape[-1]) // (64 * cfg['CX'] * cfg['WX']))
+        if ntx & (ntx - 1):
+            # tiles per row not a power of two: dispatch order instead of the XCD-aware remap. Through the op,
+            # fwd + bwd, same process (scripts/probes/map_ab.py, profiles/r03_map_ab.log): 768³ fp32 -8.6 %
+            # (5.91 / 5.78 TB/s), 640³ -4.4 %, 768³ fp16 -4.7 %, 640³ fp64 -2.5 %; with 2 or 4 tiles per row
+            # the dispatch order pins each XCD to the same x columns of every plane: 1024³ +10 %, 128×1024²
+            # +10 %, 512³ fp64 +6 % — those keep the remap
+            cfg['MAP'] = 1
     return MarchConfig(VE=ve, **cfg)
 
 

@@ -36,7 +36,7 @@ import sympy as sp
 
 from .. import ps
 from ..autodiff import AutoDiffOp
-from ._lattice_kernels import LatticeKernels, neighbour_mask, row_interleaved_empty
+from ._lattice_kernels import LatticeKernels, neighbour_mask
 from ._method import LBStencil
 from .boundaries import AdjointBoundaryCondition, AdjointNoSlip, BoundaryHandling, NoSlip
 
@@ -55,6 +55,24 @@ class SimulationResultsTensors:
         self.output_pdf_tensor = output_pdf_tensor
         self.output_density_tensor = output_density_tensor
         self.output_velocity_tensor = output_velocity_tensor
+
+
+def _lattice_sweeps(step, which, launches):
+    """The lattice kernels over ``launches`` (tensor tuples of ``LatticeKernels.forward`` / ``adjoint``) on the
+    current stream: one launch plan per distinct (shapes, strides) — the first, middle and last steps — and only
+    the pointers packed per launch."""
+    K = step._lattice_kernels()
+    mask = step._flag_arg()
+    om = step._omega_of()
+    mptr = mask.data_ptr() if mask is not None else 0
+    stream = _torch()._C._cuda_getCurrentRawStream(launches[0][0].device.index)
+    plans = {}
+    for ts in launches:
+        sig = tuple(t.stride() for t in ts)
+        plan = plans.get(sig)
+        if plan is None:
+            plan = plans[sig] = K.plan(which, list(ts), mask, om)
+        plan(tuple(t.data_ptr() for t in ts) + (mptr,), stream)
 
 
 def _guess_src_dst_field_from_update_rule(update_rule, src_hint, dst_hint):
@@ -210,17 +228,18 @@ class AutoDiffLatticeBoltzmannStep:
         out.copy_(t)
         return out
 
-    def _internal_state(self):
-        """A state only the time-step op sees: the row-interleaved layout (lattice schedule)."""
+    def _internal_states(self, n):
+        """``n`` states only the time-step op sees, in the row-interleaved layout (lattice schedule), as views
+        of one allocation."""
+        if n <= 0:
+            return []
         torch = _torch()
         dev = self._device or torch.device('cuda', torch.cuda.current_device())
-        return row_interleaved_empty(self.domain_size, int(self.pdf_field.index_shape[0]),
-                                     getattr(torch, np.dtype(self.pdf_field.dtype.numpy_dtype).name), dev)
-
-    def _alloc_strides(self):
-        if getattr(self, '_alloc_st', None) is None:
-            self._alloc_st = tuple(self._array(self._pdf_arr_name).stride())
-        return self._alloc_st
+        Q = int(self.pdf_field.index_shape[0])
+        dims = list(self.domain_size)
+        base = torch.empty([n] + dims[:-1] + [Q, dims[-1]],
+                           dtype=getattr(torch, np.dtype(self.pdf_field.dtype.numpy_dtype).name), device=dev)
+        return list(base.transpose(-1, -2).unbind(0))
 
     def _lattice_input_ok(self, t):
         """A tensor the lattice kernels take as it is: ``[*domain, q]`` of the pdf dtype on the step's device."""
@@ -390,14 +409,19 @@ class AutoDiffLatticeBoltzmannStep:
                 # states on fresh arrays: the input is the first state (the lattice kernels read any strides;
                 # the AutoDiffOp kernels need the field's layout — ``empty_pdfs`` — or get a copy), the output, in
                 # the field's layout, the last; the lattice schedule keeps the states between in the
-                # row-interleaved layout (no copies either way)
+                # row-interleaved layout, all in one allocation (no copies either way)
                 lattice = step._lattice is not None
                 x0 = pdfs.detach()
-                states = [x0 if lattice and step._lattice_input_ok(x0) else step._as_layout(x0)]
-                for t in range(T):
-                    out = step._alloc(zero=False) if (t == T - 1 or not lattice) else step._internal_state()
-                    step._fwd(states[-1], out, {})
-                    states.append(out)
+                x0 = x0 if lattice and step._lattice_input_ok(x0) else step._as_layout(x0)
+                if lattice:
+                    states = [x0] + step._internal_states(T - 1) + [step._alloc(zero=False)]
+                    _lattice_sweeps(step, 'fwd', [(states[t], states[t + 1]) for t in range(T)])
+                else:
+                    states = [x0]
+                    for t in range(T):
+                        out = step._alloc(zero=False)
+                        step._fwd(states[-1], out, {})
+                        states.append(out)
                 # state 0 may be the caller's tensor: keep it through save_for_backward, so that an in-place
                 # change between forward and backward raises (version counter) instead of skewing the adjoint
                 ctx.input_is_state0 = states[0].data_ptr() == pdfs.data_ptr()
@@ -418,18 +442,24 @@ class AutoDiffLatticeBoltzmannStep:
                 x0 = ctx.saved_tensors[0].detach() if ctx.input_is_state0 else None
                 records = ([x0 if lattice and step._lattice_input_ok(x0) else step._as_layout(x0)]
                            if ctx.input_is_state0 else []) + list(ctx.records)
-                cur, spare = g, None                # cur: adjoint of state t + 1 (never written when it is g)
-                for t in reversed(range(T)):
-                    if spare is not None:
-                        nxt = spare
-                    else:
-                        nxt = step._alloc(zero=False) if (t == 0 or not lattice) else step._internal_state()
-                    if lattice and t == 0 and nxt.stride() != step._alloc_strides():
-                        nxt = step._alloc(zero=False)       # the gradient leaves in the field's layout
-                    step._bwd(records[t], cur, nxt, {}, {})
-                    spare = cur if cur is not g else None
-                    cur = nxt
                 ctx.records = None
+                if lattice:
+                    # adjoints of states T-1 .. 1 alternate between two row-interleaved arrays; the gradient
+                    # (adjoint of state 0) leaves in the field's layout
+                    ping = step._internal_states(min(2, T - 1))
+                    out = step._alloc(zero=False)
+                    cur, launches = g, []
+                    for t in reversed(range(T)):
+                        nxt = out if t == 0 else ping[(T - 1 - t) % 2]
+                        launches.append((records[t], cur, nxt))
+                        cur = nxt
+                    _lattice_sweeps(step, 'adj', launches)
+                    return out
+                cur = g
+                for t in reversed(range(T)):
+                    nxt = step._alloc(zero=False)
+                    step._bwd(records[t], cur, nxt, {}, {})
+                    cur = nxt
                 return cur
 
         LbmTimesteps.num_time_steps = T

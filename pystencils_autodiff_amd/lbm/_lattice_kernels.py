@@ -33,7 +33,7 @@ import struct
 
 import numpy as np
 
-__all__ = ['LatticeKernels', 'lattice_strides', 'row_interleaved_empty', 'neighbour_mask']
+__all__ = ['LatticeKernels', 'LaunchPlan', 'lattice_strides', 'row_interleaved_empty', 'neighbour_mask']
 
 
 def _c(v):
@@ -268,8 +268,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
         # x-shifted stores cover cache lines that the neighbouring wave also touches — in one block, or in a
         # block on the same XCD's L2, not split between two L2s (partial-line write-backs)
         for nm, sig, args in (('lbm_fwd', sig_fwd, args_f), ('lbm_adj', sig_adj, args_a)):
-            L.append(f'extern "C" __global__ void __launch_bounds__(256) {nm}({sig}, const int rb)\n{{')
-            L.append('  (void)rb;')
+            L.append(f'extern "C" __global__ void __launch_bounds__(256) {nm}({sig})\n{{')
             L.append('  const unsigned nb = gridDim.x, b = blockIdx.x;')
             L.append('  const unsigned per = nb >> 3, rem = nb & 7, xcd = b & 7, bi = b >> 3;')
             L.append('  const unsigned lb = (xcd < rem) ? xcd * (per + 1) + bi : rem * (per + 1) + (xcd - rem) * per + bi;')
@@ -417,77 +416,54 @@ class LatticeKernels:
             fn_args += list(lattice_strides(t, self.stencil.D))
         return idx, addr, fn_args
 
-    def _cached(self, which, tensors, mask, omega, stream):
-        """Launch from the argument template of an earlier call with the same shapes, strides, dtype, device,
-        walls and ω (only the pointers are patched): the time-step op launches T times per apply."""
+    def plan(self, which, tensors, mask, omega):
+        """The launch of ``which`` ('fwd' / 'adj') on tensors of these shapes, strides, dtype and device (with or
+        without walls, at ω): a ``LaunchPlan`` whose pointer slots are patched per launch — the time-step op
+        launches T of them per apply."""
         key = (which, float(omega), mask is not None) + tuple((tuple(t.shape), tuple(t.stride()), t.dtype, t.device)
                                                              for t in tensors)
         plan = self._plans.get(key)
-        if plan is None:
-            return key, False
-        fn, nblocks, template, device = plan
-        buf = bytearray(template)
+        if plan is not None:
+            return plan
+        idx, addr, strides = self._common(tensors, mask)
+        dev = tensors[0].device.index
+        fn = self._gpu_fn(which, idx, addr, dev)
+        Z, Y, X = self._extent(tensors[0])
+        code = 'i' if idx == 'int' else 'q'
+        nblocks = self._blocks(X, Y, Z)
+        reach = [self._reach(t) * t.element_size() for t in tensors]
         ptrs = [t.data_ptr() for t in tensors] + [mask.data_ptr() if mask is not None else 0]
-        struct.pack_into(f'<{len(ptrs)}Q', buf, 0, *ptrs)
-        import torch
-        self._launch(fn, None, nblocks, bytes(buf), device, stream, torch)
-        return key, True
+        fmt = 'Q' * len(ptrs) + 'iii' + code * (4 * len(tensors)) + 'q' * len(tensors) + \
+            ('d' if self.ct == 'double' else 'f')
+        args = _pack(fmt, *ptrs, Z, Y, X, *strides, *reach, float(omega))
+        plan = self._plans[key] = LaunchPlan(fn, nblocks, args, len(ptrs))
+        return plan
 
     def forward(self, src, dst, omega, mask=None, stream=None):
         """``dst = stream-pull-collide(src)`` (torch tensors ``[*domain, q]``, any strides)."""
         if self.target != 'gpu':
             return self._cpu('fwd', [src, dst], omega, mask)
-        key, done = self._cached('fwd', [src, dst], mask, omega, stream)
-        if done:
-            return
-        import torch
-        idx, addr, strides = self._common([src, dst], mask)
-        fn = self._gpu_fn('fwd', idx, addr, src.device.index)
-        Z, Y, X = self._extent(src)
-        code = 'i' if idx == 'int' else 'q'
-        rb, gy = self._rows_per_block(X, Y, Z)
-        args = _pack('QQQiii' + code * 8 + 'qq' + ('d' if self.ct == 'double' else 'f') + 'i',
-                     src.data_ptr(), dst.data_ptr(), mask.data_ptr() if mask is not None else 0, Z, Y, X, *strides,
-                     self._reach(src) * src.element_size(), self._reach(dst) * dst.element_size(), float(omega), rb)
-        self._plans[key] = (fn, gy, args, src.device.index)
-        self._launch(fn, X, gy, args, src.device.index, stream, torch)
+        self.plan('fwd', [src, dst], mask, omega)(
+            (src.data_ptr(), dst.data_ptr(), mask.data_ptr() if mask is not None else 0), _stream(stream, src))
 
     def adjoint(self, src, g, out, omega, mask=None, stream=None):
         """``out = (∂ step / ∂ src)ᵀ g`` at the state ``src``."""
         if self.target != 'gpu':
             return self._cpu('adj', [src, g, out], omega, mask)
-        key, done = self._cached('adj', [src, g, out], mask, omega, stream)
-        if done:
-            return
-        import torch
-        idx, addr, strides = self._common([src, g, out], mask)
-        fn = self._gpu_fn('adj', idx, addr, src.device.index)
-        Z, Y, X = self._extent(src)
-        code = 'i' if idx == 'int' else 'q'
-        rb, gy = self._rows_per_block(X, Y, Z)
-        args = _pack('QQQQiii' + code * 12 + 'qqq' + ('d' if self.ct == 'double' else 'f') + 'i',
-                     src.data_ptr(), g.data_ptr(), out.data_ptr(), mask.data_ptr() if mask is not None else 0,
-                     Z, Y, X, *strides, *[self._reach(t) * t.element_size() for t in (src, g, out)], float(omega), rb)
-        self._plans[key] = (fn, gy, args, src.device.index)
-        self._launch(fn, X, gy, args, src.device.index, stream, torch)
+        self.plan('adj', [src, g, out], mask, omega)(
+            (src.data_ptr(), g.data_ptr(), out.data_ptr(), mask.data_ptr() if mask is not None else 0),
+            _stream(stream, src))
 
     def _extent(self, t):
         shape = [int(n) for n in t.shape[:self.stencil.D]]
         return [1] + shape if self.stencil.D == 2 else shape
 
     @staticmethod
-    def _rows_per_block(X, Y, Z):
-        """(unused by the kernel, 1) and the grid: one block per 256 consecutive cells."""
-        return 1, -(-(X * Y * Z) // 256)
-
-    @staticmethod
-    def _launch(fn, X, nblocks, args, device, stream, torch):
-        from ..backends import hip_runtime as rt
-        if stream is None:
-            stream = torch._C._cuda_getCurrentRawStream(device)
-        if nblocks * 256 >= 2 ** 32:
+    def _blocks(X, Y, Z):
+        """One block per 256 consecutive cells (cell indices are 32-bit in the kernel)."""
+        if X * Y * Z + 255 >= 2 ** 32:
             raise ValueError('lattice of 2^32 cells or more: too large for one launch')
-        rt.launch(fn, (nblocks,), (256, 1, 1), args, stream)
+        return -(-(X * Y * Z) // 256)
 
     # -- CPU ---------------------------------------------------------------------------------------
     def _cpu_fn(self, which):
@@ -526,6 +502,28 @@ class LatticeKernels:
         B = (ctypes.c_longlong * 1)(0)
         Dv = (ctypes.c_double * 1)(float(omega))
         fn(P, N, S, B, Dv)
+
+
+class LaunchPlan:
+    """One lattice kernel launch with its argument buffer; ``plan(ptrs, stream)`` patches the leading pointer
+    slots (the pdf arrays, then the neighbour mask) and launches."""
+    __slots__ = ('fn', 'nblocks', 'template', 'fmt')
+
+    def __init__(self, fn, nblocks, template, nptr):
+        self.fn, self.nblocks, self.template, self.fmt = fn, nblocks, template, f'<{nptr}Q'
+
+    def __call__(self, ptrs, stream):
+        from ..backends import hip_runtime as rt
+        buf = bytearray(self.template)
+        struct.pack_into(self.fmt, buf, 0, *ptrs)
+        rt.launch(self.fn, (self.nblocks,), (256,), bytes(buf), stream)
+
+
+def _stream(stream, t):
+    if stream is not None:
+        return stream
+    import torch
+    return torch._C._cuda_getCurrentRawStream(t.device.index)
 
 
 def _pack(fmt, *vals):

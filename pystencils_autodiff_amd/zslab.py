@@ -95,6 +95,8 @@ class RcclHalo:
             comm = ctypes.c_void_p()
             rt._check(L.psad_rccl_comm_init(uid_raw, self.world, self.rank, ctypes.byref(comm)), 'ncclCommInitRank')
             self.comm = comm
+            # (a high-priority stream for the exchange measured slower: 0.74 vs 0.42 ms per 128×1024² fp32
+            # loopback step, profiles/r03p_slab_variants.log)
             self.stream = torch.cuda.Stream(device=self.device)
             # reused stream-order events (Stream.wait_stream would create two per sweep)
             self.ev_faces = torch.cuda.Event()

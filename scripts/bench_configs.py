@@ -180,9 +180,9 @@ def run_slab(name, builder, shape, dtype, full_cells, steps=20, warmup=3):
     sys.stdout.flush()
 
 
-def run_lbm(name, stencil, shape, dtype, T=10, reps=3, compressible=False, walls=False):
+def run_lbm(name, stencil, shape, dtype, T=10, reps=5, compressible=False, walls=False):
     """Lattice Boltzmann time-step op (lbm.AutoDiffLatticeBoltzmannStep.create_timestep_op): T forward steps
-    and the T adjoint steps, HIP events around Op.apply and backward. MLUPS = cells · T / time; algorithmic
+    and the T adjoint steps, HIP events around Op.apply and backward (back-to-back applies). MLUPS = cells · T / time; algorithmic
     bytes per cell and step: forward 2q·s (read src, write dst), adjoint 3q·s (read diffdst and the recorded
     src, write diffsrc), s = element size; the ghost sync, state records and adjoint border fills are extra."""
     import torch
@@ -211,18 +211,23 @@ def run_lbm(name, stencil, shape, dtype, T=10, reps=3, compressible=False, walls
         Op.apply(x).backward(gr)
         x.grad = None
     settle(one)
-    for i in range(reps + 1):
+    # back-to-back applies as run() times the stencil configs (the queue stays ahead of the GPU: event times are
+    # the op's GPU time, not the host latency to its first launch after an idle GPU)
+    ev = []
+    for i in range(reps + 2):
         e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
         e0.record()
         out = Op.apply(x)
         e1.record()
         out.backward(gr)
         e2.record()
-        torch.cuda.synchronize()
         x.grad = None
-        if i:
-            fw.append(e0.elapsed_time(e1))
-            bw.append(e1.elapsed_time(e2))
+        if i >= 2:
+            ev.append((e0, e1, e2))
+    torch.cuda.synchronize()
+    for e0, e1, e2 in ev:
+        fw.append(e0.elapsed_time(e1))
+        bw.append(e1.elapsed_time(e2))
     cells = 1
     for n in shape:
         cells *= n
@@ -280,6 +285,10 @@ def main():
         ('diffusion7_f32_512^3', lambda: W.diffusion_7pt(), (512, 512, 512), torch.float32, 'zeros', 1, 8, 8),
         ('diffusion7_f32_1024^3', lambda: W.diffusion_7pt(), (1024, 1024, 1024), torch.float32, 'zeros', 1, 8, 8),
         ('stencil27_f16_768^3', lambda: W.stencil_27pt(), (768, 768, 768), torch.float16, 'zeros', 1, 4, 4),
+        # not a BASELINE config: the non-power-of-two extent of config 5 on the config-4 sweep
+        ('diffusion7_f32_768^3', lambda: W.diffusion_7pt(), (768, 768, 768), torch.float32, 'zeros', 1, 8, 8),
+        ('diffusion7_f16_768^3', lambda: W.diffusion_7pt(dtype='float16'), (768, 768, 768), torch.float16, 'zeros', 1,
+         4, 4),
         ('diffusion7_f64_512^3', lambda: W.diffusion_7pt(dtype='float64'), (512, 512, 512), torch.float64,
          'zeros', 1, 16, 16),
         ('veclaplace7_f32_384^3x3', lambda: W.vector_laplace_7pt(), (384, 384, 384, 3), torch.float32, 'zeros', 1,

@@ -148,8 +148,30 @@ def time_sweeps(zl=96, wl='stencil27', steps=300):
     zop.close()
 
 
+def trace(zl=128, wl='diffusion7', steps=20):
+    """A short run for ``rocprofv3 --kernel-trace``: the plain op, then the native slab step (faces on the compute
+    stream), ``steps`` fwd+bwd each after warm-up (``scripts/trace_timeline.py`` shows the last ones)."""
+    n = 768 if wl == 'stencil27' else 1024
+    op = pa.AutoDiffOp(W.stencil_27pt() if wl == 'stencil27' else W.diffusion_7pt(), boundary_handling='zeros')
+    dt = torch.float16 if wl == 'stencil27' else torch.float32
+    u = torch.rand((zl, n, n), device='cuda').to(dt)
+    d = (torch.rand_like(u, dtype=torch.float32) * 2 - 1).to(dt)
+    plain = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    zop = ZSlabOp(op, use_cuda=True)
+    zop._halo = RcclHalo(loopback=True)
+    zfn = zop.autograd_function()
+    torch.autograd.set_multithreading_enabled(False)
+    for name, fn in (('plain op', plain), ('zslab', zfn)):
+        wall, host = timed(fn, u, d, steps)
+        print(f'{name:10s} {wl} {zl}x{n}^2: {wall:.4f} ms/step wall, {host:.4f} ms/step host', flush=True)
+        time.sleep(0.01)
+    zop.close()
+
+
 if __name__ == '__main__':
-    if len(sys.argv) > 3 and sys.argv[3] == 'profile':
+    if len(sys.argv) > 3 and sys.argv[3] == 'trace':
+        trace(int(sys.argv[1]), sys.argv[2])
+    elif len(sys.argv) > 3 and sys.argv[3] == 'profile':
         profile_host(int(sys.argv[1]), sys.argv[2])
     elif len(sys.argv) > 3 and sys.argv[3] == 'sweeps':
         time_sweeps(int(sys.argv[1]), sys.argv[2])
