@@ -43,6 +43,23 @@ extern "C" __global__ void __launch_bounds__(256) rd_dma(const unsigned* __restr
   if (lds[threadIdx.x] == 0x12345678u && n16 == 0) out[0] = 1;
 }
 
+// LDS-DMA from ONE wave per workgroup (the WS loader's situation: one wave per CU issues every piece), up to
+// `depth` pieces in flight
+extern "C" __global__ void __launch_bounds__(64) rd_dma1(const unsigned* __restrict__ src, unsigned* __restrict__ out,
+                                                        unsigned n16, int off) {
+  __shared__ __attribute__((aligned(1024))) unsigned lds[16 * 256];
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, 0x7fffffff, 0x00020000);
+  const int lane = threadIdx.x & 63;
+  unsigned k = 0;
+  for (unsigned w = blockIdx.x; w * 64u < n16; w += gridDim.x, ++k) {
+    __attribute__((address_space(3))) void* dst = (__attribute__((address_space(3))) void*)(&lds[(k & 15) * 256]);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst, 16, (w * 64u + lane) * 16u + (unsigned)off, 0, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0x0F7C);          // vmcnt <= 12
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  if (lds[threadIdx.x] == 0x12345678u && n16 == 0) out[0] = 1;
+}
+
 // streaming writes of 8 / 16 B per lane at byte offset `off` (the XM sweeps' output rows start 4-byte aligned)
 extern "C" __global__ void __launch_bounds__(256) wr_b64(unsigned* __restrict__ dst, unsigned n8, int off) {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)dst, (short)0, 0x7fffffff, 0x00020000);
@@ -83,12 +100,14 @@ def main():
         torch.cuda.synchronize()
         v = sorted(a.elapsed_time(b) for a, b in ev)
         return v[len(v) // 2]
-    for kname in ('rd_reg', 'rd_dma'):
+    for kname, grid, block in (('rd_reg', 4096, 256), ('rd_dma', 4096, 256), ('rd_dma1', 256, 64),
+                               ('rd_dma1', 512, 64)):
         fn = rt.load_function(code, kname, dev)
         for off in (0, 4, 8, 12, 16):
             args = struct.pack('<QQIi', src.data_ptr(), out.data_ptr(), n16, off)
-            ms = timed(lambda: rt.launch(fn, (4096,), (256,), args, stream))
-            print(f'{kname} offset {off:2d} B: {ms:.4f} ms {nbytes / ms / 1e6:7.0f} GB/s', flush=True)
+            ms = timed(lambda: rt.launch(fn, (grid,), (block,), args, stream))
+            label = kname if kname != 'rd_dma1' else f'rd_dma1 x{grid}'
+            print(f'{label} offset {off:2d} B: {ms:.4f} ms {nbytes / ms / 1e6:7.0f} GB/s', flush=True)
     dst = torch.empty(nbytes // 4 + 64, dtype=torch.int32, device='cuda')
     for kname, w in (('wr_b64', 8), ('wr_b128', 16)):
         fn = rt.load_function(code, kname, dev)
