@@ -122,14 +122,29 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
 
     centre = '_'.join('0' for _ in axes)
 
+    def load_v(prefix, voff):
+        """One buffer load at a per-lane byte offset (plane offset folded in, no scalar offset)."""
+        bits = 'b64' if esize == 8 else 'b32'
+        ty = 'u32x2' if esize == 8 else 'unsigned'
+        return (f'({ct})__builtin_bit_cast(T, ({ty})__builtin_amdgcn_raw_buffer_load_{bits}('
+                f'rs_{prefix}, {voff}, 0, 0))')
+
+    def store_v(prefix, voff, val):
+        bits = 'b64' if esize == 8 else 'b32'
+        ty = 'u32x2' if esize == 8 else 'unsigned'
+        return (f'__builtin_amdgcn_raw_buffer_store_{bits}(__builtin_bit_cast({ty}, (T)({val})), rs_{prefix}, '
+                f'{voff}, 0, 0);')
+
     def pull_loads(L, prefix, arr):
         for i in range(Q):
             k = key(dirs[i])
             if walls and any(dirs[i]):
                 if buf:
-                    L.append(f'  const bool bb{i} = (msk >> {i}) & 1u;')
-                    L.append(f'  const {ct} f{i} = bb{i} ? {load(prefix, arr, inv[i], f"{prefix}o_{centre}")} : '
-                             f'{load(prefix, arr, i, f"{prefix}o_{k}")};')
+                    # a bounced component is read from the cell itself: ONE load whose per-lane offset selects
+                    # (component, cell) — not both loads and a select
+                    L.append(f'  const unsigned vo{i} = ((msk >> {i}) & 1u) ? {prefix}o_{centre} + '
+                             f'(unsigned)({inv[i]} * {prefix}_qb) : {prefix}o_{k} + (unsigned)({i} * {prefix}_qb);')
+                    L.append(f'  const {ct} f{i} = {load_v(prefix, f"vo{i}")};')
                 else:
                     L.append(f'  const {ct} f{i} = {arr}[(msk >> {i}) & 1u ? (IDX){inv[i]} * {prefix}_q + '
                              f'{prefix}o_{centre} : (IDX){i} * {prefix}_q + {prefix}o_{k}];')
@@ -249,8 +264,9 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
         k = key(dirs[j])
         if walls and any(dirs[j]):
             if buf:
-                L.append(f'    if ((msk >> {j}) & 1u) {store("o", "out", inv[j], f"oo_{centre}", "v")}')
-                L.append(f'    else {store("o", "out", j, f"oo_{k}", "v")} }}')
+                L.append(f'    const unsigned vs = ((msk >> {j}) & 1u) ? oo_{centre} + (unsigned)({inv[j]} * o_qb) : '
+                         f'oo_{k} + (unsigned)({j} * o_qb);')
+                L.append(f'    {store_v("o", "vs", "v")} }}')
             else:
                 L.append(f'    out[(msk >> {j}) & 1u ? (IDX){inv[j]} * o_q + oo_{centre} : (IDX){j} * o_q + oo_{k}] '
                          f'= (T)v; }}')
