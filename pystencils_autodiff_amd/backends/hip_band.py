@@ -1,0 +1,321 @@
+"""Row-band schedule for half-precision 3-D stencils (fp16 storage, fp32 arithmetic) on gfx950.
+
+The ``zsum`` schedule tiles a plane in 256×8 tiles: a workgroup's share of a plane is eight 512-byte row segments,
+and the stores of a sweep reach ~5.4 TB/s (``scripts/probes/store_patterns.py``). Here a workgroup owns a BAND:
+``TY`` full rows of a plane, which in a dense row-major field is ONE contiguous block of ``TY·X`` halves.
+
+* loader wave: the band's rows ``y0-1 … y0+TY`` of plane ``q`` are one contiguous block as well, streamed into an
+  LDS slot by LDS-DMA (``buffer_load_dwordx4 … lds``, 1 KiB per wave instruction, rows outside the plane read as
+  zeros by the buffer range check, planes outside the domain from the z-slab halo buffers or zeros);
+  ``D`` planes in flight in a ring of ``D + 1`` slots, published by one workgroup barrier per plane.
+* compute lanes: lane ``t`` owns the 16-byte chunk ``col = t mod X/8`` (8 x-adjacent cells) of the ``R`` rows of
+  row group ``t div X/8``. Per plane it reads its ``R + 2`` input rows once (``ds_read_b128``), takes the x
+  neighbours from the adjacent lanes (DPP ``wave_shr/shl:1``; the wave's end lanes read one LDS dword; full rows
+  make columns 0 and X/8-1 the domain's x boundary), converts each value once to fp32 and runs packed FMAs over
+  the cell pairs ``(x+e, x+e+4)`` so every tap operand is a register pair as converted.
+* z partial sums (as ``zsum``): input plane ``q`` adds its taps to outputs ``q+1``, ``q``, ``q-1``; the three
+  accumulator sets rotate with the plane index (loop unrolled by 3, no moves); the first two and last two planes
+  of a chunk skip the taps of outputs outside it (uniform branches), so a chunk costs ``zc`` planes of FMAs.
+* stores: output ``q-1`` row by row, 16 bytes per lane, 1 KiB contiguous per wave instruction, non-temporal.
+
+Eligible: 3-D, every field fp16, one stencil field (radius ≤ 1), every store a linear combination of its taps
+(``zsum_plan`` with no centre-plane remainder), rows a multiple of 16 bytes. Measured against the ``zsum`` half ring
+in ``scripts/probes/rowblock27r.py`` (``profiles/r03_band_*.log``).
+"""
+import numpy as np
+
+from .hip_emitter import PRELUDE, MarchConfig, _field_params, _scalar_params, _ws_plane_base, zsum_plan
+from .printer import KernelExprPrinter
+
+__all__ = ['band_plans', 'band_geometry', 'band_choice', 'emit_band']
+
+
+def band_plans(ir):
+    """Per-store tap weights ``{(dz, dy, dx): coefficient}`` if the kernel fits the band schedule, else None."""
+    if ir.ndim != 3 or ir.has_index_dims or ir.periodic:
+        return None
+    if any(np.dtype(f.dtype.numpy_dtype).itemsize != 2 for f in ir.fields):
+        return None
+    stencil = ir.stencil_fields
+    if len(stencil) != 1 or any(r > 1 for r in ir.radius):
+        return None
+    if set(ir.fields) - set(ir.fields_written) - set(stencil):
+        return None                     # other (point) fields read
+    plans = zsum_plan(ir, MarchConfig(VE=8, ZSUM=True))
+    if plans is None or not 1 <= len(plans) <= 2:
+        return None
+    out = []
+    for pl in plans:
+        if pl['rest'] != 0 or pl['k'] != 0:
+            return None
+        w = {}
+        for dz, terms in pl['lin'].items():
+            for coeff, f, dy, dx, k in terms:
+                if f is not stencil[0] and f.name != stencil[0].name or k != 0:
+                    return None
+                w[(dz, dy, dx)] = w.get((dz, dy, dx), 0) + coeff
+        out.append(dict(field=pl['field'], w=w))
+    return out
+
+
+def band_geometry(X, TY, R, D):
+    """Launch / LDS geometry of a band of ``TY`` rows (``R`` per lane) on rows of ``X`` halves."""
+    CPR = X // 8
+    G = TY // R
+    ntask = G * CPR
+    NCT = -(-ntask // 64) * 64
+    NPIECE = (TY + 2) * CPR
+    NI = -(-NPIECE // 64)
+    SLOT = NI * 512
+    NS = D + 1
+    return dict(CPR=CPR, G=G, ntask=ntask, NCT=NCT, NT=NCT + 64, NPIECE=NPIECE, NI=NI, SLOT=SLOT, NS=NS,
+                lds_bytes=(NS * SLOT + 64) * 2)
+
+
+def _fits(X, TY, R, D):
+    g = band_geometry(X, TY, R, D)
+    return g['ntask'] % 64 == 0 and g['NCT'] <= 960 and D * g['NI'] <= 63 and g['lds_bytes'] <= 80 * 1024
+
+
+def band_choice(X, nstore=1):
+    """(TY, R, D) for rows of X halves, or None. Measured (scripts/probes/band_ab.py, profiles/r03_band_ab*.log):
+    8-row bands of 4 rows per lane with 2 planes in flight at X = 768 and 1024 (27-point 1024³: 0.895 ms vs
+    0.921 for 4-row bands of 2 rows per lane, 3 planes in flight); three workgroups per CU."""
+    if X % 8 or X < 128:
+        return None
+    rmax = 4 if nstore == 1 else 2
+    cands = [(8, 4, 2), (4, 2, 3), (8, 2, 3), (12, 4, 2), (16, 4, 2), (16, 2, 2), (32, 4, 2), (32, 2, 2)]
+    for TY, R, D in cands:
+        if R <= rmax and _fits(X, TY, R, D):
+            return TY, R, D
+    return None
+
+
+def emit_band(ir, name, cfg):
+    """HIP source of the band kernel (signature identical to the march / zsum kernels: fields, 2 halo pointers
+    per stencil field, Z Y X zlo zhi ylo yhi xlo xhi zc zstep ntx nty, scalars)."""
+    plans = band_plans(ir)
+    if plans is None:
+        raise ValueError('kernel is not eligible for the band schedule')
+    fixed = [f for f in ir.fields if f.has_fixed_shape]
+    X = cfg.BX
+    TY, R, D = cfg.BTY, cfg.BAND, cfg.D
+    g = band_geometry(X, TY, R, D)
+    CPR, G, NCT, NT, NPIECE, NI, SLOT, NS = (g[k] for k in ('CPR', 'G', 'NCT', 'NT', 'NPIECE', 'NI', 'SLOT', 'NS'))
+    assert D * NI <= 63 and NCT <= 960, (X, TY, R, D)
+    assert not fixed or int(fixed[0].spatial_shape[-1]) == X, 'band kernel compiled for another row length'
+    S = ir.stencil_fields[0]
+    pr = KernelExprPrinter('float', dict(ir.symbol_names))
+    W = []
+    for pl in plans:
+        W.append({k: f'(float)({pr.doprint_expr(v)})' for k, v in pl['w'].items() if v != 0})
+    NP = len(plans)
+
+    def A(si, s, o, p):
+        return f'S{si}_{s}_{o}_{p}'
+
+    params = _field_params(ir)
+    params += [f'const _Float16* __restrict__ hlo_{S.name}', f'const _Float16* __restrict__ hhi_{S.name}']
+    params += ['const int Z', 'const int Y', 'const int X', 'const int zlo', 'const int zhi', 'const int ylo',
+               'const int yhi', 'const int xlo', 'const int xhi', 'const int zc', 'const int zstep', 'const int ntx',
+               'const int nty']
+    params += _scalar_params(ir)
+    L = [PRELUDE, 'typedef unsigned u32x4 __attribute__((ext_vector_type(4)));']
+    L.append(f'// band schedule: {TY}-row bands of full {X}-element rows, {R} rows x 8 cells per lane, {NCT // 64} '
+             f'compute waves + LDS-DMA loader wave, {NS}-slot fp16 plane ring ({D} planes in flight), z partial sums '
+             f'in 3 rotating register sets, LDS {g["lds_bytes"]} B')
+    L.append(f'extern "C" __global__ void __launch_bounds__({NT}) {name}({", ".join(params)})\n{{')
+    L.append(f'  __shared__ __attribute__((aligned(1024))) _Float16 lds[{NS * SLOT + 64}];')
+    L.append('  const int tid = threadIdx.x, lane = tid & 63;')
+    L.append('  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);')
+    if cfg.MAP == 1:
+        L.append('  const int lb = blockIdx.x;')
+    else:
+        L.append('  // XCD-aware, bijective block remap: consecutive bands share one XCD (and its L2)')
+        L.append('  const int nb = gridDim.x, b = blockIdx.x;')
+        L.append('  const int per = nb >> 3, rem = nb & 7, xcd = b & 7, bi = b >> 3;')
+        L.append('  const int lb = (xcd < rem) ? xcd * (per + 1) + bi : rem * (per + 1) + (xcd - rem) * per + bi;')
+    L.append('  const int band = lb % nty, chunk = lb / nty;')
+    L.append(f'  const int y0 = band * {TY};')
+    L.append('  const int zb = zlo + chunk * zstep;       // zstep = zc, or the gap of a two-range launch')
+    L.append('  const int ze = min(zb + zc, zhi);')
+    L.append('  if (zb >= ze) return;')
+    L.append(f'  const i64 YX = (i64)Y * {X};')
+    L.append('  const int nplanes = ze - zb + 2;')
+    # ---- loader wave
+    L.append(f'  if (wave == {NCT // 64}) {{')
+    L.append(f'    int vo[{NI}];')
+    L.append('    #pragma unroll')
+    L.append(f'    for (int i = 0; i < {NI}; ++i) {{')
+    L.append('      const int k = i * 64 + lane;')
+    L.append(f'      vo[i] = k < {NPIECE} ? ((y0 - 1) * {X} * 2 + 16 * k) : 0x7ffffff0;   // row -1 / past Y: range check')
+    L.append('    }')
+    L.append('    auto issue = [&](const int q, const int slot) {')
+    L.append(f'      const _Float16* pb = {_ws_plane_base(S, 1, "q")};')
+    L.append(f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? pb : f_{S.name}), '
+             '(short)0, pb ? (int)(YX * 2) : 0, 0x00020000);')
+    L.append(f'      _Float16* dst = lds + slot * {SLOT};')
+    L.append('      #pragma unroll')
+    L.append(f'      for (int i = 0; i < {NI}; ++i)')
+    L.append('        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + i * 512), '
+             '16, vo[i], 0, 0, 0);')
+    L.append('    };')
+    L.append(f'    for (int i = 0; i < {D}; ++i)')
+    L.append('      if (i < nplanes) issue(zb - 1 + i, i);')
+    L.append('    for (int j = 0; j < nplanes; ++j) {')
+    L.append('      // barrier j publishes plane j: the planes issued after it stay in flight')
+    L.append(f'      const int after = min({D - 1}, nplanes - 1 - j);')
+    L.append('      switch (after) {')
+    for a in range(D):
+        L.append(f'        case {a}: asm volatile("s_waitcnt vmcnt({a * NI})" ::: "memory"); break;')
+    L.append('      }')
+    L.append('      __builtin_amdgcn_s_barrier();')
+    L.append(f'      if (j + {D} < nplanes) issue(zb - 1 + j + {D}, (j + {D}) % {NS});')
+    L.append('    }')
+    L.append('    return;')
+    L.append('  }')
+    # ---- compute lanes
+    L.append(f'  const bool active = tid < {g["ntask"]};')
+    L.append(f'  const int t = active ? tid : {g["ntask"] - 1};')
+    L.append(f'  const int grp = t / {CPR}, col = t - grp * {CPR};')
+    L.append(f'  const int lofs = grp * {R * X} + col * 8;          // slot row grp*R = input row y0 + grp*R - 1')
+    L.append('  const int x = col * 8;')
+    L.append(f'  const bool lmask = col == 0, rmask = col == {CPR - 1};')
+    if cfg.BMASK:
+        L.append('  const bool xfull = x >= xlo && x + 8 <= xhi;')
+    L.append(f'  const int yrow0 = y0 + grp * {R};')
+    L.append(f'  const unsigned sofs = (unsigned)(yrow0 * {X} + x) * 2u;')
+    if cfg.BMASK:
+        L.append('  unsigned rowok = 0u;                           // rows of the lane inside [ylo, yhi), one bit each')
+        L.append(f'  for (int o = 0; o < {R}; ++o) rowok |= (active && yrow0 + o >= ylo && yrow0 + o < yhi) ? (1u << o) : 0u;')
+    L.append('  // edge dword (halves, from the lane\'s chunk): lane 0 the dword left of it, lane 63 the one right of it,')
+    L.append('  // the other lanes consecutive dwords of the wave\'s block (conflict-free, unused)')
+    L.append('  const int eoff = 2 * (lane == 0 ? -1 : (lane == 63 ? 256 : lane)) - 8 * lane;')
+    for si in range(NP):
+        for s in range(3):
+            for o in range(R):
+                L.append('  f32x2 ' + ', '.join(f'{A(si, s, o, p)} = (f32x2)(0.f)' for p in range(4)) + ';')
+    store_field = [pl['field'] for pl in plans]
+
+    def step(k, ind):
+        sp, s0, sn = (k + 2) % 3, k, (k + 1) % 3
+        B = [f'{ind}if (jj < nplanes) {{', f'{ind}  __syncthreads();',
+             f'{ind}  const _Float16* sl = lds + (jj % {NS}) * {SLOT} + lofs;',
+             ]
+        if cfg.BTRIM:
+            B.append(f'{ind}  const bool nd_p = jj >= 2, nd_0 = jj >= 1 && jj + 1 < nplanes, nd_n = jj + 2 < nplanes;')
+        first = set()
+        for r in range(R + 2):
+            B.append(f'{ind}  {{')
+            B.append(f'{ind}    const _Float16* rp = sl + {r * X};')
+            B.append(f'{ind}    const f16x8 v = *(const f16x8*)rp;')
+            B.append(f'{ind}    const u32x4 d = __builtin_bit_cast(u32x4, v);')
+            B.append(f'{ind}    const unsigned e = *(const unsigned*)(rp + eoff);')
+            B.append(f'{ind}    const unsigned lw = __builtin_amdgcn_update_dpp(e, d.w, 0x138, 0xf, 0xf, false);   '
+                     '// wave_shr:1')
+            B.append(f'{ind}    const unsigned rw = __builtin_amdgcn_update_dpp(e, d.x, 0x130, 0xf, 0xf, false);   '
+                     '// wave_shl:1')
+            B.append(f'{ind}    const _Float16 l = lmask ? (_Float16)0 : __builtin_bit_cast(f16x2, lw)[1];')
+            B.append(f'{ind}    const _Float16 rr = rmask ? (_Float16)0 : __builtin_bit_cast(f16x2, rw)[0];')
+            B.append(f'{ind}    const f32x2 P0 = {{(float)l, (float)v[3]}}, P1 = {{(float)v[0], (float)v[4]}}, '
+                     'P2 = {(float)v[1], (float)v[5]};')
+            B.append(f'{ind}    const f32x2 P3 = {{(float)v[2], (float)v[6]}}, P4 = {{(float)v[3], (float)v[7]}}, '
+                     'P5 = {(float)v[4], (float)rr};')
+            if not cfg.BTRIM:
+                # every set every plane: one block, dx outer then the three sets, rows and pairs (12-36 independent
+                # FMAs between two dependent ones)
+                for dx in (-1, 0, 1):
+                    for st, dz in ((sp, 1), (s0, 0), (sn, -1)):
+                        for si in range(NP):
+                            for o in range(R):
+                                dy = r - o - 1
+                                wv = W[si].get((dz, dy, dx)) if -1 <= dy <= 1 else None
+                                if wv is None:
+                                    continue
+                                for p in range(4):
+                                    acc = A(si, st, o, p)
+                                    term = f'{wv} * P{p + dx + 1}'
+                                    if dz == -1 and (si, o, p) not in first:
+                                        first.add((si, o, p))
+                                        B.append(f'{ind}    {acc} = {term};')
+                                    else:
+                                        B.append(f'{ind}    {acc} = {acc} + {term};')
+                B.append(f'{ind}  }}')
+                continue
+            for st, dz, flag in ((sp, 1, 'nd_p'), (s0, 0, 'nd_0'), (sn, -1, 'nd_n')):
+                body = []
+                # tap by tap (dx outer): the chains of the rows' and pairs' accumulators interleave (8-12 independent
+                # FMAs between two dependent ones)
+                for dx in (-1, 0, 1):
+                    for si in range(NP):
+                        for o in range(R):
+                            dy = r - o - 1
+                            wv = W[si].get((dz, dy, dx)) if -1 <= dy <= 1 else None
+                            if wv is None:
+                                continue
+                            for p in range(4):
+                                acc = A(si, st, o, p)
+                                term = f'{wv} * P{p + dx + 1}'
+                                if dz == -1 and (si, o, p) not in first:
+                                    first.add((si, o, p))
+                                    body.append(f'{ind}      {acc} = {term};')
+                                else:
+                                    body.append(f'{ind}      {acc} = {acc} + {term};')
+                if body:
+                    B.append(f'{ind}    if ({flag}) {{')
+                    B += body
+                    B.append(f'{ind}    }}')
+            B.append(f'{ind}  }}')
+        # outputs of q+1 that received no tap this plane (no dz = -1 taps in some row) start from zero
+        for si in range(NP):
+            for o in range(R):
+                for p in range(4):
+                    if (si, o, p) not in first:
+                        B.append(f'{ind}  {A(si, sn, o, p)} = (f32x2)(0.f);')
+        B.append(f'{ind}  if (jj >= 2) {{')
+        for si, fld in enumerate(store_field):
+            B.append(f'{ind}    {{')
+            B.append(f'{ind}      const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc('
+                     f'(void*)(f_{fld.name} + (i64)(zb - 2 + jj) * YX), (short)0, (int)(YX * 2), 0x00020000);')
+            for o in range(R):
+                vals = ', '.join(f'(_Float16){A(si, sp, o, p)}.{c}' for c in 'xy' for p in range(4))
+                st = (f'__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ov), ors, '
+                      f'sofs + {o * X * 2}u, 0, 2);')
+                if not cfg.BMASK:
+                    # every row of every band inside [ylo, yhi), x range = whole rows (checked at plan time)
+                    B.append(f'{ind}      {{ const f16x8 ov = {{{vals}}}; {st} }}')
+                    continue
+                B.append(f'{ind}      if (rowok & {1 << o}u) {{')
+                B.append(f'{ind}        const f16x8 ov = {{{vals}}};')
+                B.append(f'{ind}        if (xfull) {{')
+                B.append(f'{ind}          {st}')
+                if cfg.XB:
+                    B.append(f'{ind}        }} else {{   // x border cells: zeros')
+                    B.append(f'{ind}          f16x8 zv = ov;')
+                    B.append(f'{ind}          #pragma unroll')
+                    B.append(f'{ind}          for (int q8 = 0; q8 < 8; ++q8) if (x + q8 < xlo || x + q8 >= xhi) zv[q8] = '
+                             '(_Float16)0;')
+                    B.append(f'{ind}          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, zv), ors, '
+                             f'sofs + {o * X * 2}u, 0, 2);')
+                else:
+                    B.append(f'{ind}        }} else {{   // x border: interior cells only')
+                    B.append(f'{ind}          #pragma unroll')
+                    B.append(f'{ind}          for (int q8 = 0; q8 < 8; ++q8) if (x + q8 >= xlo && x + q8 < xhi)')
+                    B.append(f'{ind}            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, '
+                             f'ov[q8]), ors, sofs + {o * X * 2}u + 2 * q8, 0, 0);')
+                B.append(f'{ind}        }}')
+                B.append(f'{ind}      }}')
+            B.append(f'{ind}    }}')
+        B.append(f'{ind}  }}')
+        B.append(f'{ind}  ++jj;')
+        B.append(f'{ind}}}')
+        return B
+    L.append('  int jj = 0;')
+    L.append('  #pragma unroll 1')
+    L.append('  while (jj < nplanes) {')
+    for k in range(3):
+        L += step(k, '    ')
+    L.append('  }')
+    L.append('}')
+    return '\n'.join(L) + '\n'
+

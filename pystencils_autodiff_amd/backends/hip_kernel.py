@@ -14,13 +14,55 @@ import os
 import numpy as np
 
 from . import hip_runtime as rt
+from .hip_band import band_choice, band_geometry, band_plans, emit_band
 from .hip_emitter import (MarchConfig, emit_generic, emit_march, emit_pointwise, emit_zsum, march_geometry, ws_geometry,
                           zsum_plan)
 
 __all__ = ['HipStencilKernel', 'default_march_config']
 
 
-def default_march_config(ir, ve, shape=None, tuning=None):
+# row-band chunk length (planes per workgroup), settled A/B rounds through the kernels (scripts/probes/band_ab.py,
+# profiles/r03_band_ab*.log): box stencils (27 taps) 24 planes (768³ 0.375 vs 0.385 ms at 8, zsum ring 0.395),
+# star stencils 8 (768³ 7-point fp16 0.318 vs 0.324 at 16, 0.329 at 24, zsum ring 0.344). Fewer workgroups than
+# BAND_MIN_WG (z-slabs of a few planes: 96×768² 27-point 0.052 ms either way) keep the zsum ring.
+BAND_ZC_BOX, BAND_ZC_STAR = 24, 8
+BAND_MIN_WG = 1536
+
+
+def _band_config(ir, ve, shape, over):
+    """The row-band schedule (``hip_band``) for fp16 stencils it fits, when the row length is known and no tile
+    override asks for another schedule (``BAND=0`` or ``PSAD_BAND=0`` turn it off, ``BAND=R`` / ``BTY`` pick
+    rows per lane / band height)."""
+    if shape is None or ir.ndim != 3 or os.environ.get('PSAD_BAND', '1') == '0':
+        return None
+    if 'BAND' in over:
+        if not int(over['BAND']):
+            return None
+    elif any(k in over for k in ('CX', 'WX', 'NR', 'NW', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D')):
+        return None
+    plans = band_plans(ir)
+    X = int(shape[-1])
+    choice = band_choice(X, len(plans)) if plans else None
+    if choice is None:
+        return None
+    TY, R, D = choice
+    if 'BAND' in over:
+        R = int(over['BAND'])
+    TY = int(over.get('BTY', TY if TY % R == 0 else R * max(1, TY // R)))
+    D = int(over.get('D', D))
+    g = band_geometry(X, TY, R, D)
+    if TY % R or g['NCT'] > 960 or D * g['NI'] > 63 or g['lds_bytes'] > 160 * 1024:
+        raise ValueError(f'band schedule: BTY={TY} BAND={R} D={D} do not fit rows of {X} elements')
+    ntaps = max(len(pl['w']) for pl in plans)
+    zc = int(over.get('ZMIN', BAND_ZC_BOX if ntaps > 12 else BAND_ZC_STAR))
+    if 'BAND' not in over and -(-int(shape[-2]) // TY) * -(-int(shape[0]) // zc) < BAND_MIN_WG:
+        return None
+    return MarchConfig(VE=ve, BAND=R, BTY=TY, BX=X, D=D, ZSUM=True, NT_STORE=True, ZMIN=zc,
+                       ZMAX=int(over.get('ZMAX', zc)), BLK=int(over.get('BLK', 512)), MAP=int(over.get('MAP', 0)),
+                       BTRIM=bool(int(over.get('BTRIM', 1))))
+
+
+def default_march_config(ir, ve, shape=None, tuning=None, band=True):
     """Tile shape for a kernel and field shape (measured on MI355X).
 
     3-D stencils linear in their off-centre planes use the z-partial-sum schedule (``emit_zsum``):
@@ -94,7 +136,7 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             over[k.strip()] = v.strip() if k.strip() == 'VIEW2D' else int(v)
     for k, v in over.items():
         if k not in ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D',
-                     'ZC', 'BLOCKS', 'MAP'):
+                     'ZC', 'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM'):
             raise ValueError(f"unknown tile parameter '{k}' (gpu_indexing_params / PSAD_MARCH)")
         if k in ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'MAP'):
             cfg[k] = int(v)
@@ -102,6 +144,9 @@ def default_march_config(ir, ve, shape=None, tuning=None):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
         elif k == 'VIEW2D':
             cfg[k] = str(v)
+    bc = _band_config(ir, ve, shape, over) if band else None
+    if bc is not None:
+        return bc
     if 'NW' in over and 'WX' not in over:
         cfg['WX'] = min(cfg['WX'], cfg['NW'])
     if cfg['ZSUM'] and zsum_plan(ir, MarchConfig(VE=ve, **cfg)) is None:
@@ -201,8 +246,8 @@ class HipStencilKernel:
     def _vec_elems(self):
         return 16 // self.ir.fields[0].dtype.itemsize
 
-    def _march_cfg(self, ve, shape=None):
-        return default_march_config(self.ir, ve, shape, self.kernel.tuning)
+    def _march_cfg(self, ve, shape=None, band=True):
+        return default_march_config(self.ir, ve, shape, self.kernel.tuning, band=band)
 
     def source(self, variant):
         if variant not in self._variants:
@@ -210,6 +255,9 @@ class HipStencilKernel:
             kname = f"{self.name}_{kind}"
             if kind == 'pointwise':
                 src = emit_pointwise(self.ir, kname)
+            elif kind == 'march' and variant[1].BAND:
+                kname = f"{self.name}_band"
+                src = emit_band(self.ir, kname, variant[1])
             elif kind == 'march' and variant[1].ZSUM:
                 kname = f"{self.name}_zsum"
                 src = emit_zsum(self.ir, kname, variant[1])
@@ -510,8 +558,11 @@ class HipStencilKernel:
             Y = 1
             (zlo, zhi), (xlo, xhi) = bounds
             ylo, yhi = 0, 1
-        ntx = max(1, math.ceil((X if cfg.XB else xhi) / cfg.TX))
-        nty = max(1, math.ceil(yhi / cfg.TY))
+        if cfg.BAND:            # full-row bands (hip_band): one band column, x handled inside the kernel
+            ntx, nty = 1, max(1, math.ceil(yhi / cfg.BTY))
+        else:
+            ntx = max(1, math.ceil((X if cfg.XB else xhi) / cfg.TX))
+            nty = max(1, math.ceil(yhi / cfg.TY))
         nt = ntx * nty
         nz = max(0, zhi - zlo)
         # chunk length: aim at ~2 workgroups per CU (512 blocks), ZMIN..ZMAX planes per chunk (each chunk
@@ -565,7 +616,7 @@ class HipStencilKernel:
             # rows whose pitch is not a multiple of 16 bytes but of 4 (fp32 / fp64, fp16 with X even): the LDS-DMA
             # ring still takes 16-byte pieces (dword-aligned; the image in LDS keeps its layout) and zero-fills
             # past each row end (XM) — where the WS schedule applies
-            probe = self._march_cfg(ve, shape)
+            probe = self._march_cfg(ve, shape, band=False)
             xm = bool(probe.WS) and ws_geometry(ir, probe) is not None
         xo = False
         if not xm and not fits(ve) and esize == 2 and not ir.has_index_dims and os.environ.get('PSAD_XO', '1') != '0' and \
@@ -574,11 +625,11 @@ class HipStencilKernel:
             # fp16 rows starting on half dwords (X odd, or an odd-element base): the half-precision LDS-DMA ring
             # loads such rows one element early and shifts them back in LDS (XO) — 255³ fp16 instead of the
             # register-prefetch path
-            probe = self._march_cfg(ve, shape)
+            probe = self._march_cfg(ve, shape, band=False)
             ws_p = ws_geometry(ir, probe) if probe.WS else None
             xo = ws_p is not None and ws_p['kind'] == 'h'
         if xm or xo:
-            cfg = MarchConfig(**{**self._march_cfg(ve, shape).__dict__, 'XM': True,
+            cfg = MarchConfig(**{**self._march_cfg(ve, shape, band=False).__dict__, 'XM': True,
                                  'XO': (1 if X % 2 else 2) if xo else 0})
         else:
             # widest plane-load vector the rows allow: 16 bytes (and the LDS-DMA loader) when the row pitch is a
@@ -590,7 +641,10 @@ class HipStencilKernel:
                 # 2-D rows of scalar loads: the one-thread-per-cell schedule streams them faster (4097² 5-point
                 # 0.028 vs 0.046 ms, 4095×4094 0.027 vs 0.043; profiles/r02_misaligned.log)
                 return self._plan_generic(tensors, shape, device)
-            cfg = self._march_cfg(ve, shape)
+            # the row-band schedule (hip_band): 16-byte pieces and stores on every field and halo, 32-bit plane offsets
+            band_ok = ve == self._vec_elems() and all(t.data_ptr() % 16 == 0 for t in tensors) and \
+                int(np.prod(shape[1:])) * esize < 2 ** 31 - 1024
+            cfg = self._march_cfg(ve, shape, band=band_ok)
         if halo_list and ir.ndim == 2 and cfg.VIEW2D == 'yx':
             cfg = MarchConfig(**{**cfg.__dict__, 'VIEW2D': 'zy'})
         from .hip_emitter import ncomp
@@ -609,6 +663,11 @@ class HipStencilKernel:
         if x_border and cfg.ZSUM and (xlo > 0 or xhi < shape[-1]) and \
                 not (ir.ndim == 2 and cfg.VIEW2D == 'zy'):
             cfg = MarchConfig(**{**cfg.__dict__, 'XB': True})
+        if cfg.BAND:
+            # unmasked stores when every band row lies in [ylo, yhi) and the x range is whole rows
+            g0 = self.march_launch_geometry(shape, cfg, z_range, z_limits=z_limits)
+            if not (g0['ylo'] == 0 and g0['yhi'] == g0['nty'] * cfg.BTY and g0['xlo'] == 0 and g0['xhi'] == g0['X']):
+                cfg = MarchConfig(**{**cfg.__dict__, 'BMASK': True})
         variant = ('march', cfg)
         fn = self.function(variant, device)
         ws = ws_geometry(ir, cfg)
@@ -630,8 +689,8 @@ class HipStencilKernel:
                                           'nty')]
         kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics) + \
             [self._scalar_kind()] * len(ir.scalars)
-        return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics, xb=cfg.XB,
-                     block=ws['block'] if ws else cfg.NT)
+        block = ws['block'] if ws else (band_geometry(cfg.BX, cfg.BTY, cfg.BAND, cfg.D)['NT'] if cfg.BAND else cfg.NT)
+        return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics, xb=cfg.XB, block=block)
 
 
 class _Plane:

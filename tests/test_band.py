@@ -1,0 +1,209 @@
+"""Row-band schedule (``backends/hip_band.py``): fp16 stencils on full-width bands of rows.
+
+CPU part: eligibility (one fp16 stencil field, linear taps, radius 1), the (band height, rows per lane, depth)
+choice and that the emitted kernels hiprtc-compile for gfx950. GPU part (``-m gpu``): forward and adjoint vs
+the float64 oracle (fp16 tolerance 1e-3·max|ref|, tests/test_gpu_parity.py), ``None`` boundary handling
+(interior-only stores, masked variant), ragged band counts, the z-slab launch pattern (halo planes read in place,
+two-range face launches) bitwise equal to one full launch, chunk-length independence (bitwise), misaligned views
+falling back to the zsum ring, and a two-output kernel."""
+import numpy as np
+import pytest
+import sympy as sp
+
+import pystencils_autodiff_amd as pa
+from oracle import evaluate as OE
+from pystencils_autodiff_amd import ps
+from pystencils_autodiff_amd import workloads as W
+from pystencils_autodiff_amd.backends.hip_band import band_choice, band_geometry, band_plans
+from pystencils_autodiff_amd.backends.hip_kernel import HipStencilKernel, default_march_config
+from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+from tests.conftest import assert_close_rel
+
+TOL16 = 1e-3
+
+
+def _kernel(ac, bh='zeros', name='bandk', **tun):
+    return StencilKernel(ac, boundary_handling=bh, function_name=name, target='gpu', gpu_indexing_params=tun)
+
+
+def test_band_eligibility():
+    op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
+    for ac in (op.forward_assignments, op.backward_assignments):
+        plans = band_plans(HipStencilKernel(_kernel(ac)).ir)
+        assert plans is not None and len(plans) == 1 and len(plans[0]['w']) == 27
+    star = pa.AutoDiffOp(W.diffusion_7pt(dtype='float16'), boundary_handling='zeros')
+    assert len(band_plans(HipStencilKernel(_kernel(star.forward_assignments)).ir)[0]['w']) == 7
+    # fp32 storage, a second field read pointwise, radius 2: not the band schedule
+    f32 = pa.AutoDiffOp(W.stencil_27pt(dtype='float32'), boundary_handling='zeros')
+    assert band_plans(HipStencilKernel(_kernel(f32.forward_assignments)).ir) is None
+    u, v, out = ps.fields('u, v, out: float16[3d]')
+    two = ps.AssignmentCollection({out.center: u[1, 0, 0] + u[-1, 0, 0] * v.center})
+    assert band_plans(HipStencilKernel(_kernel(two)).ir) is None
+    wide = ps.AssignmentCollection({out.center: u[2, 0, 0] + u.center})
+    assert band_plans(HipStencilKernel(_kernel(wide)).ir) is None
+
+
+def test_band_choice_and_geometry():
+    assert band_choice(768) == (8, 4, 2)
+    assert band_choice(1024) == (8, 4, 2) and band_choice(768, 2)[1] == 2
+    assert band_choice(264) is None and band_choice(100) is None and band_choice(96) is None
+    for X in (256, 512, 768, 1024, 640, 2048):
+        c = band_choice(X)
+        if c is None:
+            continue
+        TY, R, D = c
+        g = band_geometry(X, TY, R, D)
+        assert g['ntask'] % 64 == 0 and g['NCT'] <= 960 and D * g['NI'] <= 63 and g['lds_bytes'] <= 80 * 1024
+
+
+@pytest.mark.parametrize('shape,expect', [((768, 768, 768), 4), ((1024, 1024, 1024), 4), ((96, 768, 768), 0),
+                                          ((64, 256, 256), 0), ((40, 40, 264), 0), ((512, 1024, 1024), 4)])
+def test_band_default_selection(shape, expect):
+    op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
+    cfg = default_march_config(HipStencilKernel(_kernel(op.forward_assignments)).ir, 8, shape)
+    assert cfg.BAND == expect, cfg
+    # overrides of the zsum tile (or BAND=0) keep the zsum schedule
+    cfg = default_march_config(HipStencilKernel(_kernel(op.forward_assignments)).ir, 8, shape, {'BAND': 0})
+    assert cfg.BAND == 0
+
+
+def test_band_sources_compile():
+    from pystencils_autodiff_amd.backends import hip_runtime as rt
+    from pystencils_autodiff_amd.backends.hip_emitter import MarchConfig
+    for ac in (pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros').backward_assignments,
+               pa.AutoDiffOp(W.diffusion_7pt(dtype='float16'), boundary_handling='zeros').forward_assignments):
+        hk = HipStencilKernel(_kernel(ac))
+        cfg = default_march_config(hk.ir, 8, (32, 64, 256), {'BAND': 4})
+        for c in (cfg, MarchConfig(**{**cfg.__dict__, 'BMASK': True}), MarchConfig(**{**cfg.__dict__, 'BTRIM': False}),
+                  MarchConfig(**{**cfg.__dict__, 'BMASK': True, 'XB': True})):
+            src, kname = hk.source(('march', c))
+            assert kname.endswith('_band') and 'band schedule' in src
+            assert len(rt.compile_hip(src)) > 0
+
+
+# ---------------------------------------------------------------------------------------------------------- GPU
+def _torch():
+    return pytest.importorskip('torch')
+
+
+CASES = [('27pt', W.stencil_27pt), ('7pt_f16', lambda: W.diffusion_7pt(dtype='float16')),
+         ('asym_f16', lambda: W.asym_7pt(dtype='float16'))]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', CASES, ids=lambda c: c[0])
+@pytest.mark.parametrize('shape', [(11, 24, 256), (9, 21, 256), (7, 16, 768), (5, 12, 1024)])
+@pytest.mark.parametrize('bh', ['zeros', None])
+def test_band_vs_oracle(case, shape, bh):
+    """Forward and adjoint sweeps on the band schedule vs the float64 oracle; Y not a multiple of the band height
+    (ragged last band) and interior-only stores take the masked variant."""
+    torch = _torch()
+    op = pa.AutoDiffOp(case[1](), boundary_handling=bh)
+    rng = np.random.default_rng(sum(shape))
+    for which, ac in (('f', op.forward_assignments), ('b', op.backward_assignments)):
+        k = _kernel(ac, bh, f'band_{which}', BAND=band_choice(shape[-1])[1]).compile()
+        ins = {f.name: rng.uniform(-1, 1, shape).astype(np.float16) for f in k.ir.fields_read}
+        ref = OE.evaluate(ac, {n: a.astype(np.float64) for n, a in ins.items()}, boundary_handling=bh)
+        outs = {f.name: torch.zeros(shape, dtype=torch.float16, device='cuda') for f in k.ir.fields_written}
+        k(**{n: torch.from_numpy(a).cuda() for n, a in ins.items()}, **outs)
+        torch.cuda.synchronize()
+        cfg = k.last_variant[1]
+        assert k.last_variant[0] == 'march' and cfg.BAND > 0, cfg
+        whole = bh == 'zeros' and shape[1] % cfg.BTY == 0
+        assert cfg.BMASK == (not whole), cfg
+        for n, t in outs.items():
+            assert_close_rel(t.double().cpu().numpy(), ref[n], TOL16, f'{case[0]} {which} {n} {shape} {bh}')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('bh', ['zeros', None])
+def test_band_zslab_launch_pattern_bitwise(bh):
+    """z-slab sweep launches (interior z range, then both faces in one two-range launch reading the halo planes in
+    place) == one full-domain launch, bitwise, on the band schedule."""
+    torch = _torch()
+    from pystencils_autodiff_amd.zslab import ZSlabOp
+    op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling=bh)
+    k = _kernel(op.forward_assignments, bh, 'bandz', BAND=4).compile()
+    g = torch.Generator().manual_seed(3)
+    Z = 30
+    u = (torch.rand((Z, 40, 256), generator=g) * 2 - 1).half().cuda()
+    full = torch.zeros_like(u)
+    k(u=u, out=full)
+    assert k.last_variant[1].BAND > 0
+    kz = None if bh == 'zeros' else (1, Z - 1)
+    outs = []
+    for a, b in [(0, 11), (11, 19), (19, Z)]:
+        sl = u[a:b].contiguous()
+        out = torch.zeros_like(sl)
+        lo = u[a - 1:a].contiguous() if a > 0 else None
+        hi = u[b:b + 1].contiguous() if b < Z else None
+        zl = None if kz is None else (max(0, kz[0] - a), min(b - a, kz[1] - a))
+        inner, faces = ZSlabOp._launches(b - a, 1, zl or (0, b - a))
+        if inner:
+            k(u=sl, out=out, z_range=inner, z_limits=zl)
+        ZSlabOp._launch_faces(k, {'u': (lo, hi)}, faces, zl, {'u': sl, 'out': out})
+        assert k.last_variant[1].BAND > 0
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(outs), full)
+    ref = OE.evaluate(op.forward_assignments, {'u': u.double().cpu().numpy()}, boundary_handling=bh)['out']
+    assert_close_rel(full.double().cpu().numpy(), ref, TOL16)
+
+
+@pytest.mark.gpu
+def test_band_chunk_length_and_trim_bitwise():
+    """Every output plane sees the same FMA sequence whatever the chunk length and with or without the trimmed
+    first / last planes: results bitwise equal."""
+    torch = _torch()
+    op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
+    g = torch.Generator().manual_seed(11)
+    u = (torch.rand((37, 32, 768), generator=g) * 2 - 1).half().cuda()
+    res = []
+    for tun in ({'BAND': 4}, {'BAND': 4, 'ZMIN': 5, 'ZMAX': 5}, {'BAND': 4, 'ZMIN': 16, 'ZMAX': 16},
+                {'BAND': 4, 'BTRIM': 0, 'ZMIN': 9, 'ZMAX': 9}):
+        k = _kernel(op.forward_assignments, 'zeros', 'bandc', **tun).compile()
+        out = torch.full_like(u, float('nan'))
+        k(u=u, out=out)
+        assert k.last_variant[1].BAND == 4
+        res.append(out)
+    torch.cuda.synchronize()
+    for r in res[1:]:
+        assert torch.equal(r, res[0])
+
+
+@pytest.mark.gpu
+def test_band_misaligned_views_fall_back():
+    """A field view whose base is not 16-byte aligned cannot take the band schedule's 16-byte pieces: the zsum
+    half ring (XO rows) runs instead; the same kernel object on an aligned view takes the band schedule again."""
+    torch = _torch()
+    op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
+    k = _kernel(op.forward_assignments, 'zeros', 'bandm', BAND=4).compile()
+    shape = (6, 16, 256)
+    base = (torch.rand(int(np.prod(shape)) + 8) * 2 - 1).half().cuda()
+    for off, band in ((1, False), (8, True)):
+        u = base[off:off + int(np.prod(shape))].view(shape)
+        out = torch.zeros(shape, dtype=torch.float16, device='cuda')
+        k(u=u, out=out)
+        torch.cuda.synchronize()
+        assert (k.last_variant[1].BAND > 0) == band, k.last_variant
+        ref = OE.evaluate(op.forward_assignments, {'u': u.double().cpu().numpy()}, boundary_handling='zeros')['out']
+        assert_close_rel(out.double().cpu().numpy(), ref, TOL16, f'offset {off}')
+
+
+@pytest.mark.gpu
+def test_band_two_outputs():
+    """Two outputs from one stencil field (two z-partial-sum accumulator sets per cell, 2 rows per lane)."""
+    torch = _torch()
+    u, a, b = ps.fields('u, a, b: float16[3d]')
+    ac = ps.AssignmentCollection({a.center: u[1, 0, 0] - 2 * u.center + u[0, -1, 1],
+                                  b.center: sp.Float(0.25) * (u[0, 0, 1] + u[-1, 1, 0] + u[1, 1, 1])})
+    k = _kernel(ac, 'zeros', 'band2', BAND=2).compile()
+    shape = (10, 24, 256)
+    x = np.random.default_rng(2).uniform(-1, 1, shape).astype(np.float16)
+    outs = {n: torch.zeros(shape, dtype=torch.float16, device='cuda') for n in ('a', 'b')}
+    k(u=torch.from_numpy(x).cuda(), **outs)
+    torch.cuda.synchronize()
+    assert k.last_variant[1].BAND == 2, k.last_variant
+    ref = OE.evaluate(ac, {'u': x.astype(np.float64)}, boundary_handling='zeros')
+    for n in ('a', 'b'):
+        assert_close_rel(outs[n].double().cpu().numpy(), ref[n], TOL16, n)
