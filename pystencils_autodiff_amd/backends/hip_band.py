@@ -290,19 +290,22 @@ def emit_band(ir, name, cfg):
                 B.append(f'{ind}        if (xfull) {{')
                 B.append(f'{ind}          {st}')
                 if cfg.XB:
-                    B.append(f'{ind}        }} else {{   // x border cells: zeros')
-                    B.append(f'{ind}          f16x8 zv = ov;')
-                    B.append(f'{ind}          #pragma unroll')
-                    B.append(f'{ind}          for (int q8 = 0; q8 < 8; ++q8) if (x + q8 < xlo || x + q8 >= xhi) zv[q8] = '
-                             '(_Float16)0;')
+                    # x border cells: zeros (the row is stored whole); each cell selected on its own
+                    sel = ', '.join(f'(x + {q8} >= xlo && x + {q8} < xhi) ? (_Float16){A(si, sp, o, q8 % 4)}.'
+                                    f'{"x" if q8 < 4 else "y"} : (_Float16)0' for q8 in range(8))
+                    B.append(f'{ind}        }} else {{')
+                    B.append(f'{ind}          const f16x8 zv = {{{sel}}};')
                     B.append(f'{ind}          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, zv), ors, '
                              f'sofs + {o * X * 2}u, 0, 2);')
                 else:
-                    B.append(f'{ind}        }} else {{   // x border: interior cells only')
-                    B.append(f'{ind}          #pragma unroll')
-                    B.append(f'{ind}          for (int q8 = 0; q8 < 8; ++q8) if (x + q8 >= xlo && x + q8 < xhi)')
-                    B.append(f'{ind}            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, '
-                             f'ov[q8]), ors, sofs + {o * X * 2}u + 2 * q8, 0, 0);')
+                    # x border: interior cells only, one 2-byte store per cell, each converted on its own (a lane
+                    # extracted from the packed f16x8 was stored as element 0 for every cell by hipcc 7.2)
+                    B.append(f'{ind}        }} else {{')
+                    for q8 in range(8):
+                        cell = f'(_Float16){A(si, sp, o, q8 % 4)}.{"x" if q8 < 4 else "y"}'
+                        B.append(f'{ind}          if (x + {q8} >= xlo && x + {q8} < xhi) '
+                                 f'__builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, {cell}), '
+                                 f'ors, sofs + {o * X * 2 + 2 * q8}u, 0, 0);')
                 B.append(f'{ind}        }}')
                 B.append(f'{ind}      }}')
             B.append(f'{ind}    }}')

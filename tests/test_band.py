@@ -207,3 +207,29 @@ def test_band_two_outputs():
     ref = OE.evaluate(ac, {'u': x.astype(np.float64)}, boundary_handling='zeros')
     for n in ('a', 'b'):
         assert_close_rel(outs[n].double().cpu().numpy(), ref[n], TOL16, n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('bh', ['zeros', None])
+def test_band_through_the_op(bh, monkeypatch):
+    """The drop-in op (``create_tensorflow_op(backend='torch_native')``) on the band schedule (forced with
+    ``PSAD_MARCH=BAND=4``): forward and adjoint vs the oracle; with ``None`` the op asks the kernel for the x ends of
+    its rows (x_border, zeros) — the band kernel stores them as part of whole rows."""
+    torch = _torch()
+    monkeypatch.setenv('PSAD_MARCH', 'BAND=4')
+    op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling=bh)
+    fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    shape = (12, 24, 256)
+    rng = np.random.default_rng(7)
+    u = rng.uniform(-1, 1, shape).astype(np.float16)
+    d = rng.uniform(-1, 1, shape).astype(np.float16)
+    ut = torch.from_numpy(u).cuda().requires_grad_(True)
+    (out,) = fn.apply(ut)
+    out.backward(torch.from_numpy(d).cuda())
+    torch.cuda.synchronize()
+    assert op.forward_ast_gpu.compile().last_variant[1].BAND == 4
+    ref = OE.evaluate(op.forward_assignments, {'u': u.astype(np.float64)}, boundary_handling=bh)['out']
+    assert_close_rel(out.detach().double().cpu().numpy(), ref, TOL16, 'forward')
+    refb = OE.evaluate(op.backward_assignments, {'diffout': d.astype(np.float64)}, boundary_handling=bh)
+    (gname,) = refb.keys()
+    assert_close_rel(ut.grad.double().cpu().numpy(), refb[gname], TOL16, 'adjoint')
