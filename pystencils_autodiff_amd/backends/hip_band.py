@@ -27,15 +27,16 @@ import numpy as np
 from .hip_emitter import PRELUDE, MarchConfig, _field_params, _scalar_params, _ws_plane_base, zsum_plan
 from .printer import KernelExprPrinter
 
-__all__ = ['band_plans', 'band_geometry', 'band_choice', 'emit_band']
+__all__ = ['band_plans', 'band_geometry', 'band_choice', 'band_esize', 'emit_band']
 
 
 def band_plans(ir):
     """Per-store tap weights ``{(dz, dy, dx): coefficient}`` if the kernel fits the band schedule, else None."""
     if ir.ndim != 3 or ir.has_index_dims or ir.periodic:
         return None
-    if any(np.dtype(f.dtype.numpy_dtype).itemsize != 2 for f in ir.fields):
-        return None
+    if len({np.dtype(f.dtype.numpy_dtype).itemsize for f in ir.fields}) != 1 or \
+            np.dtype(ir.fields[0].dtype.numpy_dtype).itemsize not in (2, 4):
+        return None                     # fp16 (fp32 arithmetic) or fp32 storage
     stencil = ir.stencil_fields
     if len(stencil) != 1 or any(r > 1 for r in ir.radius):
         return None
@@ -58,35 +59,44 @@ def band_plans(ir):
     return out
 
 
-def band_geometry(X, TY, R, D):
-    """Launch / LDS geometry of a band of ``TY`` rows (``R`` per lane) on rows of ``X`` halves."""
-    CPR = X // 8
+def band_esize(ir):
+    return np.dtype(ir.fields[0].dtype.numpy_dtype).itemsize
+
+
+def band_geometry(X, TY, R, D, es=2):
+    """Launch / LDS geometry of a band of ``TY`` rows (``R`` per lane) on rows of ``X`` elements of ``es`` bytes."""
+    VE = 16 // es
+    CPR = X // VE
     G = TY // R
     ntask = G * CPR
     NCT = -(-ntask // 64) * 64
     NPIECE = (TY + 2) * CPR
     NI = -(-NPIECE // 64)
-    SLOT = NI * 512
+    SLOT = NI * 64 * VE
     NS = D + 1
-    return dict(CPR=CPR, G=G, ntask=ntask, NCT=NCT, NT=NCT + 64, NPIECE=NPIECE, NI=NI, SLOT=SLOT, NS=NS,
-                lds_bytes=(NS * SLOT + 64) * 2)
+    return dict(VE=VE, CPR=CPR, G=G, ntask=ntask, NCT=NCT, NT=NCT + 64, NPIECE=NPIECE, NI=NI, SLOT=SLOT, NS=NS,
+                lds_bytes=(NS * SLOT + 64) * es)
 
 
-def _fits(X, TY, R, D):
-    g = band_geometry(X, TY, R, D)
+def _fits(X, TY, R, D, es=2):
+    g = band_geometry(X, TY, R, D, es)
     return g['ntask'] % 64 == 0 and g['NCT'] <= 960 and D * g['NI'] <= 63 and g['lds_bytes'] <= 80 * 1024
 
 
-def band_choice(X, nstore=1):
-    """(TY, R, D) for rows of X halves, or None. Measured (scripts/probes/band_ab.py, profiles/r03_band_ab*.log):
-    8-row bands of 4 rows per lane with 2 planes in flight at X = 768 and 1024 (27-point 1024³: 0.895 ms vs
-    0.921 for 4-row bands of 2 rows per lane, 3 planes in flight); three workgroups per CU."""
-    if X % 8 or X < 128:
+def band_choice(X, nstore=1, es=2):
+    """(TY, R, D) for rows of X elements, or None. fp16, measured (scripts/probes/band_ab.py,
+    profiles/r03_band_ab*.log): 8-row bands of 4 rows per lane with 2 planes in flight at X = 768 and 1024
+    (27-point 1024³: 0.895 ms vs 0.921 for 4-row bands of 2 rows per lane, 3 planes in flight); three workgroups
+    per CU. fp32 rows hold half the cells per 16-byte chunk: 4-row bands of 4 rows per lane first (the loader's
+    vmcnt budget and 80 KB of LDS)."""
+    VE = 16 // es
+    if X % VE or X < 16 * VE:
         return None
     rmax = 4 if nstore == 1 else 2
-    cands = [(8, 4, 2), (4, 2, 3), (8, 2, 3), (12, 4, 2), (16, 4, 2), (16, 2, 2), (32, 4, 2), (32, 2, 2)]
+    cands = [(8, 4, 2), (4, 2, 3), (8, 2, 3)] if es == 2 else [(4, 4, 2), (8, 4, 2), (4, 2, 2), (8, 2, 2)]
+    cands += [(12, 4, 2), (16, 4, 2), (16, 2, 2), (32, 4, 2), (32, 2, 2)]
     for TY, R, D in cands:
-        if R <= rmax and _fits(X, TY, R, D):
+        if R <= rmax and _fits(X, TY, R, D, es):
             return TY, R, D
     return None
 
@@ -98,34 +108,49 @@ def emit_band(ir, name, cfg):
     if plans is None:
         raise ValueError('kernel is not eligible for the band schedule')
     fixed = [f for f in ir.fields if f.has_fixed_shape]
+    es = band_esize(ir)
     X = cfg.BX
     TY, R, D = cfg.BTY, cfg.BAND, cfg.D
-    g = band_geometry(X, TY, R, D)
-    CPR, G, NCT, NT, NPIECE, NI, SLOT, NS = (g[k] for k in ('CPR', 'G', 'NCT', 'NT', 'NPIECE', 'NI', 'SLOT', 'NS'))
+    g = band_geometry(X, TY, R, D, es)
+    VE, CPR, G, NCT, NT, NPIECE, NI, SLOT, NS = (g[k] for k in ('VE', 'CPR', 'G', 'NCT', 'NT', 'NPIECE', 'NI', 'SLOT',
+                                                                 'NS'))
     assert D * NI <= 63 and NCT <= 960, (X, TY, R, D)
     assert not fixed or int(fixed[0].spatial_shape[-1]) == X, 'band kernel compiled for another row length'
     S = ir.stencil_fields[0]
+    half = es == 2
+    et = '_Float16' if half else 'float'            # storage element type
     pr = KernelExprPrinter('float', dict(ir.symbol_names))
     W = []
     for pl in plans:
         W.append({k: f'(float)({pr.doprint_expr(v)})' for k, v in pl['w'].items() if v != 0})
     NP = len(plans)
+    # accumulator slots per (set, row): fp16 = 4 fp32 pairs over the cells (x+a, x+a+4), fp32 = 4 floats
+    at, azero = ('f32x2', '(f32x2)(0.f)') if half else ('float', '0.f')
 
-    def A(si, s, o, p):
-        return f'S{si}_{s}_{o}_{p}'
+    def A(si, s, o, a):
+        return f'S{si}_{s}_{o}_{a}'
+
+    def operand(a, dx):
+        return f'P{a + dx + 1}' if half else f'H{a + dx + 1}'
+
+    def cell(si, s, o, q):
+        """Cell q (0..VE-1) of a row's chunk as a storage-type value."""
+        if half:
+            return f'(_Float16){A(si, s, o, q % 4)}.{"x" if q < 4 else "y"}'
+        return A(si, s, o, q)
 
     params = _field_params(ir)
-    params += [f'const _Float16* __restrict__ hlo_{S.name}', f'const _Float16* __restrict__ hhi_{S.name}']
+    params += [f'const {et}* __restrict__ hlo_{S.name}', f'const {et}* __restrict__ hhi_{S.name}']
     params += ['const int Z', 'const int Y', 'const int X', 'const int zlo', 'const int zhi', 'const int ylo',
                'const int yhi', 'const int xlo', 'const int xhi', 'const int zc', 'const int zstep', 'const int ntx',
                'const int nty']
     params += _scalar_params(ir)
     L = [PRELUDE, 'typedef unsigned u32x4 __attribute__((ext_vector_type(4)));']
-    L.append(f'// band schedule: {TY}-row bands of full {X}-element rows, {R} rows x 8 cells per lane, {NCT // 64} '
-             f'compute waves + LDS-DMA loader wave, {NS}-slot fp16 plane ring ({D} planes in flight), z partial sums '
+    L.append(f'// band schedule: {TY}-row bands of full {X}-element rows, {R} rows x {VE} cells per lane, {NCT // 64} '
+             f'compute waves + LDS-DMA loader wave, {NS}-slot {et} plane ring ({D} planes in flight), z partial sums '
              f'in 3 rotating register sets, LDS {g["lds_bytes"]} B')
     L.append(f'extern "C" __global__ void __launch_bounds__({NT}) {name}({", ".join(params)})\n{{')
-    L.append(f'  __shared__ __attribute__((aligned(1024))) _Float16 lds[{NS * SLOT + 64}];')
+    L.append(f'  __shared__ __attribute__((aligned(1024))) {et} lds[{NS * SLOT + 64}];')
     L.append('  const int tid = threadIdx.x, lane = tid & 63;')
     L.append('  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);')
     if cfg.MAP == 1:
@@ -148,17 +173,17 @@ def emit_band(ir, name, cfg):
     L.append('    #pragma unroll')
     L.append(f'    for (int i = 0; i < {NI}; ++i) {{')
     L.append('      const int k = i * 64 + lane;')
-    L.append(f'      vo[i] = k < {NPIECE} ? ((y0 - 1) * {X} * 2 + 16 * k) : 0x7ffffff0;   // row -1 / past Y: range check')
+    L.append(f'      vo[i] = k < {NPIECE} ? ((y0 - 1) * {X * es} + 16 * k) : 0x7ffffff0;   // row -1 / past Y: range check')
     L.append('    }')
     L.append('    auto issue = [&](const int q, const int slot) {')
-    L.append(f'      const _Float16* pb = {_ws_plane_base(S, 1, "q")};')
+    L.append(f'      const {et}* pb = {_ws_plane_base(S, 1, "q")};')
     L.append(f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? pb : f_{S.name}), '
-             '(short)0, pb ? (int)(YX * 2) : 0, 0x00020000);')
-    L.append(f'      _Float16* dst = lds + slot * {SLOT};')
+             f'(short)0, pb ? (int)(YX * {es}) : 0, 0x00020000);')
+    L.append(f'      {et}* dst = lds + slot * {SLOT};')
     L.append('      #pragma unroll')
     L.append(f'      for (int i = 0; i < {NI}; ++i)')
-    L.append('        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + i * 512), '
-             '16, vo[i], 0, 0, 0);')
+    L.append(f'        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + i * '
+             f'{64 * VE}), 16, vo[i], 0, 0, 0);')
     L.append('    };')
     L.append(f'    for (int i = 0; i < {D}; ++i)')
     L.append('      if (i < nplanes) issue(zb - 1 + i, i);')
@@ -178,137 +203,140 @@ def emit_band(ir, name, cfg):
     L.append(f'  const bool active = tid < {g["ntask"]};')
     L.append(f'  const int t = active ? tid : {g["ntask"] - 1};')
     L.append(f'  const int grp = t / {CPR}, col = t - grp * {CPR};')
-    L.append(f'  const int lofs = grp * {R * X} + col * 8;          // slot row grp*R = input row y0 + grp*R - 1')
-    L.append('  const int x = col * 8;')
+    L.append(f'  const int lofs = grp * {R * X} + col * {VE};          // slot row grp*R = input row y0 + grp*R - 1')
+    L.append(f'  const int x = col * {VE};')
     L.append(f'  const bool lmask = col == 0, rmask = col == {CPR - 1};')
     if cfg.BMASK:
-        L.append('  const bool xfull = x >= xlo && x + 8 <= xhi;')
+        L.append(f'  const bool xfull = x >= xlo && x + {VE} <= xhi;')
     L.append(f'  const int yrow0 = y0 + grp * {R};')
-    L.append(f'  const unsigned sofs = (unsigned)(yrow0 * {X} + x) * 2u;')
+    L.append(f'  const unsigned sofs = (unsigned)(yrow0 * {X} + x) * {es}u;')
     if cfg.BMASK:
         L.append('  unsigned rowok = 0u;                           // rows of the lane inside [ylo, yhi), one bit each')
         L.append(f'  for (int o = 0; o < {R}; ++o) rowok |= (active && yrow0 + o >= ylo && yrow0 + o < yhi) ? (1u << o) : 0u;')
-    L.append('  // edge dword (halves, from the lane\'s chunk): lane 0 the dword left of it, lane 63 the one right of it,')
-    L.append('  // the other lanes consecutive dwords of the wave\'s block (conflict-free, unused)')
-    L.append('  const int eoff = 2 * (lane == 0 ? -1 : (lane == 63 ? 256 : lane)) - 8 * lane;')
+    L.append("  // edge dword (elements, from the lane's chunk): lane 0 the dword left of it, lane 63 the one right of it,")
+    L.append("  // the other lanes consecutive dwords of the wave's block (conflict-free, unused)")
+    dw = 4 // es                                          # elements per dword
+    L.append(f'  const int eoff = {dw} * (lane == 0 ? -1 : (lane == 63 ? {16 * VE // dw} : lane)) - {VE} * lane;')
     for si in range(NP):
-        for s in range(3):
+        for s_ in range(3):
             for o in range(R):
-                L.append('  f32x2 ' + ', '.join(f'{A(si, s, o, p)} = (f32x2)(0.f)' for p in range(4)) + ';')
+                L.append(f'  {at} ' + ', '.join(f'{A(si, s_, o, a)} = {azero}' for a in range(4)) + ';')
     store_field = [pl['field'] for pl in plans]
+
+    def row_prologue(ind, r):
+        B = [f'{ind}    const {et}* rp = sl + {r * X};']
+        if half:
+            B += [f'{ind}    const f16x8 v = *(const f16x8*)rp;',
+                  f'{ind}    const u32x4 d = __builtin_bit_cast(u32x4, v);']
+        else:
+            B += [f'{ind}    const f32x4 v = *(const f32x4*)rp;',
+                  f'{ind}    const u32x4 d = __builtin_bit_cast(u32x4, v);']
+        B += [f'{ind}    const unsigned e = *(const unsigned*)(rp + eoff);',
+              f'{ind}    const unsigned lw = __builtin_amdgcn_update_dpp(e, d.w, 0x138, 0xf, 0xf, false);   // wave_shr:1',
+              f'{ind}    const unsigned rw = __builtin_amdgcn_update_dpp(e, d.x, 0x130, 0xf, 0xf, false);   // wave_shl:1']
+        if half:
+            B += [f'{ind}    const _Float16 l = lmask ? (_Float16)0 : __builtin_bit_cast(f16x2, lw)[1];',
+                  f'{ind}    const _Float16 rr = rmask ? (_Float16)0 : __builtin_bit_cast(f16x2, rw)[0];',
+                  f'{ind}    const f32x2 P0 = {{(float)l, (float)v[3]}}, P1 = {{(float)v[0], (float)v[4]}}, '
+                  'P2 = {(float)v[1], (float)v[5]};',
+                  f'{ind}    const f32x2 P3 = {{(float)v[2], (float)v[6]}}, P4 = {{(float)v[3], (float)v[7]}}, '
+                  'P5 = {(float)v[4], (float)rr};']
+        else:
+            B += [f'{ind}    const float H0 = lmask ? 0.f : __builtin_bit_cast(float, lw), '
+                  'H5 = rmask ? 0.f : __builtin_bit_cast(float, rw);',
+                  f'{ind}    const float H1 = v.x, H2 = v.y, H3 = v.z, H4 = v.w;']
+        return B
+
+    def taps(ind, r, sets, first):
+        """FMA statements of input row r into the given (set, dz) accumulators, dx outer."""
+        B = []
+        for dx in (-1, 0, 1):
+            for st, dz in sets:
+                for si in range(NP):
+                    for o in range(R):
+                        dy = r - o - 1
+                        wv = W[si].get((dz, dy, dx)) if -1 <= dy <= 1 else None
+                        if wv is None:
+                            continue
+                        for a in range(4):
+                            acc = A(si, st, o, a)
+                            term = f'{wv} * {operand(a, dx)}'
+                            if dz == -1 and (si, o, a) not in first:
+                                first.add((si, o, a))
+                                B.append(f'{ind}{acc} = {term};')
+                            else:
+                                B.append(f'{ind}{acc} = {acc} + {term};')
+        return B
+
+    def stores(ind, si, sp, fld):
+        B = [f'{ind}{{',
+             f'{ind}  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc('
+             f'(void*)(f_{fld.name} + (i64)(zb - 2 + jj) * YX), (short)0, (int)(YX * {es}), 0x00020000);']
+        vt = 'f16x8' if half else 'f32x4'
+        for o in range(R):
+            vals = ', '.join(cell(si, sp, o, q) for q in range(VE))
+            st = f'__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ov), ors, sofs + {o * X * es}u, 0, 2);'
+            if not cfg.BMASK:
+                # every row of every band inside [ylo, yhi), x range = whole rows (checked at plan time)
+                B.append(f'{ind}  {{ const {vt} ov = {{{vals}}}; {st} }}')
+                continue
+            B.append(f'{ind}  if (rowok & {1 << o}u) {{')
+            B.append(f'{ind}    const {vt} ov = {{{vals}}};')
+            B.append(f'{ind}    if (xfull) {{')
+            B.append(f'{ind}      {st}')
+            B.append(f'{ind}    }} else {{')
+            if cfg.XB:
+                # x border cells: zeros (the row is stored whole); each cell selected on its own
+                sel = ', '.join(f'(x + {q} >= xlo && x + {q} < xhi) ? {cell(si, sp, o, q)} : ({et})0' for q in range(VE))
+                B.append(f'{ind}      const {vt} zv = {{{sel}}};')
+                B.append(f'{ind}      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, zv), ors, '
+                         f'sofs + {o * X * es}u, 0, 2);')
+            else:
+                # x border: interior cells only, one store per cell, each converted on its own (a lane extracted
+                # from the packed f16x8 was stored as element 0 for every cell by hipcc 7.2)
+                for q in range(VE):
+                    if half:
+                        stq = (f'__builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, '
+                               f'{cell(si, sp, o, q)}), ors, sofs + {o * X * es + es * q}u, 0, 0);')
+                    else:
+                        stq = (f'__builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, '
+                               f'{cell(si, sp, o, q)}), ors, sofs + {o * X * es + es * q}u, 0, 0);')
+                    B.append(f'{ind}      if (x + {q} >= xlo && x + {q} < xhi) {stq}')
+            B.append(f'{ind}    }}')
+            B.append(f'{ind}  }}')
+        B.append(f'{ind}}}')
+        return B
 
     def step(k, ind):
         sp, s0, sn = (k + 2) % 3, k, (k + 1) % 3
         B = [f'{ind}if (jj < nplanes) {{', f'{ind}  __syncthreads();',
-             f'{ind}  const _Float16* sl = lds + (jj % {NS}) * {SLOT} + lofs;',
-             ]
+             f'{ind}  const {et}* sl = lds + (jj % {NS}) * {SLOT} + lofs;']
         if cfg.BTRIM:
             B.append(f'{ind}  const bool nd_p = jj >= 2, nd_0 = jj >= 1 && jj + 1 < nplanes, nd_n = jj + 2 < nplanes;')
         first = set()
         for r in range(R + 2):
             B.append(f'{ind}  {{')
-            B.append(f'{ind}    const _Float16* rp = sl + {r * X};')
-            B.append(f'{ind}    const f16x8 v = *(const f16x8*)rp;')
-            B.append(f'{ind}    const u32x4 d = __builtin_bit_cast(u32x4, v);')
-            B.append(f'{ind}    const unsigned e = *(const unsigned*)(rp + eoff);')
-            B.append(f'{ind}    const unsigned lw = __builtin_amdgcn_update_dpp(e, d.w, 0x138, 0xf, 0xf, false);   '
-                     '// wave_shr:1')
-            B.append(f'{ind}    const unsigned rw = __builtin_amdgcn_update_dpp(e, d.x, 0x130, 0xf, 0xf, false);   '
-                     '// wave_shl:1')
-            B.append(f'{ind}    const _Float16 l = lmask ? (_Float16)0 : __builtin_bit_cast(f16x2, lw)[1];')
-            B.append(f'{ind}    const _Float16 rr = rmask ? (_Float16)0 : __builtin_bit_cast(f16x2, rw)[0];')
-            B.append(f'{ind}    const f32x2 P0 = {{(float)l, (float)v[3]}}, P1 = {{(float)v[0], (float)v[4]}}, '
-                     'P2 = {(float)v[1], (float)v[5]};')
-            B.append(f'{ind}    const f32x2 P3 = {{(float)v[2], (float)v[6]}}, P4 = {{(float)v[3], (float)v[7]}}, '
-                     'P5 = {(float)v[4], (float)rr};')
+            B += row_prologue(ind, r)
             if not cfg.BTRIM:
-                # every set every plane: one block, dx outer then the three sets, rows and pairs (12-36 independent
+                # every set every plane, one block: dx outer, then the three sets, rows and slots (12-36 independent
                 # FMAs between two dependent ones)
-                for dx in (-1, 0, 1):
-                    for st, dz in ((sp, 1), (s0, 0), (sn, -1)):
-                        for si in range(NP):
-                            for o in range(R):
-                                dy = r - o - 1
-                                wv = W[si].get((dz, dy, dx)) if -1 <= dy <= 1 else None
-                                if wv is None:
-                                    continue
-                                for p in range(4):
-                                    acc = A(si, st, o, p)
-                                    term = f'{wv} * P{p + dx + 1}'
-                                    if dz == -1 and (si, o, p) not in first:
-                                        first.add((si, o, p))
-                                        B.append(f'{ind}    {acc} = {term};')
-                                    else:
-                                        B.append(f'{ind}    {acc} = {acc} + {term};')
-                B.append(f'{ind}  }}')
-                continue
-            for st, dz, flag in ((sp, 1, 'nd_p'), (s0, 0, 'nd_0'), (sn, -1, 'nd_n')):
-                body = []
-                # tap by tap (dx outer): the chains of the rows' and pairs' accumulators interleave (8-12 independent
-                # FMAs between two dependent ones)
-                for dx in (-1, 0, 1):
-                    for si in range(NP):
-                        for o in range(R):
-                            dy = r - o - 1
-                            wv = W[si].get((dz, dy, dx)) if -1 <= dy <= 1 else None
-                            if wv is None:
-                                continue
-                            for p in range(4):
-                                acc = A(si, st, o, p)
-                                term = f'{wv} * P{p + dx + 1}'
-                                if dz == -1 and (si, o, p) not in first:
-                                    first.add((si, o, p))
-                                    body.append(f'{ind}      {acc} = {term};')
-                                else:
-                                    body.append(f'{ind}      {acc} = {acc} + {term};')
-                if body:
-                    B.append(f'{ind}    if ({flag}) {{')
-                    B += body
-                    B.append(f'{ind}    }}')
+                B += taps(f'{ind}    ', r, ((sp, 1), (s0, 0), (sn, -1)), first)
+            else:
+                # the first two / last two planes of a chunk skip the taps of outputs outside it (uniform branches)
+                for st, dz, flag in ((sp, 1, 'nd_p'), (s0, 0, 'nd_0'), (sn, -1, 'nd_n')):
+                    body = taps(f'{ind}      ', r, ((st, dz),), first)
+                    if body:
+                        B += [f'{ind}    if ({flag}) {{'] + body + [f'{ind}    }}']
             B.append(f'{ind}  }}')
-        # outputs of q+1 that received no tap this plane (no dz = -1 taps in some row) start from zero
+        # outputs of q+1 that received no tap this plane (no dz = -1 taps) start from zero
         for si in range(NP):
             for o in range(R):
-                for p in range(4):
-                    if (si, o, p) not in first:
-                        B.append(f'{ind}  {A(si, sn, o, p)} = (f32x2)(0.f);')
+                for a in range(4):
+                    if (si, o, a) not in first:
+                        B.append(f'{ind}  {A(si, sn, o, a)} = {azero};')
         B.append(f'{ind}  if (jj >= 2) {{')
         for si, fld in enumerate(store_field):
-            B.append(f'{ind}    {{')
-            B.append(f'{ind}      const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc('
-                     f'(void*)(f_{fld.name} + (i64)(zb - 2 + jj) * YX), (short)0, (int)(YX * 2), 0x00020000);')
-            for o in range(R):
-                vals = ', '.join(f'(_Float16){A(si, sp, o, p)}.{c}' for c in 'xy' for p in range(4))
-                st = (f'__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ov), ors, '
-                      f'sofs + {o * X * 2}u, 0, 2);')
-                if not cfg.BMASK:
-                    # every row of every band inside [ylo, yhi), x range = whole rows (checked at plan time)
-                    B.append(f'{ind}      {{ const f16x8 ov = {{{vals}}}; {st} }}')
-                    continue
-                B.append(f'{ind}      if (rowok & {1 << o}u) {{')
-                B.append(f'{ind}        const f16x8 ov = {{{vals}}};')
-                B.append(f'{ind}        if (xfull) {{')
-                B.append(f'{ind}          {st}')
-                if cfg.XB:
-                    # x border cells: zeros (the row is stored whole); each cell selected on its own
-                    sel = ', '.join(f'(x + {q8} >= xlo && x + {q8} < xhi) ? (_Float16){A(si, sp, o, q8 % 4)}.'
-                                    f'{"x" if q8 < 4 else "y"} : (_Float16)0' for q8 in range(8))
-                    B.append(f'{ind}        }} else {{')
-                    B.append(f'{ind}          const f16x8 zv = {{{sel}}};')
-                    B.append(f'{ind}          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, zv), ors, '
-                             f'sofs + {o * X * 2}u, 0, 2);')
-                else:
-                    # x border: interior cells only, one 2-byte store per cell, each converted on its own (a lane
-                    # extracted from the packed f16x8 was stored as element 0 for every cell by hipcc 7.2)
-                    B.append(f'{ind}        }} else {{')
-                    for q8 in range(8):
-                        cell = f'(_Float16){A(si, sp, o, q8 % 4)}.{"x" if q8 < 4 else "y"}'
-                        B.append(f'{ind}          if (x + {q8} >= xlo && x + {q8} < xhi) '
-                                 f'__builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, {cell}), '
-                                 f'ors, sofs + {o * X * 2 + 2 * q8}u, 0, 0);')
-                B.append(f'{ind}        }}')
-                B.append(f'{ind}      }}')
-            B.append(f'{ind}    }}')
+            B += stores(f'{ind}    ', si, sp, fld)
         B.append(f'{ind}  }}')
         B.append(f'{ind}  ++jj;')
         B.append(f'{ind}}}')
@@ -321,4 +349,3 @@ def emit_band(ir, name, cfg):
     L.append('  }')
     L.append('}')
     return '\n'.join(L) + '\n'
-

@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 from . import hip_runtime as rt
-from .hip_band import band_choice, band_geometry, band_plans, emit_band
+from .hip_band import band_choice, band_esize, band_geometry, band_plans, emit_band
 from .hip_emitter import (MarchConfig, emit_generic, emit_march, emit_pointwise, emit_zsum, march_geometry, ws_geometry,
                           zsum_plan)
 
@@ -27,6 +27,7 @@ __all__ = ['HipStencilKernel', 'default_march_config']
 # BAND_MIN_WG (z-slabs of a few planes: 96×768² 27-point 0.052 ms either way) keep the zsum ring.
 BAND_ZC_BOX, BAND_ZC_STAR = 24, 8
 BAND_MIN_WG = 1536
+BAND_F32 = False            # fp32 storage on the band schedule by default (see DESIGN §4 "Row bands")
 
 
 def _band_config(ir, ve, shape, over):
@@ -42,7 +43,10 @@ def _band_config(ir, ve, shape, over):
         return None
     plans = band_plans(ir)
     X = int(shape[-1])
-    choice = band_choice(X, len(plans)) if plans else None
+    es = band_esize(ir) if plans else 0
+    if plans and es == 4 and not BAND_F32 and 'BAND' not in over:
+        return None                    # fp32 storage: only when asked (BAND=R) until it measures faster
+    choice = band_choice(X, len(plans), es) if plans else None
     if choice is None:
         return None
     TY, R, D = choice
@@ -50,7 +54,7 @@ def _band_config(ir, ve, shape, over):
         R = int(over['BAND'])
     TY = int(over.get('BTY', TY if TY % R == 0 else R * max(1, TY // R)))
     D = int(over.get('D', D))
-    g = band_geometry(X, TY, R, D)
+    g = band_geometry(X, TY, R, D, es)
     if TY % R or g['NCT'] > 960 or D * g['NI'] > 63 or g['lds_bytes'] > 160 * 1024:
         raise ValueError(f'band schedule: BTY={TY} BAND={R} D={D} do not fit rows of {X} elements')
     ntaps = max(len(pl['w']) for pl in plans)
@@ -689,7 +693,8 @@ class HipStencilKernel:
                                           'nty')]
         kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics) + \
             [self._scalar_kind()] * len(ir.scalars)
-        block = ws['block'] if ws else (band_geometry(cfg.BX, cfg.BTY, cfg.BAND, cfg.D)['NT'] if cfg.BAND else cfg.NT)
+        block = ws['block'] if ws else (band_geometry(cfg.BX, cfg.BTY, cfg.BAND, cfg.D, esize)['NT'] if cfg.BAND else
+                                        cfg.NT)
         return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics, xb=cfg.XB, block=block)
 
 

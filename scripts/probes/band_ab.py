@@ -21,6 +21,18 @@ CASES = {
     's7_1024': (lambda: W.diffusion_7pt(dtype='float16'), (1024, 1024, 1024)),
     'slab27': (W.stencil_27pt, (96, 768, 768)),
     'slab7': (lambda: W.diffusion_7pt(dtype='float16'), (128, 1024, 1024)),
+    'f7_1024': (W.diffusion_7pt, (1024, 1024, 1024)),
+    'f7_768': (W.diffusion_7pt, (768, 768, 768)),
+    'f7_512': (W.diffusion_7pt, (512, 512, 512)),
+}
+VARIANTS_F32 = {
+    'zsum (BAND=0)': {'BAND': 0},
+    'band R4 TY4 D2 zc8': {'BAND': 4, 'BTY': 4, 'D': 2, 'ZMIN': 8, 'ZMAX': 8},
+    'band R4 TY4 D2 zc24': {'BAND': 4, 'BTY': 4, 'D': 2, 'ZMIN': 24, 'ZMAX': 24},
+    'band R4 TY4 D2 zc64': {'BAND': 4, 'BTY': 4, 'D': 2, 'ZMIN': 64, 'ZMAX': 64},
+    'band R2 TY4 D2 zc16': {'BAND': 2, 'BTY': 4, 'D': 2, 'ZMIN': 16, 'ZMAX': 16},
+    'band R4 TY4 D1 zc16': {'BAND': 4, 'BTY': 4, 'D': 1, 'ZMIN': 16, 'ZMAX': 16},
+    'band R4 TY4 D2 nt16': {'BAND': 4, 'BTY': 4, 'D': 2, 'ZMIN': 16, 'ZMAX': 16, 'BTRIM': 0},
 }
 VARIANTS = {
     'zsum (BAND=0)': {'BAND': 0},
@@ -65,16 +77,17 @@ def main():
         for which, ac in (('fwd', op.forward_assignments), ('bwd', op.backward_assignments)):
             runs = []
             ref = None
-            for vname, tun in VARIANTS.items():
+            for vname, tun in (VARIANTS_F32 if case.startswith('f7') else VARIANTS).items():
                 try:
                     k = StencilKernel(ac, boundary_handling='zeros', function_name=f'ab_{which}',
                                       target='gpu', gpu_indexing_params=tun).compile()
                 except ValueError as e:
                     print(f'{case} {which} {vname}: {e}', flush=True)
                     continue
-                ins = {f.name: (torch.rand(shape, device='cuda', generator=g) * 2 - 1).half()
+                dt = torch.float32 if case.startswith('f7') else torch.float16
+                ins = {f.name: (torch.rand(shape, device='cuda', generator=g) * 2 - 1).to(dt)
                        for f in k.ir.fields_read} if ref is None else ins
-                outs = {f.name: torch.full(shape, float('nan'), dtype=torch.float16, device='cuda')
+                outs = {f.name: torch.full(shape, float('nan'), dtype=dt, device='cuda')
                         for f in k.ir.fields_written}
                 try:
                     k(**ins, **outs)
@@ -90,7 +103,7 @@ def main():
                     err = 0.0
                 else:
                     err = float((o.float() - ref).abs().max()) / max(1e-30, float(ref.abs().max()))
-                    if not err <= 1e-3:
+                    if not err <= (1e-6 if dt == torch.float32 else 1e-3):
                         print(f'{case} {which} {vname}: MISMATCH rel err {err:.3e}', flush=True)
                         continue
                 runs.append((f'{case} {which} {vname:16s} {tag:32s} err {err:.1e}', (lambda k=k, a={**ins, **outs}: k(**a))))
@@ -100,7 +113,7 @@ def main():
                 for lab, fn in runs:
                     settle(fn, 0.1)
                     res[lab].append(timed(fn))
-            nbytes = 2 * 2 * shape[0] * shape[1] * shape[2]
+            nbytes = 2 * (4 if case.startswith('f7') else 2) * shape[0] * shape[1] * shape[2]
             for lab, _ in runs:
                 v = sorted(res[lab])
                 med = (v[1] + v[2]) / 2
