@@ -33,9 +33,14 @@ def test_band_eligibility():
         assert plans is not None and len(plans) == 1 and len(plans[0]['w']) == 27
     star = pa.AutoDiffOp(W.diffusion_7pt(dtype='float16'), boundary_handling='zeros')
     assert len(band_plans(HipStencilKernel(_kernel(star.forward_assignments)).ir)[0]['w']) == 7
-    # fp32 storage, a second field read pointwise, radius 2: not the band schedule
+    # fp32 storage fits (opt-in, BAND=R); fp64, a second field read pointwise, radius 2: not the band schedule
     f32 = pa.AutoDiffOp(W.stencil_27pt(dtype='float32'), boundary_handling='zeros')
-    assert band_plans(HipStencilKernel(_kernel(f32.forward_assignments)).ir) is None
+    ir32 = HipStencilKernel(_kernel(f32.forward_assignments)).ir
+    assert band_plans(ir32) is not None
+    assert default_march_config(ir32, 4, (768, 768, 768)).BAND == 0
+    assert default_march_config(ir32, 4, (768, 768, 768), {'BAND': 4}).BAND == 4
+    f64 = pa.AutoDiffOp(W.stencil_27pt(dtype='float64'), boundary_handling='zeros')
+    assert band_plans(HipStencilKernel(_kernel(f64.forward_assignments)).ir) is None
     u, v, out = ps.fields('u, v, out: float16[3d]')
     two = ps.AssignmentCollection({out.center: u[1, 0, 0] + u[-1, 0, 0] * v.center})
     assert band_plans(HipStencilKernel(_kernel(two)).ir) is None
@@ -87,7 +92,8 @@ def _torch():
 
 
 CASES = [('27pt', W.stencil_27pt), ('7pt_f16', lambda: W.diffusion_7pt(dtype='float16')),
-         ('asym_f16', lambda: W.asym_7pt(dtype='float16'))]
+         ('asym_f16', lambda: W.asym_7pt(dtype='float16')), ('asym_f32', W.asym_7pt),
+         ('27pt_f32', lambda: W.stencil_27pt(dtype='float32'))]
 
 
 @pytest.mark.gpu
@@ -101,10 +107,15 @@ def test_band_vs_oracle(case, shape, bh):
     op = pa.AutoDiffOp(case[1](), boundary_handling=bh)
     rng = np.random.default_rng(sum(shape))
     for which, ac in (('f', op.forward_assignments), ('b', op.backward_assignments)):
-        k = _kernel(ac, bh, f'band_{which}', BAND=band_choice(shape[-1])[1]).compile()
-        ins = {f.name: rng.uniform(-1, 1, shape).astype(np.float16) for f in k.ir.fields_read}
+        k0 = _kernel(ac, bh, f'band_{which}')
+        dt = np.dtype(k0.ir.fields[0].dtype.numpy_dtype)
+        choice = band_choice(shape[-1], 1, dt.itemsize)
+        if choice is None:
+            pytest.skip(f'no band geometry for rows of {shape[-1]} {dt}')
+        k = _kernel(ac, bh, f'band_{which}', BAND=choice[1]).compile()
+        ins = {f.name: rng.uniform(-1, 1, shape).astype(dt) for f in k.ir.fields_read}
         ref = OE.evaluate(ac, {n: a.astype(np.float64) for n, a in ins.items()}, boundary_handling=bh)
-        outs = {f.name: torch.zeros(shape, dtype=torch.float16, device='cuda') for f in k.ir.fields_written}
+        outs = {f.name: torch.zeros(shape, dtype=getattr(torch, dt.name), device='cuda') for f in k.ir.fields_written}
         k(**{n: torch.from_numpy(a).cuda() for n, a in ins.items()}, **outs)
         torch.cuda.synchronize()
         cfg = k.last_variant[1]
@@ -112,7 +123,8 @@ def test_band_vs_oracle(case, shape, bh):
         whole = bh == 'zeros' and shape[1] % cfg.BTY == 0
         assert cfg.BMASK == (not whole), cfg
         for n, t in outs.items():
-            assert_close_rel(t.double().cpu().numpy(), ref[n], TOL16, f'{case[0]} {which} {n} {shape} {bh}')
+            assert_close_rel(t.double().cpu().numpy(), ref[n], TOL16 if dt.itemsize == 2 else 1e-6,
+                             f'{case[0]} {which} {n} {shape} {bh}')
 
 
 @pytest.mark.gpu
