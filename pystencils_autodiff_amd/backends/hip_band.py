@@ -216,7 +216,8 @@ def emit_band(ir, name, cfg):
     L.append("  // edge dword (elements, from the lane's chunk): lane 0 the dword left of it, lane 63 the one right of it,")
     L.append("  // the other lanes consecutive dwords of the wave's block (conflict-free, unused)")
     dw = 4 // es                                          # elements per dword
-    L.append(f'  const int eoff = {dw} * (lane == 0 ? -1 : (lane == 63 ? {16 * VE // dw} : lane)) - {VE} * lane;')
+    # dword targets relative to the wave's block: -1, 1 .. 62, 256 (64 chunks of 4 dwords)
+    L.append(f'  const int eoff = {dw} * (lane == 0 ? -1 : (lane == 63 ? 256 : lane)) - {VE} * lane;')
     for si in range(NP):
         for s_ in range(3):
             for o in range(R):

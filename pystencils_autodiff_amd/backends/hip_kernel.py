@@ -27,7 +27,10 @@ __all__ = ['HipStencilKernel', 'default_march_config']
 # BAND_MIN_WG (z-slabs of a few planes: 96×768² 27-point 0.052 ms either way) keep the zsum ring.
 BAND_ZC_BOX, BAND_ZC_STAR = 24, 8
 BAND_MIN_WG = 1536
-BAND_F32 = False            # fp32 storage on the band schedule by default (see DESIGN §4 "Row bands")
+# fp32 storage (4 cells per 16-byte chunk): the band schedule wins on rows up to 768 elements and loses on
+# 1024-element rows, where the 4-row bands' 74 KB of LDS leave two workgroups per CU (7-point, settled A/B:
+# 768³ 0.608 vs 0.636 ms, 512³ 0.195 vs 0.200, 1024³ 1.53 vs 1.43; profiles/r03_band_ab_f32.log)
+BAND_F32_MAX_X = 768
 
 
 def _band_config(ir, ve, shape, over):
@@ -44,8 +47,8 @@ def _band_config(ir, ve, shape, over):
     plans = band_plans(ir)
     X = int(shape[-1])
     es = band_esize(ir) if plans else 0
-    if plans and es == 4 and not BAND_F32 and 'BAND' not in over:
-        return None                    # fp32 storage: only when asked (BAND=R) until it measures faster
+    if plans and es == 4 and X > BAND_F32_MAX_X and 'BAND' not in over:
+        return None
     choice = band_choice(X, len(plans), es) if plans else None
     if choice is None:
         return None
