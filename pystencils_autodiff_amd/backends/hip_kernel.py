@@ -21,16 +21,16 @@ from .hip_emitter import (MarchConfig, emit_generic, emit_march, emit_pointwise,
 __all__ = ['HipStencilKernel', 'default_march_config']
 
 
-# row-band chunk length (planes per workgroup), settled A/B rounds through the kernels (scripts/probes/band_ab.py,
-# profiles/r03_band_ab*.log): box stencils (27 taps) 24 planes (768³ 0.375 vs 0.385 ms at 8, zsum ring 0.395),
-# star stencils 8 (768³ 7-point fp16 0.318 vs 0.324 at 16, 0.329 at 24, zsum ring 0.344). Fewer workgroups than
-# BAND_MIN_WG (z-slabs of a few planes: 96×768² 27-point 0.052 ms either way) keep the zsum ring.
-BAND_ZC_BOX, BAND_ZC_STAR = 24, 8
+# row-band defaults, settled A/B rounds through the op (fn.apply + backward, same process;
+# scripts/probes/op_band_ab.py, profiles/r03_op_band_ab*.log): box stencils (27 taps) 48-plane chunks without the
+# trimmed chunk-edge planes (fwd+bwd 1024³ 1.707 vs 1.809 ms zsum, trimmed 24-plane chunks 2.01; 768³ 0.731 vs
+# 0.762), star stencils 8-plane chunks (fp16 7-point 1024³ 1.461 vs 1.538, 768³ 0.635 vs 0.682). Launches of fewer
+# than BAND_MIN_WG workgroups (z-slabs of a few planes) keep the zsum ring.
+BAND_ZC_BOX, BAND_ZC_STAR = 48, 8
 BAND_MIN_WG = 1536
-# fp32 storage (4 cells per 16-byte chunk): the band schedule wins on rows up to 768 elements and loses on
-# 1024-element rows, where the 4-row bands' 74 KB of LDS leave two workgroups per CU (7-point, settled A/B:
-# 768³ 0.608 vs 0.636 ms, 512³ 0.195 vs 0.200, 1024³ 1.53 vs 1.43; profiles/r03_band_ab_f32.log)
-BAND_F32_MAX_X = 768
+# fp32 storage (4 cells per 16-byte chunk) measured slower through the op (7-point 512³ 0.387 vs 0.373 ms, 768³
+# 1.325 vs 1.261): opt-in only (BAND=R)
+BAND_F32_MAX_X = 0
 
 
 def _band_config(ir, ve, shape, over):
@@ -66,7 +66,7 @@ def _band_config(ir, ve, shape, over):
         return None
     return MarchConfig(VE=ve, BAND=R, BTY=TY, BX=X, D=D, ZSUM=True, NT_STORE=True, ZMIN=zc,
                        ZMAX=int(over.get('ZMAX', zc)), BLK=int(over.get('BLK', 512)), MAP=int(over.get('MAP', 0)),
-                       BTRIM=bool(int(over.get('BTRIM', 1))))
+                       BTRIM=bool(int(over.get('BTRIM', 0))))
 
 
 def default_march_config(ir, ve, shape=None, tuning=None, band=True):

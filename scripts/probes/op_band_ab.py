@@ -1,0 +1,73 @@
+"""Band schedule on / off through the drop-in op (fn.apply + backward, the native autograd node), same process,
+settled A/B rounds: op A plans its kernels with PSAD_BAND=0 (zsum ring), op B with the band default.
+
+python scripts/probes/op_band_ab.py [workload:edge[:PSAD_MARCH variant ...] ...]
+  e.g. f7:512 s27:768 s27:1024:BTRIM=0,ZMIN=48,ZMAX=48:ZMIN=48,ZMAX=48
+"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', '..'))
+import pystencils_autodiff_amd as pa  # noqa: E402
+from pystencils_autodiff_amd import workloads as W  # noqa: E402
+
+WL = {'f7': (W.diffusion_7pt, torch.float32), 'h7': (lambda: W.diffusion_7pt(dtype='float16'), torch.float16),
+      's27': (W.stencil_27pt, torch.float16), 'f27': (lambda: W.stencil_27pt(dtype='float32'), torch.float32)}
+
+
+def make(name, n, band, march=''):
+    b, dt = WL[name]
+    os.environ['PSAD_BAND'] = '1' if band else '0'
+    if march:
+        os.environ['PSAD_MARCH'] = march
+    op = pa.AutoDiffOp(b(), boundary_handling='zeros')
+    fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    g = torch.Generator(device='cuda').manual_seed(0)
+    u = torch.rand((n, n, n), device='cuda', generator=g).to(dt).requires_grad_(True)
+    d = (torch.rand((n, n, n), device='cuda', generator=g) * 2 - 1).to(dt)
+
+    def step():
+        (o,) = fn.apply(u)
+        o.backward(d)
+        u.grad = None
+    step()
+    torch.cuda.synchronize()
+    cfg = op.forward_ast_gpu.compile().last_variant[1]
+    os.environ.pop('PSAD_BAND', None)
+    os.environ.pop('PSAD_MARCH', None)
+    return step, f'BAND={cfg.BAND} BTY={cfg.BTY} {march}'
+
+
+def main():
+    torch.autograd.set_multithreading_enabled(False)
+    for spec in sys.argv[1:] or ['f7:512', 'f7:768', 's27:768', 'h7:768']:
+        name, n, *extra = spec.split(':')
+        n = int(n)
+        runs = [make(name, n, False), make(name, n, True)] + [make(name, n, True, m) for m in extra]
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 1.0:
+            runs[0][0]()
+        torch.cuda.synchronize()
+        res = [[] for _ in runs]
+        for _ in range(5):
+            for i, (fn, _) in enumerate(runs):
+                for _ in range(10):
+                    fn()
+                torch.cuda.synchronize()
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(20):
+                    fn()
+                b.record()
+                torch.cuda.synchronize()
+                res[i].append(a.elapsed_time(b) / 20)
+        for (fn, tag), r in zip(runs, res):
+            v = sorted(r)
+            print(f'{spec.split(":")[0]}:{n:<5d} {tag:44s} fwd+bwd {v[2]:.4f} ms  [{" ".join(f"{x:.4f}" for x in r)}]', flush=True)
+
+
+if __name__ == '__main__':
+    main()
