@@ -27,7 +27,7 @@ __all__ = ['HipStencilKernel', 'default_march_config']
 # 0.762), star stencils 8-plane chunks (fp16 7-point 1024³ 1.461 vs 1.538, 768³ 0.635 vs 0.682). Launches of fewer
 # than BAND_MIN_WG workgroups (z-slabs of a few planes) keep the zsum ring.
 BAND_ZC_BOX, BAND_ZC_STAR = 48, 8
-BAND_MIN_WG = 1536
+BAND_MIN_WG = 1024
 # fp32 storage (4 cells per 16-byte chunk) measured slower through the op (7-point 512³ 0.387 vs 0.373 ms, 768³
 # 1.325 vs 1.261): opt-in only (BAND=R)
 BAND_F32_MAX_X = 0
