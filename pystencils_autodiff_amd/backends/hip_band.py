@@ -52,7 +52,7 @@ def band_plans(ir):
         w = {}
         for dz, terms in pl['lin'].items():
             for coeff, f, dy, dx, k in terms:
-                if f is not stencil[0] and f.name != stencil[0].name or k != 0:
+                if (f is not stencil[0] and f.name != stencil[0].name) or k != 0:
                     return None
                 w[(dz, dy, dx)] = w.get((dz, dy, dx), 0) + coeff
         out.append(dict(field=pl['field'], w=w))

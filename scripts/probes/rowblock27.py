@@ -19,13 +19,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 WEIGHTS = [(i - 13.3) / 50.0 for i in range(27)]
 
 
-def source(X, TY, D, MODE, MAP, WPE=3):
+def source(X, TY, D, MODE, MAP, WPE=None, NCH=1):
     CPR = X // 8
     NPIECE = (TY + 2) * CPR
     NI = -(-NPIECE // 64)
     SLOT = NI * 512
     NS = D + 1
-    NCH = -(-(TY * CPR) // 256)
+    NCT = TY * CPR // NCH          # compute threads: one chunk of 8 halves per lane and pass
+    assert NCT * NCH == TY * CPR and NCT % 64 == 0 and NCT <= 960
+    NT = NCT + 64
+    wpe = f'__attribute__((amdgpu_waves_per_eu({WPE})))' if WPE else ''
     assert D * NI <= 63
     waits = '\n'.join(f'        case {a}: asm volatile("s_waitcnt vmcnt({a * NI})" ::: "memory"); break;'
                       for a in range(D))
@@ -55,7 +58,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef long long i64;
 
-extern "C" __global__ void __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu({WPE}))) rb27(const _Float16* __restrict__ u, _Float16* __restrict__ out,
+extern "C" __global__ void __launch_bounds__({NT}) {wpe} rb27(const _Float16* __restrict__ u, _Float16* __restrict__ out,
                                                       const int Y, const int Z, const int zc, const int nbands)
 {{
   __shared__ __attribute__((aligned(16))) _Float16 lds[{NS * SLOT + 64}];
@@ -69,7 +72,7 @@ extern "C" __global__ void __launch_bounds__(320) __attribute__((amdgpu_waves_pe
   if (zb >= ze) return;
   const i64 YX = (i64)Y * {X};
   const int nplanes = ze - zb + 2;
-  if (wave == 4) {{
+  if (wave == {NCT // 64}) {{
     int vo[{NI}];
     #pragma unroll
     for (int i = 0; i < {NI}; ++i) {{
@@ -104,7 +107,7 @@ extern "C" __global__ void __launch_bounds__(320) __attribute__((amdgpu_waves_pe
     for (int p = 0; p < 4; ++p) {{ A0[i][p] = (f32x2)(0.f); A1[i][p] = (f32x2)(0.f); }}
   // edge dword (in halves, relative to the lane's own chunk): lane 0 the dword left of it, lane 63 the one right of
   // it, the other lanes consecutive dwords of the wave's block (conflict-free, unused)
-  const int eoff = 2 * (lane == 0 ? -1 : (lane == 63 ? 256 : lane)) - 8 * lane;
+  const int eoff = 2 * (lane == 0 ? -1 : (lane == 63 ? 256 : lane)) - 8 * lane;   // NOLINT
   #pragma unroll 1
   for (int j = 0; j < nplanes; ++j) {{
     const int q = zb - 1 + j;
@@ -114,7 +117,7 @@ extern "C" __global__ void __launch_bounds__(320) __attribute__((amdgpu_waves_pe
                                                                          (int)(YX * 2), 0x00020000);
     #pragma unroll
     for (int i = 0; i < {NCH}; ++i) {{
-      const int c = i * 256 + tid;
+      const int c = i * {NCT} + tid;
       const int col = c % {CPR};
       f32x2 P0[6], P1[6], P2[6];
       auto row = [&](const int dy, f32x2 (&P)[6]) {{
@@ -161,8 +164,11 @@ def main():
     torch.manual_seed(0)
     u = torch.rand(N, N, N, device='cuda').half()
     out = torch.empty_like(u)
-    K = torch.tensor(WEIGHTS, dtype=torch.float32, device='cuda').reshape(1, 1, 3, 3, 3)
-    ref = F.conv3d(u.float()[None, None], K, padding=1)[0, 0]
+    up = F.pad(u.float()[None], (1, 1, 1, 1, 1, 1))[0]      # zero halo, no MIOpen (conv3d at 1024^3 stalls)
+    ref = torch.zeros(N, N, N, device='cuda')
+    for i, (dz, dy, dx) in enumerate(itertools.product((-1, 0, 1), repeat=3)):
+        ref += WEIGHTS[i] * up[1 + dz:1 + dz + N, 1 + dy:1 + dy + N, 1 + dx:1 + dx + N]
+    del up
     nbytes = 2 * u.numel() * 2
 
     def timed(fn, reps=30):
@@ -180,6 +186,11 @@ def main():
         v = sorted(x.elapsed_time(y) for x, y in ev)
         return v[len(v) // 2]
 
+    import time
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 1.0:     # settle clocks / power before the first timing
+        torch.mul(u, 2.0, out=out)
+    torch.cuda.synchronize()
     # the drop-in op's current kernel on the same field
     import pystencils_autodiff_amd as pa
     from pystencils_autodiff_amd import workloads as W
@@ -190,34 +201,38 @@ def main():
     print(f'op forward (current schedule)            {ms_op:.4f} ms {nbytes / ms_op / 1e6:6.0f} GB/s', flush=True)
     ms_mul = timed(lambda: torch.mul(u, 2.0, out=out))
     print(f'torch mul                                {ms_mul:.4f} ms {nbytes / ms_mul / 1e6:6.0f} GB/s', flush=True)
-    cfgs = []
-    tys = [t for t in (8, 4, 12, 6) if N % t == 0 and (t * N // 8) % 256 == 0 and t * N // 8 // 256 <= 3]
-    for TY in tys[:2]:
-        for D in (3, 2, 4):
-            for MAP in (0, 1):
-                for zc in (24, 12, 48):
-                    if (D == 3 or zc == 24) and (MAP == 0 or zc == 24):
-                        cfgs.append((TY, D, 0, MAP, zc))
-        cfgs.append((TY, 3, 1, 0, 24))
+    # (TY, NCH, D, MODE, MAP, zc, WPE)
+    if N == 768:
+        cfgs = [(8, 1, 3, 0, 0, 24, None), (8, 1, 3, 0, 1, 24, None), (8, 1, 3, 0, 0, 12, None),
+                (8, 1, 3, 0, 0, 48, None), (8, 1, 2, 0, 0, 24, None), (8, 1, 4, 0, 0, 24, None),
+                (4, 1, 3, 0, 0, 24, None), (4, 1, 5, 0, 0, 24, None), (8, 2, 3, 0, 0, 24, None),
+                (2, 1, 5, 0, 0, 24, None), (8, 3, 3, 0, 0, 24, 3),
+                (8, 1, 3, 1, 0, 24, None), (4, 1, 3, 1, 0, 24, None)]
+    else:
+        cfgs = [(4, 1, 3, 0, 0, 24, None), (4, 1, 3, 0, 1, 24, None), (4, 1, 2, 0, 0, 24, None),
+                (6, 1, 3, 0, 0, 24, None), (4, 2, 3, 0, 0, 24, None), (2, 1, 5, 0, 0, 24, None),
+                (4, 1, 3, 1, 0, 24, None)]
     compiled = {}
-    for TY, D, MODE, MAP, zc in cfgs:
-        if N % TY or (TY * N // 8) % 256 or D * -(-((TY + 2) * N // 8) // 64) > 63:
+    for TY, NCH, D, MODE, MAP, zc, WPE in cfgs:
+        CPR = N // 8
+        if N % TY or (TY * CPR) % (64 * NCH) or D * -(-((TY + 2) * CPR) // 64) > 63 or TY * CPR // NCH > 960:
             continue
-        key = (TY, D, MODE, MAP)
+        NT = TY * CPR // NCH + 64
+        key = (TY, NCH, D, MODE, MAP, WPE)
         if key not in compiled:
-            code = rt.compile_hip(source(N, TY, D, MODE, MAP), name=f'rb27_{N}_{TY}_{D}_{MODE}_{MAP}.hip')
+            code = rt.compile_hip(source(N, TY, D, MODE, MAP, WPE, NCH), name=f'rb27_{N}_{"_".join(map(str, key))}.hip')
             compiled[key] = rt.load_function(code, 'rb27', dev)
         f = compiled[key]
         nbands = N // TY
         grid = nbands * (-(-N // zc))
         args = struct.pack('<QQiiii', u.data_ptr(), out.data_ptr(), N, N, zc, nbands)
-        launch = (lambda f=f, grid=grid, args=args: rt.launch(f, (grid,), (320,), args, stream))
+        launch = (lambda f=f, grid=grid, args=args, NT=NT: rt.launch(f, (grid,), (NT,), args, stream))
         out.zero_()
         launch()
         torch.cuda.synchronize()
         err = float((out.float() - ref).abs().max()) if MODE == 0 else float('nan')
         ms = timed(launch)
-        print(f'TY {TY:2d} D {D} MODE {MODE} MAP {MAP} zc {zc:2d}  {ms:.4f} ms {nbytes / ms / 1e6:6.0f} GB/s '
+        print(f'TY {TY:2d} NCH {NCH} NT {NT:4d} D {D} MODE {MODE} MAP {MAP} zc {zc:2d}  {ms:.4f} ms {nbytes / ms / 1e6:6.0f} GB/s '
               f'maxerr {err:.2e}', flush=True)
 
 
