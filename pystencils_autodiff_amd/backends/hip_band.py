@@ -335,7 +335,8 @@ def emit_band(ir, name, cfg):
                 for a in range(4):
                     if (si, o, a) not in first:
                         B.append(f'{ind}  {A(si, sn, o, a)} = {azero};')
-        B.append(f'{ind}  if (jj >= 2) {{')
+        # idle lanes (band tasks not a multiple of 64) compute on a clamped task with wrong x neighbours: no stores
+        B.append(f'{ind}  if (jj >= 2{" && active" if g["ntask"] != NCT else ""}) {{')
         for si, fld in enumerate(store_field):
             B += stores(f'{ind}    ', si, sp, fld)
         B.append(f'{ind}  }}')

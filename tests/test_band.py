@@ -169,10 +169,11 @@ def test_band_chunk_length_and_trim_bitwise():
     torch = _torch()
     op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
     g = torch.Generator().manual_seed(11)
-    u = (torch.rand((37, 32, 768), generator=g) * 2 - 1).half().cuda()
+    u = (torch.rand((37, 48, 768), generator=g) * 2 - 1).half().cuda()
     res = []
     for tun in ({'BAND': 4}, {'BAND': 4, 'ZMIN': 5, 'ZMAX': 5}, {'BAND': 4, 'ZMIN': 16, 'ZMAX': 16, 'BTRIM': 1},
-                {'BAND': 4, 'BTRIM': 1, 'ZMIN': 9, 'ZMAX': 9}):
+                {'BAND': 4, 'BTRIM': 1, 'ZMIN': 9, 'ZMAX': 9},
+                {'BAND': 4, 'BTY': 12}):          # 3 row groups x 96 chunks = 288 tasks on 320 lanes (idle lanes)
         k = _kernel(op.forward_assignments, 'zeros', 'bandc', **tun).compile()
         out = torch.full_like(u, float('nan'))
         k(u=u, out=out)
