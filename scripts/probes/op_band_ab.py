@@ -26,8 +26,9 @@ def make(name, n, band, march=''):
     op = pa.AutoDiffOp(b(), boundary_handling='zeros')
     fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
     g = torch.Generator(device='cuda').manual_seed(0)
-    u = torch.rand((n, n, n), device='cuda', generator=g).to(dt).requires_grad_(True)
-    d = (torch.rand((n, n, n), device='cuda', generator=g) * 2 - 1).to(dt)
+    shape = (n[0], n[1], n[1]) if isinstance(n, tuple) else (n, n, n)
+    u = torch.rand(shape, device='cuda', generator=g).to(dt).requires_grad_(True)
+    d = (torch.rand(shape, device='cuda', generator=g) * 2 - 1).to(dt)
 
     def step():
         (o,) = fn.apply(u)
@@ -45,7 +46,7 @@ def main():
     torch.autograd.set_multithreading_enabled(False)
     for spec in sys.argv[1:] or ['f7:512', 'f7:768', 's27:768', 'h7:768']:
         name, n, *extra = spec.split(':')
-        n = int(n)
+        n = tuple(int(v) for v in n.split('x')) if 'x' in n else int(n)      # 'ZxN' = a Z x N x N slab
         runs = [make(name, n, False), make(name, n, True)] + [make(name, n, True, m) for m in extra]
         t0 = time.perf_counter()
         while time.perf_counter() - t0 < 1.0:
@@ -66,7 +67,7 @@ def main():
                 res[i].append(a.elapsed_time(b) / 20)
         for (fn, tag), r in zip(runs, res):
             v = sorted(r)
-            print(f'{spec.split(":")[0]}:{n:<5d} {tag:44s} fwd+bwd {v[2]:.4f} ms  [{" ".join(f"{x:.4f}" for x in r)}]', flush=True)
+            print(f'{spec.split(":")[0]}:{str(n):<9s} {tag:44s} fwd+bwd {v[2]:.4f} ms  [{" ".join(f"{x:.4f}" for x in r)}]', flush=True)
 
 
 if __name__ == '__main__':
