@@ -14,11 +14,11 @@ and the stores of a sweep reach ~5.4 TB/s (``scripts/probes/store_patterns.py``)
   make columns 0 and X/8-1 the domain's x boundary), converts each value once to fp32 and runs packed FMAs over
   the cell pairs ``(x+e, x+e+4)`` so every tap operand is a register pair as converted.
 * z partial sums (as ``zsum``): input plane ``q`` adds its taps to outputs ``q+1``, ``q``, ``q-1``; the three
-  accumulator sets rotate with the plane index (loop unrolled by 3, no moves); the first two and last two planes
-  of a chunk skip the taps of outputs outside it (uniform branches), so a chunk costs ``zc`` planes of FMAs.
+  accumulator sets rotate with the plane index (loop unrolled by 3, no moves). (Skipping the taps of outputs outside
+  a chunk in its first / last two planes behind uniform branches measured slower: profiles/r03_op_band_ab2.log.)
 * stores: output ``q-1`` row by row, 16 bytes per lane, 1 KiB contiguous per wave instruction, non-temporal.
 
-Eligible: 3-D, every field fp16, one stencil field (radius ≤ 1), every store a linear combination of its taps
+Eligible: 3-D, every field fp16 (fp32 storage compiles too: opt-in), one stencil field (radius ≤ 1), every store a linear combination of its taps
 (``zsum_plan`` with no centre-plane remainder), rows a multiple of 16 bytes. Measured against the ``zsum`` half ring
 in ``scripts/probes/rowblock27r.py`` (``profiles/r03_band_*.log``).
 """
@@ -312,22 +312,13 @@ def emit_band(ir, name, cfg):
         sp, s0, sn = (k + 2) % 3, k, (k + 1) % 3
         B = [f'{ind}if (jj < nplanes) {{', f'{ind}  __syncthreads();',
              f'{ind}  const {et}* sl = lds + (jj % {NS}) * {SLOT} + lofs;']
-        if cfg.BTRIM:
-            B.append(f'{ind}  const bool nd_p = jj >= 2, nd_0 = jj >= 1 && jj + 1 < nplanes, nd_n = jj + 2 < nplanes;')
         first = set()
         for r in range(R + 2):
             B.append(f'{ind}  {{')
             B += row_prologue(ind, r)
-            if not cfg.BTRIM:
-                # every set every plane, one block: dx outer, then the three sets, rows and slots (12-36 independent
-                # FMAs between two dependent ones)
-                B += taps(f'{ind}    ', r, ((sp, 1), (s0, 0), (sn, -1)), first)
-            else:
-                # the first two / last two planes of a chunk skip the taps of outputs outside it (uniform branches)
-                for st, dz, flag in ((sp, 1, 'nd_p'), (s0, 0, 'nd_0'), (sn, -1, 'nd_n')):
-                    body = taps(f'{ind}      ', r, ((st, dz),), first)
-                    if body:
-                        B += [f'{ind}    if ({flag}) {{'] + body + [f'{ind}    }}']
+            # every set every plane, one block: dx outer, then the three sets, rows and slots (12-36 independent
+            # FMAs between two dependent ones)
+            B += taps(f'{ind}    ', r, ((sp, 1), (s0, 0), (sn, -1)), first)
             B.append(f'{ind}  }}')
         # outputs of q+1 that received no tap this plane (no dz = -1 taps) start from zero
         for si in range(NP):

@@ -65,8 +65,7 @@ def _band_config(ir, ve, shape, over):
     if 'BAND' not in over and -(-int(shape[-2]) // TY) * -(-int(shape[0]) // zc) < BAND_MIN_WG:
         return None
     return MarchConfig(VE=ve, BAND=R, BTY=TY, BX=X, D=D, ZSUM=True, NT_STORE=True, ZMIN=zc,
-                       ZMAX=int(over.get('ZMAX', zc)), BLK=int(over.get('BLK', 512)), MAP=int(over.get('MAP', 0)),
-                       BTRIM=bool(int(over.get('BTRIM', 0))))
+                       ZMAX=int(over.get('ZMAX', zc)), BLK=int(over.get('BLK', 512)), MAP=int(over.get('MAP', 0)))
 
 
 def default_march_config(ir, ve, shape=None, tuning=None, band=True):
@@ -143,7 +142,7 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             over[k.strip()] = v.strip() if k.strip() == 'VIEW2D' else int(v)
     for k, v in over.items():
         if k not in ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D',
-                     'ZC', 'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM'):
+                     'ZC', 'BLOCKS', 'MAP', 'BAND', 'BTY'):
             raise ValueError(f"unknown tile parameter '{k}' (gpu_indexing_params / PSAD_MARCH)")
         if k in ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'MAP'):
             cfg[k] = int(v)

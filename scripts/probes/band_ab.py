@@ -2,7 +2,9 @@
 A/B rounds (every variant timed once per round after a warm start). Checks each band variant against the zsum
 result (|diff| <= 1e-3 max|ref|, the fp16 tolerance of the parity tests) before timing.
 
-python scripts/probes/band_ab.py [case ...]   cases: s27_768 s27_1024 s7_768 s7_1024 slab27 slab7"""
+python scripts/probes/band_ab.py [case ...]   cases: s27_768 s27_1024 s7_768 s7_1024 slab27 slab7
+(profiles/r03_band_ab*.log were taken while the emitter still had a trimmed-chunk-edge option, BTRIM, since removed:
+its "notrim" rows are today's kernels.)"""
 import os
 import sys
 import time
@@ -32,16 +34,16 @@ VARIANTS_F32 = {
     'band R4 TY4 D2 zc64': {'BAND': 4, 'BTY': 4, 'D': 2, 'ZMIN': 64, 'ZMAX': 64},
     'band R2 TY4 D2 zc16': {'BAND': 2, 'BTY': 4, 'D': 2, 'ZMIN': 16, 'ZMAX': 16},
     'band R4 TY4 D1 zc16': {'BAND': 4, 'BTY': 4, 'D': 1, 'ZMIN': 16, 'ZMAX': 16},
-    'band R4 TY4 D2 nt16': {'BAND': 4, 'BTY': 4, 'D': 2, 'ZMIN': 16, 'ZMAX': 16, 'BTRIM': 0},
+    'band R4 TY4 D2 nt16': {'BAND': 4, 'BTY': 4, 'D': 2, 'ZMIN': 16, 'ZMAX': 16},
 }
 VARIANTS = {
     'zsum (BAND=0)': {'BAND': 0},
     'band default': {},
     'band zc16': {'ZMIN': 16, 'ZMAX': 16},
     'band zc8': {'ZMIN': 8, 'ZMAX': 8},
-    'band notrim zc48': {'BTRIM': 0, 'ZMIN': 48, 'ZMAX': 48},
-    'band notrim zc24': {'BTRIM': 0},
-    'band notrim zc12': {'BTRIM': 0, 'ZMIN': 12, 'ZMAX': 12},
+    'band notrim zc48': {'ZMIN': 48, 'ZMAX': 48},
+    'band zc24 (default)': {},
+    'band notrim zc12': {'ZMIN': 12, 'ZMAX': 12},
     'band R4 TY8 D2 nt': {'BAND': 4, 'BTY': 8, 'D': 2, 'BTRIM': 0, 'ZMIN': 48, 'ZMAX': 48},
     'band R2 TY4 D3 nt': {'BAND': 2, 'BTY': 4, 'D': 3, 'BTRIM': 0, 'ZMIN': 48, 'ZMAX': 48},
 }

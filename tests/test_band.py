@@ -79,7 +79,7 @@ def test_band_sources_compile():
                pa.AutoDiffOp(W.diffusion_7pt(dtype='float16'), boundary_handling='zeros').forward_assignments):
         hk = HipStencilKernel(_kernel(ac))
         cfg = default_march_config(hk.ir, 8, (32, 64, 256), {'BAND': 4})
-        for c in (cfg, MarchConfig(**{**cfg.__dict__, 'BMASK': True}), MarchConfig(**{**cfg.__dict__, 'BTRIM': False}),
+        for c in (cfg, MarchConfig(**{**cfg.__dict__, 'BMASK': True}),
                   MarchConfig(**{**cfg.__dict__, 'BMASK': True, 'XB': True})):
             src, kname = hk.source(('march', c))
             assert kname.endswith('_band') and 'band schedule' in src
@@ -163,16 +163,16 @@ def test_band_zslab_launch_pattern_bitwise(bh):
 
 
 @pytest.mark.gpu
-def test_band_chunk_length_and_trim_bitwise():
-    """Every output plane sees the same FMA sequence whatever the chunk length and with or without the trimmed
-    first / last planes: results bitwise equal."""
+def test_band_chunk_length_and_band_height_bitwise():
+    """Every output plane sees the same FMA sequence whatever the chunk length and band height (idle lanes on a
+    12-row band): results bitwise equal."""
     torch = _torch()
     op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
     g = torch.Generator().manual_seed(11)
     u = (torch.rand((37, 48, 768), generator=g) * 2 - 1).half().cuda()
     res = []
-    for tun in ({'BAND': 4}, {'BAND': 4, 'ZMIN': 5, 'ZMAX': 5}, {'BAND': 4, 'ZMIN': 16, 'ZMAX': 16, 'BTRIM': 1},
-                {'BAND': 4, 'BTRIM': 1, 'ZMIN': 9, 'ZMAX': 9},
+    for tun in ({'BAND': 4}, {'BAND': 4, 'ZMIN': 5, 'ZMAX': 5}, {'BAND': 4, 'ZMIN': 16, 'ZMAX': 16},
+                {'BAND': 4, 'ZMIN': 9, 'ZMAX': 9},
                 {'BAND': 4, 'BTY': 12}):          # 3 row groups x 96 chunks = 288 tasks on 320 lanes (idle lanes)
         k = _kernel(op.forward_assignments, 'zeros', 'bandc', **tun).compile()
         out = torch.full_like(u, float('nan'))
