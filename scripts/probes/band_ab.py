@@ -44,8 +44,8 @@ VARIANTS = {
     'band notrim zc48': {'ZMIN': 48, 'ZMAX': 48},
     'band zc24 (default)': {},
     'band notrim zc12': {'ZMIN': 12, 'ZMAX': 12},
-    'band R4 TY8 D2 nt': {'BAND': 4, 'BTY': 8, 'D': 2, 'BTRIM': 0, 'ZMIN': 48, 'ZMAX': 48},
-    'band R2 TY4 D3 nt': {'BAND': 2, 'BTY': 4, 'D': 3, 'BTRIM': 0, 'ZMIN': 48, 'ZMAX': 48},
+    'band R4 TY8 D2 nt': {'BAND': 4, 'BTY': 8, 'D': 2, 'ZMIN': 48, 'ZMAX': 48},
+    'band R2 TY4 D3 nt': {'BAND': 2, 'BTY': 4, 'D': 3, 'ZMIN': 48, 'ZMAX': 48},
 }
 
 
