@@ -53,6 +53,14 @@ def _band_config(ir, ve, shape, over):
     if choice is None:
         return None
     TY, R, D = choice
+    ntaps = max(len(pl['w']) for pl in plans)
+    zc0 = int(over.get('ZMIN', BAND_ZC_BOX if ntaps > 12 else BAND_ZC_STAR))
+    if ntaps > 12 and es == 2 and (X // 8) % 128 == 0 and R == 4 and \
+            -(-int(shape[-2]) // 16) * -(-int(shape[0]) // zc0) >= BAND_MIN_WG:
+        # box stencils on rows of a multiple of 1024 halves: 16-row bands, one plane in flight (18/16 rows read per
+        # band instead of 10/8; 72 KB LDS): 27-point 1024³ fwd+bwd 1.712-1.719 vs 1.764-1.766 ms with 8-row bands
+        # (profiles/r03_op_band_ab5.log, _ab6.log); the 7-point star stencil loses (1.65 vs 1.42), 768-wide rows too
+        TY, D = 16, 1
     if 'BAND' in over:
         R = int(over['BAND'])
     TY = int(over.get('BTY', TY if TY % R == 0 else R * max(1, TY // R)))
@@ -60,7 +68,6 @@ def _band_config(ir, ve, shape, over):
     g = band_geometry(X, TY, R, D, es)
     if TY % R or g['NCT'] > 960 or D * g['NI'] > 63 or g['lds_bytes'] > 160 * 1024:
         raise ValueError(f'band schedule: BTY={TY} BAND={R} D={D} do not fit rows of {X} elements')
-    ntaps = max(len(pl['w']) for pl in plans)
     zc = int(over.get('ZMIN', BAND_ZC_BOX if ntaps > 12 else BAND_ZC_STAR))
     if 'BAND' not in over and -(-int(shape[-2]) // TY) * -(-int(shape[0]) // zc) < BAND_MIN_WG:
         return None
