@@ -246,3 +246,24 @@ def test_band_through_the_op(bh, monkeypatch):
     refb = OE.evaluate(op.backward_assignments, {'diffout': d.astype(np.float64)}, boundary_handling=bh)
     (gname,) = refb.keys()
     assert_close_rel(ut.grad.double().cpu().numpy(), refb[gname], TOL16, 'adjoint')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape', [(6, 32, 1024), (5, 40, 1024)])
+def test_band_16_row_bands_1024(shape):
+    """The 1024-wide box-stencil geometry (16-row bands, 8 compute waves, one plane in flight) vs the oracle;
+    Y = 40 leaves a ragged last band (masked stores)."""
+    torch = _torch()
+    op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
+    rng = np.random.default_rng(shape[1])
+    for which, ac in (('f', op.forward_assignments), ('b', op.backward_assignments)):
+        k = _kernel(ac, 'zeros', f'band16_{which}', BAND=4, BTY=16, D=1).compile()
+        ins = {f.name: rng.uniform(-1, 1, shape).astype(np.float16) for f in k.ir.fields_read}
+        ref = OE.evaluate(ac, {n: a.astype(np.float64) for n, a in ins.items()}, boundary_handling='zeros')
+        outs = {f.name: torch.zeros(shape, dtype=torch.float16, device='cuda') for f in k.ir.fields_written}
+        k(**{n: torch.from_numpy(a).cuda() for n, a in ins.items()}, **outs)
+        torch.cuda.synchronize()
+        cfg = k.last_variant[1]
+        assert (cfg.BAND, cfg.BTY, cfg.D, cfg.BMASK) == (4, 16, 1, shape[1] % 16 != 0), cfg
+        for n, t in outs.items():
+            assert_close_rel(t.double().cpu().numpy(), ref[n], TOL16, f'{which} {n} {shape}')
