@@ -267,3 +267,24 @@ def test_band_16_row_bands_1024(shape):
         assert (cfg.BAND, cfg.BTY, cfg.D, cfg.BMASK) == (4, 16, 1, shape[1] % 16 != 0), cfg
         for n, t in outs.items():
             assert_close_rel(t.double().cpu().numpy(), ref[n], TOL16, f'{which} {n} {shape}')
+
+
+@pytest.mark.gpu
+def test_band_scalar_coefficient():
+    """Tap weights that are kernel parameters (a sympy symbol, passed at launch) on the band schedule."""
+    torch = _torch()
+    u, out = ps.fields('u, out: float16[3d]')
+    a = sp.Symbol('alpha')
+    ac = ps.AssignmentCollection({out.center: u.center + a * (u[1, 0, 0] + u[-1, 0, 0] + u[0, 1, 0] + u[0, -1, 0] +
+                                                              u[0, 0, 1] + u[0, 0, -1] - 6 * u.center)})
+    k = _kernel(ac, 'zeros', 'bands', BAND=4).compile()
+    shape = (9, 16, 256)
+    x = np.random.default_rng(5).uniform(-1, 1, shape).astype(np.float16)
+    res = torch.zeros(shape, dtype=torch.float16, device='cuda')
+    k(u=torch.from_numpy(x).cuda(), out=res, alpha=0.15)
+    torch.cuda.synchronize()
+    assert k.last_variant[1].BAND == 4
+    xs = x.astype(np.float64)
+    ref = OE.evaluate(ps.AssignmentCollection({out.center: ac.main_assignments[0].rhs.subs(a, 0.15)}),
+                      {'u': xs}, boundary_handling='zeros')['out']
+    assert_close_rel(res.double().cpu().numpy(), ref, TOL16)
