@@ -77,8 +77,14 @@ def cpu_baseline(budget_s, workload='diffusion7_f32', edge=1024):
     from oracle import cref
     build_dir = os.path.join(ROOT, 'oracle', 'build_native')
     lib = cref.load(build_dir=build_dir, march='native')
+    # OpenMP threads: the CPUs this process may run on (sched_getaffinity), capped by OMP_NUM_THREADS where the
+    # job sets it — the GPU box exports OMP_NUM_THREADS=16, its CPU share per GPU, while sched_getaffinity there
+    # lists every CPU of the host (256); the cap is reported with the figure
     affinity = len(os.sched_getaffinity(0))
-    mt = int(os.environ.get('OMP_NUM_THREADS', '0')) or affinity
+    omp = int(os.environ.get('OMP_NUM_THREADS', '0'))
+    mt = min(omp, affinity) if omp > 0 else affinity
+    cap = (f'OMP_NUM_THREADS={omp} (the job\'s CPU share) of {affinity} CPUs in sched_getaffinity' if 0 < omp < affinity
+           else f'sched_getaffinity: {affinity} CPUs')
     w27 = workload == 'stencil27_f16'
     if w27:
         from pystencils_autodiff_amd import workloads as W
@@ -120,7 +126,7 @@ def cpu_baseline(budget_s, workload='diffusion7_f32', edge=1024):
             'threads_1': {'value': v1, 'threads': t1, 'sweeps': reps1, 'seconds': round(el1, 2),
                           'sample': f'{p1}x{edge}x{edge}'},
             'threads_mt': {'value': vm, 'threads': tm, 'sweeps': repsm, 'seconds': round(elm, 2),
-                           'sample': f'{pm}x{edge}x{edge}', 'cpu_openmp': True},
+                           'sample': f'{pm}x{edge}x{edge}', 'cpu_openmp': True, 'threads_rule': cap},
             'cpu_model': model, 'cpus_available': affinity}
 
 
@@ -135,6 +141,29 @@ def load_traffic(workload, kernel):
         return None, None
     k = entry.get('kernels', {}).get(kernel)
     return (k['total'] if k else None), entry.get('source')
+
+
+def roofline(name, r, world):
+    """The line's ``roofline`` object: ``achieved`` = algorithmic bytes of one step (forward + adjoint sweep over the
+    whole domain) ÷ the step time (barrier-bracketed, max over ranks) ÷ GPUs, so ``frac`` is the
+    step-level figure; ``frac_fwd`` / ``frac_bwd`` are each sweep on its own (algorithmic bytes of one launch over
+    this rank's slab ÷ its HIP-event time on the launch stream). ``traffic``: HBM bytes per launch from the committed
+    PMC passes for this exact launch shape (full domain at N=1), else null (no slab-shaped entry)."""
+    wl = WORKLOADS[name]
+    n, zl = r['n'], r['zl']
+    key = f'{name}_{n}^3' if world == 1 else f'{name}_{zl}x{n}^2_slab'
+    tf, src = load_traffic(key, r['kname'])
+    tb, _ = load_traffic(key, r['kname'].replace('_forward_', '_backward_'))
+    traffic = tf + tb if tf is not None and tb is not None else None      # per step, like ``achieved``
+    return {'bound': 'hbm', 'achieved': round(r['achieved'], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(r['achieved'] / HBM_PEAK_GBS, 4),
+            'frac_fwd': round(r['achieved_fwd'] / HBM_PEAK_GBS, 4),
+            'frac_bwd': round(r['achieved_bwd'] / HBM_PEAK_GBS, 4),
+            'achieved_fwd': round(r['achieved_fwd'], 1), 'achieved_bwd': round(r['achieved_bwd'], 1),
+            'traffic': traffic, 'traffic_fwd_launch': tf,
+            'traffic_source': src or f'no PMC entry for the launch shape {key}',
+            'kernel': f'{r["kname"]} + its adjoint (step: both sweeps, {2 * wl["bytes"]} B per cell)',
+            'bytes_per_launch': r['bytes_fwd'], 'bytes_per_step': 2 * wl['bytes'] * r['cells']}
 
 
 def run_workload(name, edge, args, world, rank, distributed, extras, warmup=None):
@@ -233,9 +262,12 @@ def run_workload(name, edge, args, world, rank, distributed, extras, warmup=None
     value = cells_total * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
 
-    # kernel-level: algorithmic bytes of one forward launch over this rank's slab / its event time
+    # algorithmic bytes of one sweep (forward or adjoint) over this rank's slab; per sweep from its HIP-event time,
+    # per step (both sweeps, the line's roofline) from the barrier-bracketed clock, max over ranks, per GPU
     bytes_fwd = bytes_per_cell * zl * n * n
-    achieved = bytes_fwd / (fwd_ms * 1e-3) / 1e9
+    achieved_fwd = bytes_fwd / (fwd_ms * 1e-3) / 1e9
+    achieved_bwd = bytes_fwd / (bwd_ms * 1e-3) / 1e9
+    achieved = 2 * bytes_per_cell * cells_total / world / (ms_per_step * 1e-3) / 1e9
     result_extra = {}
     if extras and not distributed:
         # the same step with torch's default engine (backward on its device thread; the op's backward is
@@ -267,8 +299,9 @@ def run_workload(name, edge, args, world, rank, distributed, extras, warmup=None
 
     zop_keep = zop if distributed else None
     kname = fwd_k.source(fwd_k.last_variant)[1] if fwd_k.last_variant else fwd_k.name
-    out = dict(n=n, value=value, ms_per_step=ms_per_step, fwd_ms=fwd_ms, bwd_ms=bwd_ms, achieved=achieved,
-               bytes_fwd=bytes_fwd, kname=kname, cells=cells_total, extra=result_extra, zop=zop_keep)
+    out = dict(n=n, zl=zl, value=value, ms_per_step=ms_per_step, fwd_ms=fwd_ms, bwd_ms=bwd_ms, achieved=achieved,
+               achieved_fwd=achieved_fwd, achieved_bwd=achieved_bwd, bytes_fwd=bytes_fwd, kname=kname,
+               cells=cells_total, extra=result_extra, zop=zop_keep)
     del uu, u, d, fn, op
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -306,8 +339,7 @@ def main():
     n = primary['n']
     wl = WORKLOADS[args.workload]
     value, ms_per_step, fwd_ms, bwd_ms = (primary[k] for k in ('value', 'ms_per_step', 'fwd_ms', 'bwd_ms'))
-    achieved, bytes_fwd, kname, cells_total = (primary[k] for k in ('achieved', 'bytes_fwd', 'kname', 'cells'))
-    bytes_per_cell = wl['bytes']
+    achieved, cells_total = primary['achieved'], primary['cells']
     result_extra = primary['extra']
     zop = primary['zop']
     cpu = None
@@ -321,8 +353,6 @@ def main():
     if distributed:
         dist.barrier()
     if rank == 0:
-        workload = f'{args.workload}_{n}^3'
-        traffic, traffic_src = load_traffic(workload, kname)
         res = {
             'metric': f'Mcells/s forward+backward, {wl["label"]} {n}^3',
             'value': round(value, 1),
@@ -344,19 +374,13 @@ def main():
                        + ', autograd engine single-threaded (set_multithreading_enabled(False)) at every N'},
             'fwd_ms': round(fwd_ms, 4),
             'bwd_ms': round(bwd_ms, 4),
-            'hbm_roofline_frac_step': round(2 * bytes_per_cell * cells_total / (ms_per_step * 1e-3) / 1e9
-                                            / (HBM_PEAK_GBS * world), 4),
-            'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                         'traffic_source': traffic_src,
-                         'kernel': f'{kname} (forward sweep; the adjoint sweep moves the same bytes)',
-                         'bytes_per_launch': bytes_fwd},
+            'hbm_roofline_frac_step': round(achieved / HBM_PEAK_GBS, 4),
+            'roofline': roofline(args.workload, primary, world),
             'cpu_baseline': cpu,
         }
         if secondary is not None:
             w2 = WORKLOADS[args.secondary]
             n2 = secondary['n']
-            traffic2, traffic2_src = load_traffic(f'{args.secondary}_{n2}^3', secondary['kname'])
             res['secondary'] = {
                 'metric': f'Mcells/s forward+backward, {w2["label"]} {n2}^3', 'name': args.secondary,
                 'value': round(secondary['value'], 1), 'unit': 'Mcells/s', 'n_gpus': world, 'steps': args.steps,
@@ -364,13 +388,8 @@ def main():
                 'fwd_ms': round(secondary['fwd_ms'], 4), 'bwd_ms': round(secondary['bwd_ms'], 4),
                 'dtype': w2['dtype_tag'], 'cells': secondary['cells'],
                 'decomposition': f'z-slab x{world}' if world > 1 else 'single GPU',
-                'hbm_roofline_frac_step': round(2 * w2['bytes'] * secondary['cells'] / (secondary['ms_per_step'] * 1e-3)
-                                                / 1e9 / (HBM_PEAK_GBS * world), 4),
-                'roofline': {'bound': 'hbm', 'achieved': round(secondary['achieved'], 1), 'peak': HBM_PEAK_GBS,
-                             'unit': 'GB/s', 'frac': round(secondary['achieved'] / HBM_PEAK_GBS, 4),
-                             'traffic': traffic2, 'traffic_source': traffic2_src,
-                             'kernel': f'{secondary["kname"]} (forward sweep)',
-                             'bytes_per_launch': secondary['bytes_fwd']}}
+                'hbm_roofline_frac_step': round(secondary['achieved'] / HBM_PEAK_GBS, 4),
+                'roofline': roofline(args.secondary, secondary, world)}
         res.update(result_extra)
         print(json.dumps(res))
     if distributed:

@@ -185,6 +185,10 @@ def emit_band(ir, name, cfg):
     L.append(f'        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + i * '
              f'{64 * VE}), 16, vo[i], 0, 0, 0);')
     L.append('    };')
+    if cfg.BSTAG:
+        # probe: the co-resident workgroups of a CU's first round start a fraction of a plane apart
+        L.append(f'    {{ const int st = (blockIdx.x >> 8) % 3; for (int i = 0; i < st; ++i) '
+                 f'__builtin_amdgcn_s_sleep({int(cfg.BSTAG)}); }}')
     L.append(f'    for (int i = 0; i < {D}; ++i)')
     L.append('      if (i < nplanes) issue(zb - 1 + i, i);')
     L.append('    for (int j = 0; j < nplanes; ++j) {')
@@ -214,10 +218,16 @@ def emit_band(ir, name, cfg):
         L.append('  unsigned rowok = 0u;                           // rows of the lane inside [ylo, yhi), one bit each')
         L.append(f'  for (int o = 0; o < {R}; ++o) rowok |= (active && yrow0 + o >= ylo && yrow0 + o < yhi) ? (1u << o) : 0u;')
     L.append("  // edge dword (elements, from the lane's chunk): lane 0 the dword left of it, lane 63 the one right of it,")
-    L.append("  // the other lanes consecutive dwords of the wave's block (conflict-free, unused)")
+    L.append("  // the other lanes dwords of the wave's block no other lane of their 32-lane half reads (unused): banks")
+    L.append("  // (a/4) mod 32 all distinct per half (the compiler pairs these reads into ds_read2st64_b32). Lane 0 of")
+    L.append("  // column 0 (x boundary, masked) reads its own first dword instead of the one before the slot.")
     dw = 4 // es                                          # elements per dword
-    # dword targets relative to the wave's block: -1, 1 .. 62, 256 (64 chunks of 4 dwords)
-    L.append(f'  const int eoff = {dw} * (lane == 0 ? -1 : (lane == 63 ? 256 : lane)) - {VE} * lane;')
+    # dword targets relative to the wave's block (64 chunks of 4 dwords): -1, 0 .. 30 | 33 .. 63, 256
+    if cfg.BEDGE:
+        L.append(f'  const int eoff = {dw} * (lane == 0 ? (col == 0 ? 0 : -1) : (lane == 63 ? 256 : (lane < 32 ? lane - 1 '
+                 f': lane + 1))) - {VE} * lane;')
+    else:
+        L.append(f'  const int eoff = {dw} * (lane == 0 ? -1 : (lane == 63 ? 256 : lane)) - {VE} * lane;')
     for si in range(NP):
         for s_ in range(3):
             for o in range(R):
@@ -308,37 +318,84 @@ def emit_band(ir, name, cfg):
         B.append(f'{ind}}}')
         return B
 
-    def step(k, ind):
+    def step(k, ind, part='full', guard='jj < nplanes', store='jj >= 2'):
+        """One plane with static set roles (k = plane index mod 3). ``part`` drops the taps of outputs outside the
+        chunk: 'p0' = the chunk's first input plane (feeds output zb only), 'p1' = its second (not output zb-1),
+        'e0' = the second to last (not output ze), 'e1' = the last (feeds output ze-1 only)."""
         sp, s0, sn = (k + 2) % 3, k, (k + 1) % 3
-        B = [f'{ind}if (jj < nplanes) {{', f'{ind}  __syncthreads();',
+        sets = {'full': ((sp, 1), (s0, 0), (sn, -1)), 'p0': ((sn, -1),), 'p1': ((s0, 0), (sn, -1)),
+                'e0': ((sp, 1), (s0, 0)), 'e1': ((sp, 1),)}[part]
+        B = [f'{ind}if ({guard}) {{' if guard else f'{ind}{{', f'{ind}  __syncthreads();',
              f'{ind}  const {et}* sl = lds + (jj % {NS}) * {SLOT} + lofs;']
+        # sets a trimmed step leaves alone are dead (outputs already stored or outside the chunk): overwrite them first
+        # so their old values are not live through the step (a full step overwrites its q+1 set; +16-45 VGPRs else)
+        for s_ in sorted({sp, s0, sn} - {st for st, _ in sets}):
+            for si in range(NP):
+                for o in range(R):
+                    B.append(f'{ind}  ' + ' '.join(f'{A(si, s_, o, a)} = {azero};' for a in range(4)))
         first = set()
         for r in range(R + 2):
             B.append(f'{ind}  {{')
             B += row_prologue(ind, r)
             # every set every plane, one block: dx outer, then the three sets, rows and slots (12-36 independent
             # FMAs between two dependent ones)
-            B += taps(f'{ind}    ', r, ((sp, 1), (s0, 0), (sn, -1)), first)
+            B += taps(f'{ind}    ', r, sets, first)
             B.append(f'{ind}  }}')
         # outputs of q+1 that received no tap this plane (no dz = -1 taps) start from zero
-        for si in range(NP):
-            for o in range(R):
-                for a in range(4):
-                    if (si, o, a) not in first:
-                        B.append(f'{ind}  {A(si, sn, o, a)} = {azero};')
+        if any(dz == -1 for _, dz in sets):
+            for si in range(NP):
+                for o in range(R):
+                    for a in range(4):
+                        if (si, o, a) not in first:
+                            B.append(f'{ind}  {A(si, sn, o, a)} = {azero};')
         # idle lanes (band tasks not a multiple of 64) compute on a clamped task with wrong x neighbours: no stores
-        B.append(f'{ind}  if (jj >= 2{" && active" if g["ntask"] != NCT else ""}) {{')
-        for si, fld in enumerate(store_field):
-            B += stores(f'{ind}    ', si, sp, fld)
-        B.append(f'{ind}  }}')
+        act = 'active' if g['ntask'] != NCT else ''
+        cond = ' && '.join(c for c in (store, act) if c)
+        if store is not None:
+            B.append(f'{ind}  if ({cond}) {{' if cond else f'{ind}  {{')
+            for si, fld in enumerate(store_field):
+                B += stores(f'{ind}    ', si, sp, fld)
+            B.append(f'{ind}  }}')
         B.append(f'{ind}  ++jj;')
         B.append(f'{ind}}}')
         return B
     L.append('  int jj = 0;')
-    L.append('  #pragma unroll 1')
-    L.append('  while (jj < nplanes) {')
-    for k in range(3):
-        L += step(k, '    ')
-    L.append('  }')
+    if cfg.BTRIM == 1:
+        # the chunk's first two input planes run peeled steps without the taps of outputs before it (27 of 27·(zc+2)
+        # FMAs per cell column); every chunk has >= 3 planes, so no fallback loop
+        L += step(0, '  ', 'p0', None, None)
+        L += step(1, '  ', 'p1', None, None)
+        L.append('  #pragma unroll 1')
+        L.append('  while (jj < nplanes) {')
+        for k in (2, 0, 1):
+            L += step(k, '    ', 'full', 'jj < nplanes', '')
+        L.append('  }')
+    else:
+        if cfg.BTRIM == 2:
+            # also the last two input planes (the taps of outputs after the chunk; 54 of 27·(zc+2) FMAs per cell
+            # column), inside the unrolled loop at each static set role (a switch on jj % 3 after the loop made the
+            # compiler select between the register sets: 192 VGPRs instead of 156); chunks of >= 3 planes
+            L.append('  if (nplanes >= 5) {')
+            L += step(0, '    ', 'p0', None, None)
+            L += step(1, '    ', 'p1', None, None)
+            L.append('    const int nend = nplanes - 2;')
+            L.append('    #pragma unroll 1')
+            L.append('    while (jj < nplanes) {')
+            for k in (2, 0, 1):
+                full = step(k, '      ', 'full', 'jj < nend', '')
+                e0 = step(k, '      ', 'e0', 'jj == nend', '')
+                e1 = step(k, '      ', 'e1', 'jj < nplanes', '')
+                e0[0] = e0[0].replace('if', 'else if', 1)
+                e1[0] = e1[0].replace('if', 'else if', 1)
+                L += full + e0 + e1
+            L.append('    }')
+            L.append('  } else {')
+        L.append('  #pragma unroll 1')
+        L.append('  while (jj < nplanes) {')
+        for k in range(3):
+            L += step(k, '    ')
+        L.append('  }')
+        if cfg.BTRIM == 2:
+            L.append('  }')
     L.append('}')
     return '\n'.join(L) + '\n'

@@ -31,6 +31,14 @@ BAND_MIN_WG = 1024
 # fp32 storage (4 cells per 16-byte chunk) measured slower through the op (7-point 512³ 0.387 vs 0.373 ms, 768³
 # 1.325 vs 1.261): opt-in only (BAND=R)
 BAND_F32_MAX_X = 0
+BAND_TRIM = 0
+
+# gpu_indexing_params keys of pystencils' own GPU indexing (``block_size``, ``maximum_block_size``, …, e.g.
+# ``gpu_indexing_params={'block_size': (8, 4, 2)}`` in the reference's tests/test_graph_datahandling.py:70): they
+# describe a one-thread-per-cell launch these schedules do not have, so they are accepted and ignored. Upper-case
+# keys are this layer's tile parameters; an unknown one is a typo and raises.
+TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
+             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG')
 
 
 def _band_config(ir, ve, shape, over):
@@ -72,7 +80,9 @@ def _band_config(ir, ve, shape, over):
     if 'BAND' not in over and -(-int(shape[-2]) // TY) * -(-int(shape[0]) // zc) < BAND_MIN_WG:
         return None
     return MarchConfig(VE=ve, BAND=R, BTY=TY, BX=X, D=D, ZSUM=True, NT_STORE=True, ZMIN=zc,
-                       ZMAX=int(over.get('ZMAX', zc)), BLK=int(over.get('BLK', 512)), MAP=int(over.get('MAP', 0)))
+                       ZMAX=int(over.get('ZMAX', zc)), BLK=int(over.get('BLK', 512)), MAP=int(over.get('MAP', 0)),
+                       BTRIM=int(over.get('BTRIM', BAND_TRIM)), BEDGE=int(over.get('BEDGE', 1)),
+                       BSTAG=int(over.get('BSTAG', 0)))
 
 
 def default_march_config(ir, ve, shape=None, tuning=None, band=True):
@@ -142,14 +152,13 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
         # (128×1024²): 0.191 / 0.187 ms vs 0.214 / 0.208 ms with 256×32 tiles; 1024³ a tie
         cfg['CX'] = 2
     env = os.environ.get('PSAD_MARCH')
-    over = dict(tuning or {})
+    over = {k: v for k, v in dict(tuning or {}).items() if not k.islower()}     # pystencils indexing keys: ignored
     if env:
         for kv in env.split(','):
             k, v = kv.split('=')
             over[k.strip()] = v.strip() if k.strip() == 'VIEW2D' else int(v)
     for k, v in over.items():
-        if k not in ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D',
-                     'ZC', 'BLOCKS', 'MAP', 'BAND', 'BTY'):
+        if k not in TILE_KEYS:
             raise ValueError(f"unknown tile parameter '{k}' (gpu_indexing_params / PSAD_MARCH)")
         if k in ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'MAP'):
             cfg[k] = int(v)

@@ -72,7 +72,7 @@ def _lattice_sweeps(step, which, launches):
         plan = plans.get(sig)
         if plan is None:
             plan = plans[sig] = K.plan(which, list(ts), mask, om)
-        plan(tuple(t.data_ptr() for t in ts) + (mptr,), stream)
+        plan(tuple(t.data_ptr() for t in ts) + (mptr,), stream, om)
 
 
 def _guess_src_dst_field_from_update_rule(update_rule, src_hint, dst_hint):

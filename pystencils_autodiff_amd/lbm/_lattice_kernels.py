@@ -434,10 +434,11 @@ class LatticeKernels:
 
     def plan(self, which, tensors, mask, omega):
         """The launch of ``which`` ('fwd' / 'adj') on tensors of these shapes, strides, dtype and device (with or
-        without walls, at ω): a ``LaunchPlan`` whose pointer slots are patched per launch — the time-step op
-        launches T of them per apply."""
-        key = (which, float(omega), mask is not None) + tuple((tuple(t.shape), tuple(t.stride()), t.dtype, t.device)
-                                                             for t in tensors)
+        without walls): a ``LaunchPlan`` whose pointer slots and relaxation rate are patched per launch — the
+        time-step op launches T of them per apply. ω is not part of the key (a trained or scheduled rate reuses the
+        plan); the plan is built with the first ω it sees."""
+        key = (which, mask is not None) + tuple((tuple(t.shape), tuple(t.stride()), t.dtype, t.device)
+                                                for t in tensors)
         plan = self._plans.get(key)
         if plan is not None:
             return plan
@@ -452,7 +453,7 @@ class LatticeKernels:
         fmt = 'Q' * len(ptrs) + 'iii' + code * (4 * len(tensors)) + 'q' * len(tensors) + \
             ('d' if self.ct == 'double' else 'f')
         args = _pack(fmt, *ptrs, Z, Y, X, *strides, *reach, float(omega))
-        plan = self._plans[key] = LaunchPlan(fn, nblocks, args, len(ptrs))
+        plan = self._plans[key] = LaunchPlan(fn, nblocks, args, len(ptrs), dev, _offset(fmt, len(fmt) - 1), fmt[-1])
         return plan
 
     def forward(self, src, dst, omega, mask=None, stream=None):
@@ -460,7 +461,7 @@ class LatticeKernels:
         if self.target != 'gpu':
             return self._cpu('fwd', [src, dst], omega, mask)
         self.plan('fwd', [src, dst], mask, omega)(
-            (src.data_ptr(), dst.data_ptr(), mask.data_ptr() if mask is not None else 0), _stream(stream, src))
+            (src.data_ptr(), dst.data_ptr(), mask.data_ptr() if mask is not None else 0), _stream(stream, src), omega)
 
     def adjoint(self, src, g, out, omega, mask=None, stream=None):
         """``out = (∂ step / ∂ src)ᵀ g`` at the state ``src``."""
@@ -468,7 +469,7 @@ class LatticeKernels:
             return self._cpu('adj', [src, g, out], omega, mask)
         self.plan('adj', [src, g, out], mask, omega)(
             (src.data_ptr(), g.data_ptr(), out.data_ptr(), mask.data_ptr() if mask is not None else 0),
-            _stream(stream, src))
+            _stream(stream, src), omega)
 
     def _extent(self, t):
         shape = [int(n) for n in t.shape[:self.stencil.D]]
@@ -521,18 +522,27 @@ class LatticeKernels:
 
 
 class LaunchPlan:
-    """One lattice kernel launch with its argument buffer; ``plan(ptrs, stream)`` patches the leading pointer
-    slots (the pdf arrays, then the neighbour mask) and launches."""
-    __slots__ = ('fn', 'nblocks', 'template', 'fmt')
+    """One lattice kernel launch with its argument buffer; ``plan(ptrs, stream, omega)`` patches the leading pointer
+    slots (the pdf arrays, then the neighbour mask) and the relaxation rate, and launches on the plan's device
+    (made current for the launch when it is not: the function handle belongs to that device's module)."""
+    __slots__ = ('fn', 'nblocks', 'template', 'fmt', 'device', 'om_off', 'om_fmt')
 
-    def __init__(self, fn, nblocks, template, nptr):
+    def __init__(self, fn, nblocks, template, nptr, device, om_off, om_code):
         self.fn, self.nblocks, self.template, self.fmt = fn, nblocks, template, f'<{nptr}Q'
+        self.device, self.om_off, self.om_fmt = device, om_off, '<' + om_code
 
-    def __call__(self, ptrs, stream):
+    def __call__(self, ptrs, stream, omega=None):
         from ..backends import hip_runtime as rt
         buf = bytearray(self.template)
         struct.pack_into(self.fmt, buf, 0, *ptrs)
-        rt.launch(self.fn, (self.nblocks,), (256,), bytes(buf), stream)
+        if omega is not None:
+            struct.pack_into(self.om_fmt, buf, self.om_off, float(omega))
+        import torch
+        if self.device is not None and self.device != torch.cuda.current_device():
+            with torch.cuda.device(self.device):
+                rt.launch(self.fn, (self.nblocks,), (256,), bytes(buf), stream)
+        else:
+            rt.launch(self.fn, (self.nblocks,), (256,), bytes(buf), stream)
 
 
 def _stream(stream, t):
@@ -540,6 +550,18 @@ def _stream(stream, t):
         return stream
     import torch
     return torch._C._cuda_getCurrentRawStream(t.device.index)
+
+
+def _offset(fmt, i):
+    """Byte offset of argument ``i`` in ``_pack(fmt, ...)``."""
+    off = 0
+    for j, c in enumerate(fmt):
+        size = struct.calcsize(c)
+        off += (-off) % size
+        if j == i:
+            return off
+        off += size
+    raise IndexError(i)
 
 
 def _pack(fmt, *vals):

@@ -579,14 +579,19 @@ class _NativeSlab:
         except (KeyError, TypeError, ValueError):
             return None
         a0 = args[0]
-        key = (tuple(a0.shape), a0.dtype, a0.device)
+        # per-call conditions (checked on every call, never cached: a later call of the same signature may meet them)
+        for a in args:
+            if not a.is_cuda or not a.is_contiguous() or a.data_ptr() % 32 or a.device != a0.device or \
+                    tuple(a.shape) != tuple(a0.shape):
+                return None
+        key = (tuple(a0.shape), tuple(a.dtype for a in args), a0.device)
         pid = self.plans.get(key)
         if pid is None:
             try:
                 pid = self._build(args, names, halo)
             except (TypeError, ValueError):
                 pid = None
-            self.plans[key] = -1 if pid is None else pid
+            self.plans[key] = -1 if pid is None else pid     # -1: the signature itself does not fit a plan
         if pid is None or pid < 0:
             return None
         outs = native_module().apply_slab(pid, list(args), scal)

@@ -80,7 +80,8 @@ def test_band_sources_compile():
         hk = HipStencilKernel(_kernel(ac))
         cfg = default_march_config(hk.ir, 8, (32, 64, 256), {'BAND': 4})
         for c in (cfg, MarchConfig(**{**cfg.__dict__, 'BMASK': True}),
-                  MarchConfig(**{**cfg.__dict__, 'BMASK': True, 'XB': True})):
+                  MarchConfig(**{**cfg.__dict__, 'BMASK': True, 'XB': True}),
+                  MarchConfig(**{**cfg.__dict__, 'BTRIM': 1}), MarchConfig(**{**cfg.__dict__, 'BTRIM': 2})):
             src, kname = hk.source(('march', c))
             assert kname.endswith('_band') and 'band schedule' in src
             assert len(rt.compile_hip(src)) > 0
@@ -173,7 +174,12 @@ def test_band_chunk_length_and_band_height_bitwise():
     res = []
     for tun in ({'BAND': 4}, {'BAND': 4, 'ZMIN': 5, 'ZMAX': 5}, {'BAND': 4, 'ZMIN': 16, 'ZMAX': 16},
                 {'BAND': 4, 'ZMIN': 9, 'ZMAX': 9},
-                {'BAND': 4, 'BTY': 12}):          # 3 row groups x 96 chunks = 288 tasks on 320 lanes (idle lanes)
+                {'BAND': 4, 'BTY': 12},           # 3 row groups x 96 chunks = 288 tasks on 320 lanes (idle lanes)
+                # peeled chunk-edge planes (taps of outputs outside the chunk skipped): the same FMAs per stored cell
+                {'BAND': 4, 'BTRIM': 1}, {'BAND': 4, 'BTRIM': 1, 'ZMIN': 1, 'ZMAX': 1},
+                {'BAND': 4, 'BTRIM': 1, 'ZMIN': 16, 'ZMAX': 16},
+                {'BAND': 4, 'BTRIM': 2, 'ZMIN': 9, 'ZMAX': 9},
+                {'BAND': 4, 'BTRIM': 2, 'ZMIN': 2, 'ZMAX': 2}):   # chunks of < 3 planes: the untrimmed loop
         k = _kernel(op.forward_assignments, 'zeros', 'bandc', **tun).compile()
         out = torch.full_like(u, float('nan'))
         k(u=u, out=out)

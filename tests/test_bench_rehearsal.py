@@ -46,7 +46,13 @@ def test_bench_two_ranks_end_to_end(nproc, workload):
     assert res['value'] == pytest.approx(128 ** 3 * 3 / (res['ms_per_step'] * 3 / 1e3) / 1e6, rel=1e-3)
     assert res['config']['name'] == workload
     assert res['metric'].endswith('128^3') and ('27-point fp16' in res['metric']) == (workload == 'stencil27_f16')
-    assert res['roofline']['bytes_per_launch'] == (8 if workload == 'diffusion7_f32' else 4) * 64 * 128 * 128
+    rl = res['roofline']
+    bpc = 8 if workload == 'diffusion7_f32' else 4
+    assert rl['bytes_per_launch'] == bpc * 64 * 128 * 128 and rl['bytes_per_step'] == 2 * bpc * 128 ** 3
+    # frac is the step-level figure: both sweeps' algorithmic bytes / ms_per_step / (N x peak)
+    step_frac = 2 * bpc * 128 ** 3 / (res['ms_per_step'] * 1e-3) / 1e9 / (rl['peak'] * nproc)
+    assert rl['frac'] == pytest.approx(step_frac, rel=1e-2) and rl['frac_fwd'] > 0 and rl['frac_bwd'] > 0
+    assert rl['traffic'] is None            # no PMC entry for a slab-shaped launch: never the 1-GPU figure
     # rank 0 times the CPU path after the timed loop at every N (north_star: "in the same run")
     if workload == 'diffusion7_f32':            # config 5 timed in the same run (the driver's scaling runs)
         sec = res['secondary']
