@@ -1,8 +1,8 @@
 """Differentiable lattice Boltzmann time stepping (reference ``pystencils_autodiff.lbm``)."""
 from ._autodiff_lbstep import AutoDiffLatticeBoltzmannStep, PdfFieldNotDetectedException, SimulationResultsTensors
 from ._method import LBStencil, create_lb_adjoint_rule, create_lb_update_rule, equilibrium_setter, macroscopic_getter
-from .boundaries import AdjointBoundaryCondition, AdjointNoSlip, NoSlip, make_slice
+from .boundaries import UBB, AdjointBoundaryCondition, AdjointNoSlip, Boundary, NoSlip, link_coefficients, make_slice
 
 __all__ = ['AutoDiffLatticeBoltzmannStep', 'PdfFieldNotDetectedException', 'SimulationResultsTensors', 'LBStencil',
-           'create_lb_update_rule', 'create_lb_adjoint_rule', 'macroscopic_getter', 'equilibrium_setter', 'NoSlip',
-           'AdjointNoSlip', 'AdjointBoundaryCondition', 'make_slice']
+           'create_lb_update_rule', 'create_lb_adjoint_rule', 'macroscopic_getter', 'equilibrium_setter', 'Boundary',
+           'NoSlip', 'UBB', 'AdjointNoSlip', 'AdjointBoundaryCondition', 'link_coefficients', 'make_slice']

@@ -38,7 +38,8 @@ from .. import ps
 from ..autodiff import AutoDiffOp
 from ._lattice_kernels import LatticeKernels, neighbour_mask
 from ._method import LBStencil
-from .boundaries import AdjointBoundaryCondition, AdjointNoSlip, BoundaryHandling, NoSlip
+from .boundaries import (AdjointBoundaryCondition, AdjointNoSlip, Boundary, BoundaryHandling, NoSlip,  # noqa: F401
+                         link_coefficients)
 
 __all__ = ['AutoDiffLatticeBoltzmannStep', 'PdfFieldNotDetectedException', 'SimulationResultsTensors']
 
@@ -63,16 +64,17 @@ def _lattice_sweeps(step, which, launches):
     the pointers packed per launch."""
     K = step._lattice_kernels()
     mask = step._flag_arg()
+    ids = step._ids_arg()
     om = step._omega_of()
-    mptr = mask.data_ptr() if mask is not None else 0
+    mptr = (mask.data_ptr() if mask is not None else 0, ids.data_ptr() if ids is not None else 0)
     stream = _torch()._C._cuda_getCurrentRawStream(launches[0][0].device.index)
     plans = {}
     for ts in launches:
         sig = tuple(t.stride() for t in ts)
         plan = plans.get(sig)
         if plan is None:
-            plan = plans[sig] = K.plan(which, list(ts), mask, om)
-        plan(tuple(t.data_ptr() for t in ts) + (mptr,), stream, om)
+            plan = plans[sig] = K.plan(which, list(ts), mask, om, ids)
+        plan(tuple(t.data_ptr() for t in ts) + mptr, stream, om)
 
 
 def _guess_src_dst_field_from_update_rule(update_rule, src_hint, dst_hint):
@@ -168,6 +170,7 @@ class AutoDiffLatticeBoltzmannStep:
         self._boundary = BoundaryHandling(self.domain_size, on_change=self._flags_changed)
         self._adjoint_boundary_conditions = {}
         self._flag_dev = None
+        self._ids_dev = None
 
     # -- reference-named properties ----------------------------------------------------------------
     @property
@@ -272,10 +275,13 @@ class AutoDiffLatticeBoltzmannStep:
 
     def set_boundary_including_adjoint(self, boundary_condition, slice_obj=None, mask_callback=None, mask_array=None,
                                        adjoint_boundary_condition=None):
-        """Set ``boundary_condition`` (``NoSlip``) on the selected cells for the forward AND the adjoint steps
-        (the reference's signature; the adjoint condition defaults to ``AdjointBoundaryCondition(bc)``)."""
-        if not isinstance(boundary_condition, NoSlip):
-            raise NotImplementedError(f'boundary {boundary_condition!r}: only NoSlip walls are built')
+        """Set ``boundary_condition`` (a ``Boundary``: ``NoSlip``, ``UBB``, or any boundary whose link is affine,
+        ``boundaries.link_coefficients``) on the selected cells for the forward AND the adjoint steps (the
+        reference's signature; the adjoint condition defaults to ``AdjointBoundaryCondition(bc)``, derived from the
+        forward link by AD)."""
+        if not isinstance(boundary_condition, Boundary) or \
+                isinstance(boundary_condition, (AdjointNoSlip, AdjointBoundaryCondition)):
+            raise NotImplementedError(f'boundary {boundary_condition!r}: needs a forward Boundary object')
         if self._lattice is None:
             raise NotImplementedError('walls need the lattice schedule (a create_lb_update_rule rule without '
                                       'time-constant or additional fields)')
@@ -286,10 +292,13 @@ class AutoDiffLatticeBoltzmannStep:
                                                              constant_fields=self._autodiff.constant_fields))
         elif not isinstance(adjoint_boundary_condition, (AdjointNoSlip, AdjointBoundaryCondition)):
             raise NotImplementedError(f'adjoint boundary {adjoint_boundary_condition!r}')
-        self._boundary.set_boundary(boundary_condition, slice_obj, mask_callback=mask_callback, mask_array=mask_array)
+        link_coefficients(boundary_condition, adjoint_boundary_condition, self.method)   # the kernels' form, or raise
+        self._boundary.set_boundary(boundary_condition, slice_obj, mask_callback=mask_callback, mask_array=mask_array,
+                                    adjoint=adjoint_boundary_condition)
 
     def _flags_changed(self):
         self._flag_dev = None
+        self._ids_dev = None
         self._records = None
 
     def _flag_arg(self):
@@ -306,12 +315,31 @@ class AutoDiffLatticeBoltzmannStep:
                 self._flag_dev = neighbour_mask(self._boundary.flags, self.method, np)
         return self._flag_dev
 
+    def _links(self):
+        """The wall kernels' link tables (None: every wall a plain bounce-back, or no walls)."""
+        return self._boundary.link_tables(self.method) if self._boundary.has_walls else None
+
+    def _ids_arg(self):
+        """The cells' wall ids for kernels with link tables (the flag array on the kernels' device), else None."""
+        if self._links() is None:
+            return None
+        if getattr(self, '_ids_dev', None) is None:
+            if self._gpu:
+                torch = _torch()
+                dev = self._device or torch.device('cuda', torch.cuda.current_device())
+                self._ids_dev = torch.from_numpy(self._boundary.flags.copy()).to(dev)
+            else:
+                self._ids_dev = np.ascontiguousarray(self._boundary.flags)
+        return self._ids_dev
+
     def _lattice_kernels(self):
         walls = self._boundary.has_walls
-        k = self._lattice.get(walls)
+        links = self._links()
+        k = self._lattice.get((walls, links))
         if k is None:
-            k = self._lattice[walls] = LatticeKernels(self.method, getattr(self._update_rule, 'compressible', False),
-                                                      self.pdf_field.dtype.numpy_dtype, walls, self._target)
+            k = self._lattice[(walls, links)] = LatticeKernels(
+                self.method, getattr(self._update_rule, 'compressible', False), self.pdf_field.dtype.numpy_dtype,
+                walls, self._target, links)
         return k
 
     # -- kernels -----------------------------------------------------------------------------------
@@ -323,13 +351,14 @@ class AutoDiffLatticeBoltzmannStep:
 
     def _fwd(self, src, dst, extra):
         if self._lattice is not None:
-            return self._lattice_kernels().forward(src, dst, self._omega_of(), self._flag_arg())
+            return self._lattice_kernels().forward(src, dst, self._omega_of(), self._flag_arg(), ids=self._ids_arg())
         kf, _ = self._kernels()
         kf(**{self._pdf_arr_name: src, self._tmp_arr_name: dst}, **extra, **self.kernel_params)
 
     def _bwd(self, src, diffdst, diffsrc, extra, extra_adj):
         if self._lattice is not None:
-            return self._lattice_kernels().adjoint(src, diffdst, diffsrc, self._omega_of(), self._flag_arg())
+            return self._lattice_kernels().adjoint(src, diffdst, diffsrc, self._omega_of(), self._flag_arg(),
+                                                   ids=self._ids_arg())
         _, kb = self._kernels()
         kb(**{self._pdf_arr_name: src, 'diff' + self._tmp_arr_name: diffdst, 'diff' + self._pdf_arr_name: diffsrc},
            **extra, **extra_adj, **self.kernel_params)

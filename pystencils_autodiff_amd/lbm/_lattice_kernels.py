@@ -44,14 +44,17 @@ def _c(v):
 SELF_BIT = 30      # bit of a cell's neighbour mask: the cell itself is an obstacle (bits 0..Q-1: x − c_i is one)
 
 
-def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
+def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=None):
     """Source of the forward (``lbm_fwd``) and adjoint (``lbm_adj``) kernels.
 
     ``addr='buf'`` (HIP): every pdf array is one buffer resource (its bytes below 2³²); a component's plane
     offset ``q·s_q`` rides in the instruction's scalar offset and each distinct neighbour cell's byte offset is
     ONE 32-bit VGPR shared by all components that pull from it — no 64-bit address arithmetic per access.
     ``'ptr'``: plain pointers (the C target, and arrays of 4 GiB and more). ``walls``: a ``uint32`` neighbour
-    mask per cell (bit i: ``x − c_i`` is an obstacle; bit ``SELF_BIT``: ``x`` is one), one load per cell."""
+    mask per cell (bit i: ``x − c_i`` is an obstacle; bit ``SELF_BIT``: ``x`` is one), one load per cell.
+    ``links``: None (every wall a plain bounce-back), or per wall id (the flag array's values) the boundary's link
+    coefficients per direction (``boundaries.link_coefficients``): a bounced component then becomes
+    ``α·src_ī(x) + β`` (id of the wall cell ``x − c_i`` from the flag array) and its adjoint is scaled by γ."""
     D, Q = stencil.D, stencil.Q
     dirs = [tuple(d) for d in stencil.directions]
     w = [float(x) for x in stencil.weights]
@@ -68,6 +71,14 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
     L.append(f'typedef {ctype} T;\ntypedef {idx} IDX;')
     if hip:
         L.append('typedef unsigned u32x2 __attribute__((ext_vector_type(2)));')
+    if links is not None:
+        # per (wall id, pulled component j): the link of direction d = ī_j (the population that left x towards the
+        # wall cell x + c_d = x − c_j comes back as j)
+        inv0 = [stencil.inverse_direction_index(i) for i in range(Q)]
+        qual = '__constant__ T' if hip else 'static const T'
+        for nm, col in (('lk_a', 0), ('lk_b', 1), ('lk_g', 2)):
+            vals = [repr(float(links[k][inv0[j]][col])) for k in range(len(links)) for j in range(Q)]
+            L.append(f'{qual} {nm}[{len(vals)}] = {{{", ".join(vals)}}};')
 
     def c_(v):
         return f'({ct}){_c(v)}'
@@ -135,19 +146,31 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
         return (f'__builtin_amdgcn_raw_buffer_store_{bits}(__builtin_bit_cast({ty}, (T)({val})), rs_{prefix}, '
                 f'{voff}, 0, 0);')
 
+    def ncell(k):
+        """C-order cell index of the neighbour ``x − c`` of pull key ``k`` (wrapped coordinates)."""
+        if D == 3:
+            return f'((IDX){coord(k, "z")} * Y + {coord(k, "y")}) * X + {coord(k, "x")}'
+        return f'(IDX){coord(k, "y")} * X + {coord(k, "x")}'
+
     def pull_loads(L, prefix, arr):
         for i in range(Q):
             k = key(dirs[i])
+            cq = '' if links is not None and walls and any(dirs[i]) else 'const '
             if walls and any(dirs[i]):
                 if buf:
                     # a bounced component is read from the cell itself: ONE load whose per-lane offset selects
                     # (component, cell) — not both loads and a select
                     L.append(f'  const unsigned vo{i} = ((msk >> {i}) & 1u) ? {prefix}o_{centre} + '
                              f'(unsigned)({inv[i]} * {prefix}_qb) : {prefix}o_{k} + (unsigned)({i} * {prefix}_qb);')
-                    L.append(f'  const {ct} f{i} = {load_v(prefix, f"vo{i}")};')
+                    L.append(f'  {cq}{ct} f{i} = {load_v(prefix, f"vo{i}")};')
                 else:
-                    L.append(f'  const {ct} f{i} = {arr}[(msk >> {i}) & 1u ? (IDX){inv[i]} * {prefix}_q + '
+                    L.append(f'  {cq}{ct} f{i} = {arr}[(msk >> {i}) & 1u ? (IDX){inv[i]} * {prefix}_q + '
                              f'{prefix}o_{centre} : (IDX){i} * {prefix}_q + {prefix}o_{k}];')
+                if links is not None:
+                    # the wall cell's link (moving wall: α = 1, β = 6 w (c·u)); its id is loaded on this path only
+                    L.append(f'  unsigned id{i} = 0;')
+                    L.append(f'  if ((msk >> {i}) & 1u) {{ id{i} = wallid[{ncell(k)}]; '
+                             f'f{i} = lk_a[id{i} * {Q} + {i}] * f{i} + lk_b[id{i} * {Q} + {i}]; }}')
             else:
                 L.append(f'  const {ct} f{i} = {load(prefix, arr, i, f"{prefix}o_{k}")};')
 
@@ -170,7 +193,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
         s_ = ' '.join(t)
         return s_[2:] if s_.startswith('+ ') else '(' + s_ + ')'
 
-    mask_param = 'const unsigned* __restrict__ nbmask'
+    mask_param = 'const unsigned* __restrict__ nbmask, const unsigned char* __restrict__ wallid'
     sig_fwd = (f'const T* __restrict__ src, T* __restrict__ dst, {mask_param}, const int Z, const int Y, const int X, '
                'const IDX s_q, const IDX s_z, const IDX s_y, const IDX s_x, '
                'const IDX d_q, const IDX d_z, const IDX d_y, const IDX d_x, '
@@ -185,7 +208,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
 
     # ---- forward
     L.append(f'{fn} void lbm_fwd_cell({sig_fwd}, const int z, const int y, const int x)\n{{')
-    L.append('  (void)Z; (void)s_bytes; (void)d_bytes;')
+    L.append('  (void)Z; (void)s_bytes; (void)d_bytes; (void)wallid;')
     rsrc(L, 's', 'src')
     rsrc(L, 'd', 'dst')
     wrap_lines(L)
@@ -211,7 +234,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
 
     # ---- adjoint (scatter to where the forward pulled from)
     L.append(f'{fn} void lbm_adj_cell({sig_adj}, const int z, const int y, const int x)\n{{')
-    L.append('  (void)Z; (void)s_bytes; (void)g_bytes; (void)o_bytes;')
+    L.append('  (void)Z; (void)s_bytes; (void)g_bytes; (void)o_bytes; (void)wallid;')
     rsrc(L, 's', 'src')
     rsrc(L, 'g', 'g')
     rsrc(L, 'o', 'out')
@@ -260,8 +283,11 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
         cbs = ' '.join(cb)
         cbs = (cbs[2:] if cbs.startswith('+ ') else cbs) if cb else f'({ct})0'
         du = f'(({cbs}) - Bu) * irho' if compressible else f'({cbs})'
-        L.append(f'  {{ const {ct} v = (({ct})1 - omega) * g{j} + omega * (A + {du});')
+        L.append(f'  {{ {"" if links is not None and walls and any(dirs[j]) else "const "}{ct} v = (({ct})1 - omega) '
+                 f'* g{j} + omega * (A + {du});')
         k = key(dirs[j])
+        if walls and any(dirs[j]) and links is not None:
+            L.append(f'    if ((msk >> {j}) & 1u) v *= lk_g[id{j} * {Q} + {j}];')
         if walls and any(dirs[j]):
             if buf:
                 L.append(f'    const unsigned vs = ((msk >> {j}) & 1u) ? oo_{centre} + (unsigned)({inv[j]} * o_qb) : '
@@ -275,9 +301,9 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
     L.append('}')
 
     # ---- entry points
-    args_f = 'src, dst, nbmask, Z, Y, X, s_q, s_z, s_y, s_x, d_q, d_z, d_y, d_x, s_bytes, d_bytes, omega'
-    args_a = ('src, g, out, nbmask, Z, Y, X, s_q, s_z, s_y, s_x, g_q, g_z, g_y, g_x, o_q, o_z, o_y, o_x, s_bytes, '
-              'g_bytes, o_bytes, omega')
+    args_f = 'src, dst, nbmask, wallid, Z, Y, X, s_q, s_z, s_y, s_x, d_q, d_z, d_y, d_x, s_bytes, d_bytes, omega'
+    args_a = ('src, g, out, nbmask, wallid, Z, Y, X, s_q, s_z, s_y, s_x, g_q, g_z, g_y, g_x, o_q, o_z, o_y, o_x, '
+              's_bytes, g_bytes, o_bytes, omega')
     if hip:
         # a block = 256 consecutive cells of the lattice in C order (rows of x), and consecutive blocks on one XCD
         # (bijective remap of the round-robin dispatch): a lattice row's x-shifted loads and the adjoint's
@@ -302,14 +328,15 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
             L.append(f'  const {ct} omega = ({ct})Dv[0];')
             if kind == 'f':
                 L.append('  const T* src = (const T*)P[0]; T* dst = (T*)P[1]; const unsigned* nbmask = '
-                         '(const unsigned*)P[2];')
+                         '(const unsigned*)P[2]; const unsigned char* wallid = (const unsigned char*)P[3];')
                 L.append('  const IDX s_q = S[0], s_z = S[1], s_y = S[2], s_x = S[3], d_q = S[4], d_z = S[5], '
                          'd_y = S[6], d_x = S[7];')
                 L.append('  const long long s_bytes = 0, d_bytes = 0;')
                 call = f'lbm_fwd_cell({args_f}, z, y, x);'
             else:
                 L.append('  const T* src = (const T*)P[0]; const T* g = (const T*)P[1]; T* out = (T*)P[2]; '
-                         'const unsigned* nbmask = (const unsigned*)P[3];')
+                         'const unsigned* nbmask = (const unsigned*)P[3]; '
+                         'const unsigned char* wallid = (const unsigned char*)P[4];')
                 L.append('  const IDX s_q = S[0], s_z = S[1], s_y = S[2], s_x = S[3], g_q = S[4], g_z = S[5], '
                          'g_y = S[6], g_x = S[7], o_q = S[8], o_z = S[9], o_y = S[10], o_x = S[11];')
                 L.append('  const long long s_bytes = 0, g_bytes = 0, o_bytes = 0;')
@@ -321,10 +348,10 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr'):
 
 
 def neighbour_mask(flags, stencil, xp):
-    """``uint32`` per cell: bit i set where ``x − c_i`` is an obstacle (periodic), bit ``SELF_BIT`` where ``x`` is
-    one (``flags``: obstacle flags over the domain, numpy or torch)."""
+    """``uint32`` per cell: bit i set where ``x − c_i`` is a wall cell (periodic), bit ``SELF_BIT`` where ``x`` is
+    one (``flags``: wall ids over the domain, 0 = fluid, numpy or torch)."""
     is_torch = xp.__name__ == 'torch'
-    f = flags.to(xp.int32) if is_torch else flags.astype(np.int64)
+    f = (flags != 0).to(xp.int32) if is_torch else (np.asarray(flags) != 0).astype(np.int64)
     m = f * 0
     for i, c in enumerate(stencil.directions):
         if not any(c):
@@ -358,10 +385,12 @@ def row_interleaved_empty(domain, Q, dtype, device):
 
 
 class LatticeKernels:
-    """Compiled forward / adjoint lattice kernels of one (stencil, compressible, dtype, walls, target). ``mask``
-    arguments are the cells' neighbour masks (``neighbour_mask``), ``None`` without walls."""
+    """Compiled forward / adjoint lattice kernels of one (stencil, compressible, dtype, walls, links, target).
+    ``mask`` arguments are the cells' neighbour masks (``neighbour_mask``), ``None`` without walls; ``ids`` the
+    cells' wall ids (the ``uint8`` flag array, C order) when ``links`` is given (walls other than plain
+    bounce-back)."""
 
-    def __init__(self, stencil, compressible, dtype, walls, target):
+    def __init__(self, stencil, compressible, dtype, walls, target, links=None):
         self.stencil = stencil
         self.compressible = bool(compressible)
         self.dtype = np.dtype(dtype)
@@ -369,14 +398,15 @@ class LatticeKernels:
             raise NotImplementedError(f'lattice kernels for {self.dtype} pdfs')
         self.ct = 'double' if self.dtype == np.float64 else 'float'
         self.walls = bool(walls)
+        self.links = links if walls else None
         self.target = target
         self._fns = {}
         self._plans = {}
 
     def source(self, idx='int', addr='buf'):
         if self.target != 'gpu':
-            return _emit(self.stencil, self.compressible, self.ct, self.walls, 'c', 'i64', 'ptr')
-        return _emit(self.stencil, self.compressible, self.ct, self.walls, 'hip', idx, addr)
+            return _emit(self.stencil, self.compressible, self.ct, self.walls, 'c', 'i64', 'ptr', self.links)
+        return _emit(self.stencil, self.compressible, self.ct, self.walls, 'hip', idx, addr, self.links)
 
     # -- GPU ---------------------------------------------------------------------------------------
     def _gpu_fn(self, which, idx, addr, device):
@@ -394,7 +424,7 @@ class LatticeKernels:
             return [rt.compile_hip(self.source('int', a), name='psad_lbm.hip') for a in ('buf', 'ptr')]
         return self._cpu_fn('fwd')
 
-    def _check(self, tensors, mask):
+    def _check(self, tensors, mask, ids=None):
         D, Q = self.stencil.D, self.stencil.Q
         shape = tuple(tensors[0].shape)
         for t in tensors:
@@ -409,6 +439,11 @@ class LatticeKernels:
             raise ValueError(f'neighbour mask of shape {tuple(mask.shape)} does not match the domain {shape[:D]}')
         if min(shape[:D]) < 2:
             raise ValueError('the periodic lattice needs at least 2 cells per axis')
+        if (self.links is not None) != (ids is not None):
+            raise ValueError('kernels with boundary links need the wall ids (and the others none)')
+        if ids is not None and (tuple(ids.shape) != shape[:D] or not ids.is_contiguous() or ids.dtype.itemsize != 1
+                                or ids.device != tensors[0].device):
+            raise ValueError(f'wall ids of shape {tuple(ids.shape)} do not match the domain {shape[:D]}')
 
     @staticmethod
     def _reach(t):
@@ -424,15 +459,15 @@ class LatticeKernels:
             addr = 'ptr'
         return idx, addr
 
-    def _common(self, tensors, mask):
-        self._check(tensors, mask)
+    def _common(self, tensors, mask, ids=None):
+        self._check(tensors, mask, ids)
         idx, addr = self._mode(tensors)
         fn_args = []
         for t in tensors:
             fn_args += list(lattice_strides(t, self.stencil.D))
         return idx, addr, fn_args
 
-    def plan(self, which, tensors, mask, omega):
+    def plan(self, which, tensors, mask, omega, ids=None):
         """The launch of ``which`` ('fwd' / 'adj') on tensors of these shapes, strides, dtype and device (with or
         without walls): a ``LaunchPlan`` whose pointer slots and relaxation rate are patched per launch — the
         time-step op launches T of them per apply. ω is not part of the key (a trained or scheduled rate reuses the
@@ -442,34 +477,36 @@ class LatticeKernels:
         plan = self._plans.get(key)
         if plan is not None:
             return plan
-        idx, addr, strides = self._common(tensors, mask)
+        idx, addr, strides = self._common(tensors, mask, ids)
         dev = tensors[0].device.index
         fn = self._gpu_fn(which, idx, addr, dev)
         Z, Y, X = self._extent(tensors[0])
         code = 'i' if idx == 'int' else 'q'
         nblocks = self._blocks(X, Y, Z)
         reach = [self._reach(t) * t.element_size() for t in tensors]
-        ptrs = [t.data_ptr() for t in tensors] + [mask.data_ptr() if mask is not None else 0]
+        ptrs = [t.data_ptr() for t in tensors] + [mask.data_ptr() if mask is not None else 0,
+                                                  ids.data_ptr() if ids is not None else 0]
         fmt = 'Q' * len(ptrs) + 'iii' + code * (4 * len(tensors)) + 'q' * len(tensors) + \
             ('d' if self.ct == 'double' else 'f')
         args = _pack(fmt, *ptrs, Z, Y, X, *strides, *reach, float(omega))
         plan = self._plans[key] = LaunchPlan(fn, nblocks, args, len(ptrs), dev, _offset(fmt, len(fmt) - 1), fmt[-1])
         return plan
 
-    def forward(self, src, dst, omega, mask=None, stream=None):
+    def forward(self, src, dst, omega, mask=None, stream=None, ids=None):
         """``dst = stream-pull-collide(src)`` (torch tensors ``[*domain, q]``, any strides)."""
         if self.target != 'gpu':
-            return self._cpu('fwd', [src, dst], omega, mask)
-        self.plan('fwd', [src, dst], mask, omega)(
-            (src.data_ptr(), dst.data_ptr(), mask.data_ptr() if mask is not None else 0), _stream(stream, src), omega)
+            return self._cpu('fwd', [src, dst], omega, mask, ids)
+        self.plan('fwd', [src, dst], mask, omega, ids)(
+            (src.data_ptr(), dst.data_ptr(), mask.data_ptr() if mask is not None else 0,
+             ids.data_ptr() if ids is not None else 0), _stream(stream, src), omega)
 
-    def adjoint(self, src, g, out, omega, mask=None, stream=None):
+    def adjoint(self, src, g, out, omega, mask=None, stream=None, ids=None):
         """``out = (∂ step / ∂ src)ᵀ g`` at the state ``src``."""
         if self.target != 'gpu':
-            return self._cpu('adj', [src, g, out], omega, mask)
-        self.plan('adj', [src, g, out], mask, omega)(
-            (src.data_ptr(), g.data_ptr(), out.data_ptr(), mask.data_ptr() if mask is not None else 0),
-            _stream(stream, src), omega)
+            return self._cpu('adj', [src, g, out], omega, mask, ids)
+        self.plan('adj', [src, g, out], mask, omega, ids)(
+            (src.data_ptr(), g.data_ptr(), out.data_ptr(), mask.data_ptr() if mask is not None else 0,
+             ids.data_ptr() if ids is not None else 0), _stream(stream, src), omega)
 
     def _extent(self, t):
         shape = [int(n) for n in t.shape[:self.stencil.D]]
@@ -490,7 +527,7 @@ class LatticeKernels:
             fn = self._fns[which] = compile_c(self.source(), f'lbm_{which}', openmp=True)
         return fn
 
-    def _cpu(self, which, arrays, omega, mask):
+    def _cpu(self, which, arrays, omega, mask, ids=None):
         arrays = [np.asarray(a) for a in arrays]
         for a in arrays:
             if a.dtype != self.dtype:
@@ -507,8 +544,16 @@ class LatticeKernels:
             m = np.ascontiguousarray(mask, dtype=np.uint32)
             if m.shape != shape[:D]:
                 raise ValueError('neighbour mask does not match the domain')
+        if (self.links is not None) != (ids is not None):
+            raise ValueError('kernels with boundary links need the wall ids (and the others none)')
+        idv = None
+        if ids is not None:
+            idv = np.ascontiguousarray(ids, dtype=np.uint8)
+            if idv.shape != shape[:D]:
+                raise ValueError('wall ids do not match the domain')
         fn = self._cpu_fn(which)
-        ptrs = [a.ctypes.data for a in arrays] + [m.ctypes.data if m is not None else 0]
+        ptrs = [a.ctypes.data for a in arrays] + [m.ctypes.data if m is not None else 0,
+                                                  idv.ctypes.data if idv is not None else 0]
         strides = []
         for a in arrays:
             strides += list(lattice_strides(a, D))

@@ -1,17 +1,38 @@
-"""No-slip walls for ``AutoDiffLatticeBoltzmannStep`` and their adjoints (reference
-``/root/reference/src/pystencils_autodiff/lbm/adjoint_boundaryconditions.py:7-72``, lbmpy's ``NoSlip`` [ext]).
+"""Walls for ``AutoDiffLatticeBoltzmannStep`` and their adjoints (reference
+``/root/reference/src/pystencils_autodiff/lbm/adjoint_boundaryconditions.py:7-72``, lbmpy's ``NoSlip`` / ``UBB``
+[ext]).
 
-lbmpy describes a boundary by an object that prints assignments for lbmpy's boundary-handling kernels over
-index lists of boundary links, and the reference derives the adjoint object from it
-(``AdjointBoundaryCondition``: TF-MAD of the forward boundary's assignments) or spells it out
-(``AdjointNoSlip``: ``pdf(dir) = pdf[neighbour](inv_dir)``, the forward copy transposed). Here the boundary
-objects name the condition and the cells it covers are a flag array; the lattice kernels
-(``_lattice_kernels``) fuse the half-way bounce-back into the pull and its transpose into the adjoint scatter,
-so there is no separate boundary kernel, no index list and no sync step. Only no-slip is built.
+lbmpy describes a boundary by an object whose ``__call__(pdf_field, direction, lb_method)`` prints the assignment
+of one boundary LINK — from the fluid cell ``x`` in direction ``d`` into the wall cell ``x + c_d`` — for lbmpy's
+boundary kernels, which run over index lists before the streaming step writes the wall cell's incoming population:
+
+    NoSlip:  pdf[c_d](ī_d) ← pdf(d)                                 (half-way bounce-back)
+    UBB:     pdf[c_d](ī_d) ← pdf(d) − 6 w_d (c_d · u_wall)           (velocity bounce-back, 2/c_s² = 6)
+
+and the reference derives the adjoint object from it (``AdjointBoundaryCondition``: the backward assignments of the
+forward link, ``adjoint_boundaryconditions.py:24-37``) or spells one out (``AdjointNoSlip``: ``pdf(d) ←
+pdf[c_d](ī_d)``, the forward copy transposed, ``:49-72``).
+
+Here the boundary objects print the same link assignments in this package's ``ps`` front-end, and the lattice
+kernels (``_lattice_kernels``) fuse every link of the form ``f_in = α·f_out + β`` (α, β constants per object and
+direction) into the pull — ``f_j(x) = α·src_ī(x) + β`` where ``x − c_j`` is a wall cell — and the adjoint link into
+the adjoint scatter. ``link_coefficients`` reads (α, β) off the forward assignment and the adjoint coefficient off
+the adjoint object's assignment, so any boundary object of that form works (``NoSlip``, ``UBB``, user subclasses
+of ``Boundary``). ``AdjointBoundaryCondition`` derives the adjoint link with the transposed-mode AD of this package
+(``DiffModes.TRANSPOSED``): the reference's TF-MAD call reads the adjoint of an offset write at the mirrored offset and
+at component 0 (``_autodiff.py:120-151``, the quirk its own ``AdjointNoSlip`` docstring calls "bug-safe" to avoid),
+which is not the gradient; the transposed form is what ``AdjointNoSlip`` spells out, for any affine link. The cells
+a boundary covers are a flag array (one id per boundary object): no index list, no separate boundary kernel.
+
+UBB: lbmpy multiplies the velocity term by the fluid cell's density for one of its two method families (the
+``compressible`` branch differs between lbmpy versions); the density-free form above is the one built — its link is
+affine in one pdf, so it fuses. A density-weighted variant is not affine and raises.
 """
 import numpy as np
+import sympy as sp
 
-__all__ = ['NoSlip', 'AdjointNoSlip', 'AdjointBoundaryCondition', 'BoundaryHandling', 'make_slice']
+__all__ = ['Boundary', 'NoSlip', 'UBB', 'AdjointNoSlip', 'AdjointBoundaryCondition', 'BoundaryHandling',
+           'make_slice', 'link_coefficients']
 
 
 class _MakeSlice:
@@ -24,82 +45,240 @@ class _MakeSlice:
 make_slice = _MakeSlice()
 
 
-class NoSlip:
-    """Half-way simple bounce-back at obstacle cells (lbmpy ``NoSlip`` [ext]): zero velocity at the wall."""
+def _directions(lb_method):
+    st = getattr(lb_method, 'stencil', lb_method)
+    return st
+
+
+class Boundary:
+    """lbmpy's boundary surface (``lbmpy.boundaries.boundaryconditions.Boundary`` [ext]): a name, equality by
+    name, and ``__call__(pdf_field, direction, lb_method)`` → the link assignment(s) for direction index
+    ``direction`` (lbmpy passes a direction symbol evaluated over index lists; the lattice kernels here are printed
+    per direction, so it is a concrete index)."""
 
     def __init__(self, name=None):
-        self.name = name or 'NoSlip'
+        self._name = name
+
+    @property
+    def name(self):
+        return self._name if self._name is not None else type(self).__name__
+
+    def __call__(self, pdf_field, direction, lb_method, **kwargs):
+        raise NotImplementedError
 
     def __hash__(self):
-        return hash(self.name)
+        return hash((type(self).__name__, self.name))
 
     def __eq__(self, other):
-        return isinstance(other, NoSlip) and self.name == other.name
+        return type(other) is type(self) and self.name == other.name
 
     def __repr__(self):
-        return f'NoSlip({self.name!r})'
+        return f'{type(self).__name__}({self.name!r})'
 
 
-class AdjointNoSlip:
-    """The adjoint of ``NoSlip`` (``adjoint_boundaryconditions.py:49-72``): applied by the adjoint kernel."""
+class NoSlip(Boundary):
+    """Half-way simple bounce-back (lbmpy ``NoSlip`` [ext]): zero velocity at the wall."""
 
     def __init__(self, name=None):
-        self.name = name or 'AdjointNoSlip'
+        super().__init__(name if name is not None else 'NoSlip')
+
+    def __call__(self, pdf_field, direction, lb_method, **kwargs):
+        st = _directions(lb_method)
+        c = st.directions[direction]
+        from .. import ps
+        return [ps.Assignment(pdf_field[c](st.inverse_direction_index(direction)), pdf_field(direction))]
+
+
+class UBB(Boundary):
+    """Velocity bounce-back (lbmpy ``UBB`` [ext]): a wall moving with ``velocity`` (one component per spatial axis,
+    axis 0 first), e.g. the lid of a lid-driven cavity: ``pdf[c_d](ī_d) ← pdf(d) − 6 w_d (c_d · u)``."""
+
+    def __init__(self, velocity, name=None):
+        super().__init__(name if name is not None else 'UBB')
+        self.velocity = tuple(velocity)
+
+    def __call__(self, pdf_field, direction, lb_method, **kwargs):
+        st = _directions(lb_method)
+        c = st.directions[direction]
+        if len(self.velocity) != len(c):
+            raise ValueError(f'UBB velocity {self.velocity} has not one component per axis of {st.name}')
+        vel_term = 6 * st.weights[direction] * sum(ci * sp.sympify(ui) for ci, ui in zip(c, self.velocity) if ci)
+        from .. import ps
+        return [ps.Assignment(pdf_field[c](st.inverse_direction_index(direction)), pdf_field(direction) - vel_term)]
 
     def __hash__(self):
-        return hash(self.name)
+        return hash(('UBB', self.name, self.velocity))
 
     def __eq__(self, other):
-        return isinstance(other, AdjointNoSlip) and self.name == other.name
+        return isinstance(other, UBB) and self.name == other.name and self.velocity == other.velocity
+
+    def __repr__(self):
+        return f'UBB({self.velocity!r}, {self.name!r})'
 
 
-class AdjointBoundaryCondition:
-    """The adjoint of a forward boundary condition (``adjoint_boundaryconditions.py:7-46``). Built for
-    ``NoSlip`` only (its transpose is fused into the adjoint lattice kernel)."""
+class AdjointNoSlip(Boundary):
+    """The adjoint of ``NoSlip`` spelled out (``adjoint_boundaryconditions.py:49-72``):
+    ``pdf(d) ← pdf[c_d](ī_d)``, the forward copy transposed."""
+
+    def __init__(self, name=None):
+        super().__init__(name if name is not None else 'AdjointNoSlip')
+
+    def __call__(self, pdf_field, direction, lb_method, **kwargs):
+        st = _directions(lb_method)
+        c = st.directions[direction]
+        from .. import ps
+        return [ps.Assignment(pdf_field(direction), pdf_field[c](st.inverse_direction_index(direction)))]
+
+
+class AdjointBoundaryCondition(Boundary):
+    """The adjoint of a forward boundary condition (``adjoint_boundaryconditions.py:7-46``): the backward
+    assignments of the forward link (transposed-mode AD, see the module docstring), on the adjoint pdf field
+    (an ``AdjointField``, or a field named ``diff<name>`` like the reference's heuristic)."""
 
     def __init__(self, forward_boundary_condition, time_constant_fields=(), constant_fields=()):
-        if not isinstance(forward_boundary_condition, NoSlip):
-            raise NotImplementedError(f'adjoint of {forward_boundary_condition!r}: only NoSlip is built')
-        self.name = 'Adjoint' + forward_boundary_condition.name
+        if not isinstance(forward_boundary_condition, Boundary) or \
+                isinstance(forward_boundary_condition, (AdjointBoundaryCondition, AdjointNoSlip)):
+            raise NotImplementedError(f'adjoint of {forward_boundary_condition!r}: needs a forward Boundary')
+        super().__init__('Adjoint' + forward_boundary_condition.name)
         self._forward_condition = forward_boundary_condition
         self._time_constant_fields = list(time_constant_fields or [])
         self._constant_fields = list(constant_fields or [])
 
+    @property
+    def forward_condition(self):
+        return self._forward_condition
+
+    def __call__(self, pdf_field, direction, lb_method, **kwargs):
+        from .. import ps
+        from .._adjoint_field import AdjointField
+        from ..autodiff import DiffModes, create_backward_assignments
+        if not isinstance(pdf_field, AdjointField) and pdf_field.name.startswith('diff'):
+            forward_field = pdf_field.new_field_with_different_name(pdf_field.name[len('diff'):])
+            pdf_field = AdjointField(forward_field)
+        if not isinstance(pdf_field, AdjointField):
+            raise TypeError(f'{pdf_field} should be an AdjointField to use AdjointBoundaryCondition')
+        forward_field = pdf_field.corresponding_forward_field
+        fwd = self._forward_condition(forward_field, direction, lb_method, **kwargs)
+        bwd = create_backward_assignments(ps.AssignmentCollection(list(fwd)), diff_fields_prefix=pdf_field.name_prefix,
+                                          time_constant_fields=self._time_constant_fields,
+                                          constant_fields=self._constant_fields, diff_mode=DiffModes.TRANSPOSED)
+        assert bwd.all_assignments, ('Must have a at least one read field in forward boundary to have an meaningful '
+                                     'adjoint boundary condition')
+        return bwd
+
     def __hash__(self):
-        return hash(self.name)
+        return hash(('Adjoint', hash(self._forward_condition)))
 
     def __eq__(self, other):
         return isinstance(other, AdjointBoundaryCondition) and self._forward_condition == other._forward_condition
 
 
+def _affine(expr, var):
+    """(α, β) with ``expr = α·var + β`` (numbers), else None."""
+    expr = sp.expand(sp.sympify(expr))
+    a = sp.diff(expr, var)
+    b = sp.expand(expr - a * var)
+    if a.free_symbols or b.free_symbols:
+        return None
+    return float(a), float(b)
+
+
+def link_coefficients(forward_bc, adjoint_bc, lb_method):
+    """Per direction ``d`` of ``lb_method``'s stencil: ``(α, β, γ)`` with the forward link
+    ``f_{ī_d}(x + c_d) = α·f_d(x) + β`` and the adjoint link ``g_d(x) = γ·g_{ī_d}(x + c_d)`` — the form the lattice
+    kernels fuse. Raises ``NotImplementedError`` for a boundary of another form."""
+    from .. import ps
+    from .._adjoint_field import AdjointField
+    st = _directions(lb_method)
+    f = ps.fields(f'__pdf({st.Q}): [{st.D}D]')
+    g = AdjointField(f)
+    out = []
+    for d in range(st.Q):
+        c = st.directions[d]
+        if not any(c):
+            out.append((1.0, 0.0, 1.0))
+            continue
+        inv = st.inverse_direction_index(d)
+        fwd = list(forward_bc(f, d, lb_method))
+        if len(fwd) != 1 or fwd[0].lhs != f[c](inv):
+            raise NotImplementedError(f'{forward_bc!r}: the lattice kernels fuse one link assignment '
+                                      f'pdf[c_d](inv_d) <- alpha*pdf(d) + beta per direction, got {fwd}')
+        ab = _affine(fwd[0].rhs, f(d))
+        if ab is None:
+            raise NotImplementedError(f'{forward_bc!r}: link {fwd[0]} is not affine in pdf(d) with constant '
+                                      'coefficients (e.g. a density-weighted velocity term)')
+        bwd = adjoint_bc(g, d, lb_method)
+        mains = list(getattr(bwd, 'main_assignments', bwd))
+        if len(mains) != 1 or mains[0].lhs != g(d):
+            raise NotImplementedError(f'{adjoint_bc!r}: expected one adjoint link diffpdf(d) <- gamma * '
+                                      f'diffpdf[c_d](inv_d), got {mains}')
+        rhs = mains[0].rhs
+        subs = getattr(bwd, 'subexpressions', [])
+        for s in reversed(list(subs)):
+            rhs = rhs.subs(s.lhs, s.rhs)
+        gb = _affine(rhs, g[c](inv))
+        if gb is None or gb[1] != 0:
+            raise NotImplementedError(f'{adjoint_bc!r}: adjoint link {mains[0]} is not linear in diffpdf[c_d](inv_d)')
+        out.append((ab[0], ab[1], gb[0]))
+    return tuple(out)
+
+
 class BoundaryHandling:
-    """The obstacle flags of one lattice (``uint8``, one per cell, 1 = no-slip obstacle) and lbmpy's
-    ``set_boundary`` surface over them. The forward and the adjoint kernels read the same flags, so the
-    forward handling and the ``backward_boundary_handling`` of the step are this one object."""
+    """The wall flags of one lattice (``uint8``, one per cell: 0 = fluid, k ≥ 1 = the k-th boundary object set)
+    and lbmpy's ``set_boundary`` surface over them. The forward and the adjoint kernels read the same flags, so the
+    forward handling and the ``backward_boundary_handling`` of the step are this one object; each boundary object
+    keeps the adjoint condition it was set with."""
 
     def __init__(self, domain_size, on_change=None):
         self.domain_size = tuple(int(n) for n in domain_size)
         self.flags = np.zeros(self.domain_size, np.uint8)
         self._on_change = on_change
-        self.conditions = {}
+        self.conditions = {}            # forward boundary object -> flag id
+        self.adjoints = {}              # flag id -> adjoint boundary object
         self._has_walls = False
 
     @property
     def has_walls(self):
-        """Any obstacle cell (kept up to date by ``set_boundary``: the kernels ask once per launch)."""
+        """Any wall cell (kept up to date by ``set_boundary``: the kernels ask once per launch)."""
         return self._has_walls
 
-    def set_boundary(self, boundary_obj, slice_obj=None, mask_callback=None, mask_array=None, **_):
-        """Mark cells as ``boundary_obj`` (``NoSlip``; ``AdjointNoSlip`` / ``AdjointBoundaryCondition(NoSlip)``
-        or ``'domain'`` to clear them): the cells of ``slice_obj`` (domain coordinates, default all), narrowed
-        by ``mask_callback(*midpoints)`` (cell-midpoint coordinate arrays of the region, axis 0 first) or a
-        boolean ``mask_array`` (the region's or the domain's shape)."""
+    def objects(self):
+        """Forward boundary objects by flag id (index 0: fluid, None)."""
+        out = [None] * (max(self.conditions.values(), default=0) + 1)
+        for obj, k in self.conditions.items():
+            out[k] = obj
+        return out
+
+    def flag_id(self, boundary_obj, adjoint=None):
+        """The flag id of ``boundary_obj`` (allocated on first use; adjoints count as their forward condition)."""
+        if isinstance(boundary_obj, AdjointBoundaryCondition):
+            boundary_obj = boundary_obj.forward_condition
+        elif isinstance(boundary_obj, AdjointNoSlip):
+            boundary_obj = NoSlip()
+        k = self.conditions.get(boundary_obj)
+        if k is None:
+            k = len(self.conditions) + 1
+            if k > 255:
+                raise ValueError('more than 255 boundary objects on one lattice')
+            self.conditions[boundary_obj] = k
+        if adjoint is not None:
+            self.adjoints[k] = adjoint
+        elif k not in self.adjoints:
+            self.adjoints[k] = AdjointNoSlip() if isinstance(boundary_obj, NoSlip) else \
+                AdjointBoundaryCondition(boundary_obj)
+        return k
+
+    def set_boundary(self, boundary_obj, slice_obj=None, mask_callback=None, mask_array=None, adjoint=None, **_):
+        """Mark cells as ``boundary_obj`` (a ``Boundary``; its adjoint object, or ``'domain'`` to clear them): the
+        cells of ``slice_obj`` (domain coordinates, default all), narrowed by ``mask_callback(*midpoints)``
+        (cell-midpoint coordinate arrays of the region, axis 0 first) or a boolean ``mask_array`` (the region's or
+        the domain's shape)."""
         if boundary_obj == 'domain':
             value = 0
-        elif isinstance(boundary_obj, (NoSlip, AdjointNoSlip, AdjointBoundaryCondition)):
-            value = 1
+        elif isinstance(boundary_obj, Boundary):
+            value = self.flag_id(boundary_obj, adjoint)
         else:
-            raise NotImplementedError(f'boundary {boundary_obj!r}: only NoSlip walls are built')
+            raise NotImplementedError(f'boundary {boundary_obj!r}: not a Boundary object')
         if slice_obj is None:
             slice_obj = tuple(slice(None) for _ in self.domain_size)
         elif not isinstance(slice_obj, tuple):
@@ -121,7 +300,22 @@ class BoundaryHandling:
         sub = np.where(mask.reshape(sub.shape), np.uint8(value), sub)
         self.flags[slice_obj] = sub
         self._has_walls = bool(self.flags.any())
-        if value:
-            self.conditions[boundary_obj] = True
         if self._on_change is not None:
             self._on_change()
+
+    def link_tables(self, lb_method):
+        """Per flag id ≥ 1: the ``link_coefficients`` of its (forward, adjoint) boundary pair, as a tuple, or None
+        when every id is a plain bounce-back (α = γ = 1, β = 0: the kernels' fast path, no id loads)."""
+        objs = self.objects()
+        tables = [None]
+        plain = True
+        for k in range(1, len(objs)):
+            obj = objs[k]
+            t = link_coefficients(obj, self.adjoints[k], lb_method)
+            plain &= all(a == 1.0 and b == 0.0 and g == 1.0 for a, b, g in t)
+            tables.append(t)
+        if plain:
+            return None
+        st = _directions(lb_method)
+        tables[0] = tuple((1.0, 0.0, 1.0) for _ in range(st.Q))
+        return tuple(tables)

@@ -207,6 +207,18 @@ class Field:
             tuple(strides) != _c_strides(shape)
         return f
 
+    def new_field_with_different_name(self, new_name):
+        """The same field (type, dtype, layout, shape, strides) under another name (pystencils' method of the same
+        name [ext]; symbolic shape / stride symbols are renamed with it)."""
+        shape = tuple(FieldShapeSymbol([new_name], s.coordinate) if isinstance(s, FieldShapeSymbol) else s
+                      for s in self.shape)
+        strides = tuple(FieldStrideSymbol(new_name, s.coordinate) if isinstance(s, FieldStrideSymbol) else s
+                        for s in self.strides)
+        f = Field(new_name, self.field_type, self.dtype, self._layout, shape, strides)
+        f._index_dimensions = self._index_dimensions
+        f._soa = self._soa
+        return f
+
     # -- properties -----------------------------------------------------------------------------
     @property
     def name(self):

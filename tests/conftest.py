@@ -51,3 +51,76 @@ def assert_close_rel(actual, expected, rtol, what=''):
     scale = max(float(np.max(np.abs(expected))) if expected.size else 0.0, 1e-30)
     err = float(np.max(np.abs(actual - expected))) if expected.size else 0.0
     assert err <= rtol * scale, f"{what}: max abs err {err:.3e} > {rtol:.1e} * {scale:.3e}"
+
+
+F32_EPS = 2.0 ** -24           # unit roundoff of fp32 (round to nearest)
+
+
+def fp16_ulp(x):
+    """Spacing of fp16 at |x| (subnormal spacing 2^-24 near zero)."""
+    return np.spacing(np.abs(np.asarray(x, dtype=np.float64)).astype(np.float16)).astype(np.float64)
+
+
+def assert_cells(actual, ref, absterms, nterms, storage, what='', rtol=1e-6, slack=4.0):
+    """Element-wise parity of one output against the float64 oracle, cell by cell:
+
+        |gpu − ref| ≤ rtol·|ref| + (nterms + 2)·2⁻²⁴·slack·Σ|terms|   [+ ½ ulp₁₆(|ref| + that) for fp16 storage]
+
+    ``rtol`` is the north star's 1e-6 relative; the second term is the fp32 arithmetic of the kernel (a sum of
+    ``nterms`` products with fp32-rounded weights, standard forward-error bound γₙ·Σ|terms|, ``slack`` for the
+    unfolded intermediates a kernel may form); fp16 storage adds the final rounding of the fp32 result to fp16
+    — i.e. the stored value is within half an fp16 ulp of the fp32 result, which is within the accumulation
+    bound of the exact one. ``absterms`` = Σ|w·u| per cell (the same stencil with |w| on |u|)."""
+    actual = np.asarray(actual, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    absterms = np.asarray(absterms, dtype=np.float64)
+    assert actual.shape == ref.shape == absterms.shape, f'{what}: shapes {actual.shape} {ref.shape} {absterms.shape}'
+    acc = (nterms + 2) * F32_EPS * slack * absterms
+    bound = rtol * np.abs(ref) + acc
+    if np.dtype(storage) == np.float16:
+        bound = bound + 0.5 * fp16_ulp(np.abs(ref) + acc)
+    err = np.abs(actual - ref)
+    bad = err > bound
+    if bad.any():
+        i = np.unravel_index(int(np.argmax(np.where(bad, err / np.maximum(bound, 1e-300), 0))), err.shape)
+        raise AssertionError(f'{what}: {int(bad.sum())} of {bad.size} cells outside the element-wise bound; worst at '
+                             f'{i}: gpu {actual[i]!r} ref {ref[i]!r} err {err[i]:.3e} bound {bound[i]:.3e} '
+                             f'(Σ|terms| {absterms[i]:.3e})')
+
+
+def abs_linear(collection):
+    """The collection with every main assignment's right-hand side (subexpressions substituted) replaced by
+    Σ|c|·access over its linear expansion — evaluated on |inputs| it gives Σ|terms| per cell. None if a right-hand
+    side is not linear in the field accesses with numeric coefficients."""
+    import sympy as sp
+
+    from pystencils_autodiff_amd import ps
+    flat = collection.new_without_subexpressions()
+    mains = []
+    for a in flat.main_assignments:
+        rhs = sp.expand(a.rhs)
+        terms = sp.Add.make_args(rhs)
+        new = 0
+        for t in terms:
+            c, rest = t.as_coeff_Mul()
+            if not isinstance(rest, ps.Field.Access) or not c.is_number:
+                return None
+            new += abs(float(c)) * rest
+        mains.append(ps.Assignment(a.lhs, new))
+    return ps.AssignmentCollection(mains)
+
+
+def abs_terms(collection, inputs, boundary_handling='zeros'):
+    """{output name: Σ|terms| per cell} for a linear collection on ``inputs`` ({name: array})."""
+    from oracle import evaluate as OE
+    ac = abs_linear(collection)
+    assert ac is not None, 'abs_terms needs a linear stencil'
+    return OE.evaluate(ac, {n: np.abs(np.asarray(a, dtype=np.float64)) for n, a in inputs.items()},
+                       boundary_handling=boundary_handling)
+
+
+def n_terms(collection):
+    """Most terms in one main assignment's linear expansion (the products the kernel sums per cell)."""
+    ac = abs_linear(collection)
+    import sympy as sp
+    return max(len(sp.Add.make_args(a.rhs)) for a in ac.main_assignments)

@@ -17,7 +17,7 @@ from pystencils_autodiff_amd import workloads as W
 from pystencils_autodiff_amd.backends.hip_band import band_choice, band_geometry, band_plans
 from pystencils_autodiff_amd.backends.hip_kernel import HipStencilKernel, default_march_config
 from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
-from tests.conftest import assert_close_rel
+from tests.conftest import abs_terms, assert_cells, assert_close_rel, n_terms
 
 TOL16 = 1e-3
 
@@ -123,9 +123,11 @@ def test_band_vs_oracle(case, shape, bh):
         assert k.last_variant[0] == 'march' and cfg.BAND > 0, cfg
         whole = bh == 'zeros' and shape[1] % cfg.BTY == 0
         assert cfg.BMASK == (not whole), cfg
+        absr = abs_terms(ac, ins, bh)
         for n, t in outs.items():
             assert_close_rel(t.double().cpu().numpy(), ref[n], TOL16 if dt.itemsize == 2 else 1e-6,
                              f'{case[0]} {which} {n} {shape} {bh}')
+            assert_cells(t.double().cpu().numpy(), ref[n], absr[n], n_terms(ac), dt, f'{case[0]} {which} {n} {shape} {bh}')
 
 
 @pytest.mark.gpu

@@ -4,6 +4,8 @@ Tolerances (north_star: 1e-6 relative for fp32):
   fp32: |gpu - ref| <= 1e-6 * max|ref|, ref = float64 evaluation of the same inputs
   fp64: 1e-12 relative
   fp16 storage (27-point): output rounded to fp16 -> 1e-3 relative (no fp16 path in the reference)
+  element-wise (``assert_cells``, the golden linear stencils, the 512³ C-oracle run and the full-size sampled planes):
+  |gpu - ref| <= 1e-6·|ref| + (n+2)·2^-24·4·Σ|terms| per cell, + half an fp16 ulp for fp16 storage
 """
 import itertools
 
@@ -16,7 +18,7 @@ from oracle import evaluate as OE
 from oracle import stencils as S
 from pystencils_autodiff_amd import ps
 from pystencils_autodiff_amd import workloads as W
-from tests.conftest import assert_close_rel, golden
+from tests.conftest import abs_terms, assert_cells, assert_close_rel, golden, n_terms
 
 pytestmark = pytest.mark.gpu
 
@@ -53,6 +55,12 @@ def test_golden_linear_stencils(case, builder, bh):
     tol = TOL[g['u'].dtype.type]
     assert_close_rel(out, g['out'], tol, f'{case} forward')
     assert_close_rel(du, g['diffu'], tol, f'{case} adjoint')
+    # and cell by cell: 1e-6 relative + the fp32 arithmetic bound (+ half an fp16 ulp for fp16 storage)
+    st = g['u'].dtype
+    assert_cells(out, g['out'], abs_terms(op.forward_assignments, {'u': g['u']}, bh)['out'],
+                 n_terms(op.forward_assignments), st, f'{case} forward cells')
+    assert_cells(du, g['diffu'], abs_terms(op.backward_assignments, {'diffout': g['diffout']}, bh)['diffu'],
+                 n_terms(op.backward_assignments), st, f'{case} adjoint cells')
     k = op.forward_ast_gpu.compile()
     assert k.last_variant[0] == 'march'
 
@@ -260,6 +268,13 @@ def test_diffusion_512_vs_c_oracle():
     # fp32 C reference vs fp32 GPU: both round; compare at 2 ulp of the field scale
     assert_close_rel(out.detach().cpu().numpy(), ref_out, 1e-6, 'out 512^3')
     assert_close_rel(uc.grad.cpu().numpy(), ref_du, 1e-6, 'diffu 512^3')
+    # cell by cell: each side within the fp32 arithmetic bound of the exact value, so within twice it of each other
+    taps = S.taps_diffusion_7pt()
+    absw = {o: abs(w) for o, w in taps.items()}
+    assert_cells(out.detach().cpu().numpy(), ref_out, S.linear_stencil(np.abs(u.numpy()), absw), 7, np.float32,
+                 'out 512^3 cells', slack=8.0)
+    assert_cells(uc.grad.cpu().numpy(), ref_du, S.linear_stencil(np.abs(d.numpy()), absw), 7, np.float32,
+                 'diffu 512^3 cells', slack=8.0)
 
 
 def test_vector_field_generic_schedule():
@@ -978,6 +993,13 @@ def test_full_size_properties(builder, n, tol):
         ref_g = S.linear_stencil(dd, S.flip(taps))[z - lo]
         assert_close_rel(out.detach()[z].cpu().numpy(), ref_o, tol, f'out plane {z}')
         assert_close_rel(u.grad[z].cpu().numpy(), ref_g, tol, f'diffu plane {z}')
+        # cell by cell (1e-6 relative + fp32 arithmetic bound; fp16 storage: + half an fp16 ulp)
+        absw = {o: abs(w) for o, w in taps.items()}
+        st = np.float16 if dt == torch.float16 else np.float32
+        assert_cells(out.detach()[z].cpu().numpy(), ref_o, S.linear_stencil(np.abs(uu), absw)[z - lo], len(taps), st,
+                     f'out plane {z} cells')
+        assert_cells(u.grad[z].cpu().numpy(), ref_g, S.linear_stencil(np.abs(dd), S.flip(absw))[z - lo], len(taps), st,
+                     f'diffu plane {z} cells')
     lhs = torch.sum(out.detach().double() * d.double()).item()
     rhs = torch.sum(u.detach().double() * u.grad.double()).item()
     assert abs(lhs - rhs) <= (1e-5 if dt == torch.float32 else 2e-3) * max(abs(lhs), 1.0), (lhs, rhs)

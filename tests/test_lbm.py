@@ -398,3 +398,122 @@ def test_lbm_end_to_end_op_gpu():
     (ux ** 2).sum().add(r_ref.sum()).backward()
     assert torch.allclose(rho.grad, rt.grad, rtol=0, atol=1e-10 * float(rt.grad.abs().max()))
     assert torch.allclose(vel.grad, vt.grad, rtol=0, atol=1e-10 * float(vt.grad.abs().max()))
+
+
+# --- moving walls (UBB) and the generic adjoint boundary (adjoint_boundaryconditions.py:7-46) -------------
+LID_U = 0.05
+
+
+def _cavity(shape):
+    """Lid-driven cavity: no-slip walls on both ends of axis 0 and the low end of axis 1, the lid (UBB moving along
+    axis 0) on the high end of axis 1. Returns (wall mask, wall velocity [*shape, 2])."""
+    wall = np.zeros(shape, bool)
+    wall[0, :] = wall[-1, :] = wall[:, 0] = wall[:, -1] = True
+    vel = np.zeros(shape + (2,))
+    vel[1:-1, -1, 0] = LID_U
+    return wall, vel
+
+
+def _set_cavity(step, shape, adjoint=None):
+    lid = lbm.UBB((LID_U, 0.0), name='lid')
+    step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[0, :])
+    step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[-1, :])
+    step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[:, 0])
+    step.set_boundary_including_adjoint(lid, lbm.make_slice[1:-1, -1], adjoint_boundary_condition=adjoint)
+    return lid
+
+
+def test_boundary_links_and_generic_adjoint():
+    """The link assignments of NoSlip / UBB (lbmpy's form), the adjoint derived from them, and the (α, β, γ) the
+    lattice kernels fuse; a density-weighted (non-affine) link is refused."""
+    import sympy as sp
+    from pystencils_autodiff_amd import AdjointField, ps
+    st = lbm.LBStencil('D2Q9')
+    f = ps.fields('f(9): [2D]')
+    ubb = lbm.UBB((0.1, -0.2))
+    (a,) = ubb(f, 6, st)                       # direction 6 = (1, 1): link into the wall at x + (1, 1), comes back as 7
+    assert a.lhs == f[1, 1](7)
+    assert sp.simplify(a.rhs - (f(6) - 6 * sp.Rational(1, 36) * (sp.Float(0.1) - sp.Float(0.2)))) == 0
+    adj = lbm.AdjointBoundaryCondition(ubb)(AdjointField(f), 6, st)
+    (b,) = adj.main_assignments
+    g = AdjointField(f)
+    assert b.lhs == g(6) and sp.simplify(b.rhs - g[1, 1](7)) == 0     # the transpose: diff f(6) <- diff f[1,1](7)
+    # the reference's heuristic: a field named diff<name> is the adjoint of <name>
+    assert lbm.AdjointBoundaryCondition(ubb)(ps.fields('difff(9): [2D]'), 6, st).main_assignments[0].lhs.field.name == \
+        'difff'
+    co = lbm.link_coefficients(ubb, lbm.AdjointBoundaryCondition(ubb), st)
+    for d, (al, be, ga) in enumerate(co):
+        c = st.directions[d]
+        assert al == 1.0 and ga == 1.0
+        assert be == pytest.approx(-6 * float(st.weights[d]) * (0.1 * c[0] - 0.2 * c[1]))
+    assert lbm.link_coefficients(lbm.NoSlip(), lbm.AdjointNoSlip(), st) == tuple((1.0, 0.0, 1.0) for _ in range(9))
+
+    class DensityUBB(lbm.Boundary):
+        def __call__(self, pdf_field, direction, lb_method, **kw):
+            c = st.directions[direction]
+            rho = sum(pdf_field(i) for i in range(9))
+            return [ps.Assignment(pdf_field[c](st.inverse_direction_index(direction)), pdf_field(direction) - 0.1 * rho)]
+    with pytest.raises(NotImplementedError):
+        lbm.link_coefficients(DensityUBB(), lbm.AdjointBoundaryCondition(DensityUBB()), st)
+    step = lbm.AutoDiffLatticeBoltzmannStep(lbm.create_lb_update_rule('D2Q9', compressible=True),
+                                            domain_size=(6, 5), relaxation_rate=1.0, target='cpu')
+    with pytest.raises(NotImplementedError):
+        step.set_boundary_including_adjoint(DensityUBB())
+
+
+@pytest.mark.parametrize('adjoint', ['derived', 'noslip'])
+@pytest.mark.parametrize('compressible', [True, False])
+def test_lbm_lid_driven_cavity_cpu(adjoint, compressible):
+    """D2Q9 lid-driven cavity (NoSlip walls + a UBB lid) on the C lattice kernels: T forward steps vs the array-roll
+    + moving-wall restatement (oracle/lbm.py), the adjoint of T steps vs torch's reverse mode through it — with the
+    default adjoint (AdjointBoundaryCondition(UBB), derived by AD) and an explicit AdjointNoSlip (the same
+    transposed link)."""
+    import torch
+    shape, T = (14, 11), 6
+    rule = lbm.create_lb_update_rule('D2Q9', compressible=compressible)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.3, target='cpu')
+    _set_cavity(step, shape, None if adjoint == 'derived' else lbm.AdjointNoSlip())
+    wall, vel = _cavity(shape)
+    assert np.array_equal(step.boundary_handling.flags != 0, wall)
+    assert step._links() is not None
+    f0 = _init('D2Q9', shape, compressible, seed=21)
+    step.set_pdfs(f0)
+    step.run(T, record=True)
+    ft = torch.tensor(f0, requires_grad=True)
+    ref = OL.run_moving_walls(ft, 1.3, torch.tensor(wall), torch.tensor(vel), T, 'D2Q9', compressible, xp=torch)
+    assert np.abs(step.pdf_array - ref.detach().numpy()).max() <= 1e-13 * np.abs(f0).max()
+    # the lid drives the flow: the moving-wall terms are in (the no-slip-only run differs)
+    still = OL.run_walls(torch.tensor(f0), 1.3, torch.tensor(wall), T, 'D2Q9', compressible, xp=torch)
+    assert float((ref - still).abs().max()) > 1e-3
+    g = np.random.default_rng(22).standard_normal(f0.shape)
+    (gref,) = torch.autograd.grad(ref, ft, torch.tensor(g))
+    step.set_adjoint_pdfs(g)
+    step.run_backward(T)
+    assert np.abs(step.adjoint_pdf_array - gref.numpy()).max() <= 1e-12 * np.abs(gref.numpy()).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', ['float64', 'float32'])
+def test_lbm_lid_driven_cavity_gpu(dtype):
+    """The lid-driven cavity through the timestep op on the HIP lattice kernels: forward vs the moving-wall
+    restatement, the adjoint vs torch's reverse mode through it."""
+    import torch
+    shape, T = (70, 64), 8
+    rule = lbm.create_lb_update_rule('D2Q9', compressible=True, data_type=dtype)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.5, target='gpu')
+    _set_cavity(step, shape)
+    wall, vel = _cavity(shape)
+    Op = step.create_timestep_op(T)
+    f0 = _init('D2Q9', shape, True, seed=23)
+    tdt = getattr(torch, dtype)
+    x = torch.tensor(f0, dtype=tdt, device='cuda', requires_grad=True)
+    out = Op.apply(x)
+    ft = torch.tensor(f0, requires_grad=True, device='cuda')
+    ref = OL.run_moving_walls(ft, 1.5, torch.tensor(wall, device='cuda'), torch.tensor(vel, device='cuda'), T, 'D2Q9',
+                              True, xp=torch)
+    tol = 1e-12 if dtype == 'float64' else 1e-5
+    assert float((out.double() - ref).abs().max()) <= tol * float(ref.abs().max())
+    g = torch.tensor(np.random.default_rng(24).standard_normal(f0.shape), device='cuda')
+    out.backward(g.to(tdt))
+    (gref,) = torch.autograd.grad(ref, ft, g)
+    assert float((x.grad.double() - gref).abs().max()) <= 10 * tol * float(gref.abs().max())
