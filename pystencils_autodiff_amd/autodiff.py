@@ -442,14 +442,15 @@ class AutoDiffOp:
                        **kwargs):
         """``ps.create_kernel(assignments, *args, **kwargs).compile()`` (``_autodiff.py:592-598``): a
         compiled kernel of this op's forward / backward assignments with pystencils' defaults — interior
-        only unless ``ghost_layers=0`` (then out-of-domain reads are zeros, the only defined meaning)."""
+        only unless ``ghost_layers=0`` (then out-of-domain reads are zeros, the only defined meaning);
+        ``iteration_slice`` (unit-step slices / ints per axis, absolute coordinates) restricts the cells written,
+        as in pystencils (ghost layers are then ignored; reads leaving the domain read zeros)."""
         from .backends.kernel_ir import StencilKernel
-        if iteration_slice is not None:
-            raise NotImplementedError('iteration_slice is not supported')
         ac = self._forward_assignments if which == 'forward' else self._backward_assignments
         bh = 'zeros' if ghost_layers == 0 else None
         return StencilKernel(ac, boundary_handling=bh, function_name=f"{self.op_name}_{which}_{target}_custom",
-                             target=target, data_type=data_type, **{**self._kwargs, **kwargs}).compile()
+                             target=target, data_type=data_type, iteration_slice=iteration_slice,
+                             **{**self._kwargs, **kwargs}).compile()
 
     def create_forward_kernel(self, *args, **kwargs):
         return self._create_kernel('forward', *args, **kwargs)

@@ -242,8 +242,8 @@ class HipStencilKernel:
     # -- sources --------------------------------------------------------------------------------
     def schedule(self):
         ir = self.ir
-        if ir.ndim not in (1, 2, 3):
-            return 'generic'
+        if ir.ndim not in (1, 2, 3) or ir.islice is not None:
+            return 'generic'               # an iteration_slice: any rectangular subset, bound-checked reads
         if ir.pointwise:
             return 'generic' if ir.has_index_dims else 'pointwise'
         if ir.periodic:

@@ -26,7 +26,7 @@ import hashlib
 import itertools
 from dataclasses import dataclass, field as dc_field
 from functools import cached_property
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import sympy as sp
@@ -75,6 +75,7 @@ class KernelIR:
     compute_dtype: np.dtype
     symbol_names: Dict[sp.Symbol, str] = dc_field(default_factory=dict)
     periodic: bool = False                 # reads / offset writes wrap around, full iteration space
+    islice: Optional[Tuple] = None         # pystencils' iteration_slice: per-axis (start, stop), unit step
 
     @cached_property
     def pointwise(self):
@@ -97,8 +98,34 @@ class KernelIR:
 
     def iteration_bounds(self, shape):
         """Per-axis [lo, hi) of the cells this kernel writes."""
+        if self.islice is not None:
+            out = []
+            for (a, b), n in zip(self.islice, shape):
+                lo, hi, _ = slice(a, b).indices(int(n))
+                out.append((lo, max(lo, hi)))
+            return out
         g = 0 if self.zeros or self.periodic else self.ghost_layers
         return [(g, max(g, int(n) - g)) for n in shape]
+
+
+def normalize_slice(iteration_slice, ndim):
+    """``iteration_slice`` (a slice / int per spatial axis, e.g. ``make_slice[1:-1, 2]``) as ``((start, stop), …)``
+    with unit steps; missing trailing axes are whole."""
+    items = iteration_slice if isinstance(iteration_slice, tuple) else (iteration_slice,)
+    if len(items) > ndim:
+        raise ValueError(f'iteration_slice {iteration_slice} has more axes than the {ndim}-d kernel')
+    out = []
+    for it in list(items) + [slice(None)] * (ndim - len(items)):
+        if isinstance(it, slice):
+            if it.step not in (None, 1):
+                raise NotImplementedError(f'iteration_slice with step {it.step}: unit steps only')
+            out.append((it.start, it.stop))
+        elif isinstance(it, (int, np.integer)):
+            i = int(it)
+            out.append((i, i + 1 if i != -1 else None))
+        else:
+            raise TypeError(f'iteration_slice entry {it!r}: a slice or an int')
+    return tuple(out)
 
 
 def _strip_conditionals(expr):
@@ -269,12 +296,19 @@ class StencilKernel:
     """One forward or backward kernel of an ``AutoDiffOp`` for one target ('gpu' / 'cpu')."""
 
     def __init__(self, assignments, boundary_handling=None, function_name='kernel', target='gpu',
-                 data_type=None, cpu_openmp=False, gpu_indexing_params=None, **kwargs):
+                 data_type=None, cpu_openmp=False, gpu_indexing_params=None, iteration_slice=None, **kwargs):
         self.assignments = assignments
         self.boundary_handling = boundary_handling
         self.function_name = function_name
         self.target = target
-        self.ir = lower(assignments, boundary_handling, data_type)
+        if iteration_slice is not None:
+            # pystencils' create_kernel(iteration_slice=...): iterate over this rectangular subset of the field
+            # (absolute cell coordinates, ghost layers ignored); cells outside it are not touched. A read that
+            # leaves the domain reads zero here (pystencils reads out of bounds); the one-thread-per-cell schedule
+            self.ir = lower(assignments, 'zeros', data_type)
+            self.ir.islice = normalize_slice(iteration_slice, self.ir.ndim)
+        else:
+            self.ir = lower(assignments, boundary_handling, data_type)
         self.cpu_openmp = cpu_openmp
         self.tuning = dict(gpu_indexing_params or {})
         self.extra_kwargs = kwargs

@@ -42,7 +42,13 @@ def main():
                 ms = timed(lambda: k(u=u, out=out))
                 cfg = k.last_variant[1]
                 print(f'{name} {n}^3 XO={xo}: {ms:.4f} ms  {4 * n ** 3 / ms / 1e6:6.0f} GB/s  '
-                      f'(WS={cfg.WS} XM={cfg.XM} XO={cfg.XO} VE={cfg.VE} NR={cfg.NR})', flush=True)
+                      f'(WS={cfg.WS} XM={cfg.XM} XO={cfg.XO} VE={cfg.VE} NR={cfg.NR} BAND={cfg.BAND})', flush=True)
+                if cfg.BAND:
+                    # the same size on the zsum ring (what the unaligned neighbours run on)
+                    kz = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='oddz',
+                                       target='gpu', gpu_indexing_params={'BAND': 0}).compile()
+                    ms = timed(lambda: kz(u=u, out=out))
+                    print(f'{name} {n}^3 zsum: {ms:.4f} ms  {4 * n ** 3 / ms / 1e6:6.0f} GB/s', flush=True)
                 if os.environ.get('NR_SWEEP') and xo == '1':
                     for nr in (2, 4):
                         kt = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name=f'oddnr{nr}',

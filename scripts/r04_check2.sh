@@ -1,10 +1,15 @@
 set -u
 # round 4: band A/B (edge lanes, stagger, chunk lengths), element-wise parity tests, LBM GPU tests (UBB lid cavity)
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp PSAD_CACHE_DIR=/tmp/psad_cache
-timeout -k 10 600 python -u -m pytest tests/test_band.py tests/test_gpu_parity.py tests/test_lbm.py -m gpu -x -q --timeout 300 --timeout-method thread -k "band_vs_oracle or golden_linear or full_size_properties or 512_vs_c_oracle or lbm" > gpurun_out/r04_cells_pytest.log 2>&1 || { tail -40 gpurun_out/r04_cells_pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_band.py tests/test_gpu_parity.py tests/test_lbm.py tests/test_cpu_backend.py -m gpu -x -q --timeout 300 --timeout-method thread -k "band_vs_oracle or golden_linear or full_size_properties or 512_vs_c_oracle or lbm or iteration_slice" > gpurun_out/r04_cells_pytest.log 2>&1 || { tail -40 gpurun_out/r04_cells_pytest.log; exit 1; }
 tail -3 gpurun_out/r04_cells_pytest.log
 timeout -k 10 400 python -u scripts/probes/op_band_ab.py "s27:768:BEDGE=0:BTRIM=1:BTRIM=1,BEDGE=0:BTRIM=1,BSTAG=40:BTRIM=1,BSTAG=100:BTRIM=1,MAP=1:BTRIM=1,ZMIN=40,ZMAX=40:BTRIM=1,ZMIN=64,ZMAX=64" > gpurun_out/r04_op_band_ab3.log 2>&1 || exit 1
 grep -v amdgpu.ids gpurun_out/r04_op_band_ab3.log
 timeout -k 10 300 python -u scripts/probes/op_band_ab.py "s27:1024:BTRIM=1,ZMIN=32,ZMAX=32:BTRIM=1,ZMIN=32,ZMAX=32,BEDGE=0:BTRIM=1,ZMIN=32,ZMAX=32,BSTAG=40:BTRIM=1,ZMIN=40,ZMAX=40" "h7:768:BTRIM=1,BEDGE=0:BTRIM=1:BTRIM=1,ZMIN=12,ZMAX=12" > gpurun_out/r04_op_band_ab4.log 2>&1 || exit 1
 grep -v amdgpu.ids gpurun_out/r04_op_band_ab4.log
 echo done
+timeout -k 10 400 python -u scripts/probes/op_band_ab.py "f7:512:CX=2:NR=2:ZMIN=64,ZMAX=64:MAP=1:D=3:CX=2,ZMIN=64,ZMAX=64:CX=2,MAP=1" "f7:768:CX=2:MAP=0:D=3:ZMIN=64,ZMAX=64" > gpurun_out/r04_op_f7_ab.log 2>&1 || exit 1
+grep -v amdgpu.ids gpurun_out/r04_op_f7_ab.log
+timeout -k 10 300 python -u scripts/probes/odd_rows.py > gpurun_out/r04_odd_rows.log 2>&1 || exit 1
+grep -v amdgpu.ids gpurun_out/r04_odd_rows.log | head -60
+echo done2

@@ -268,6 +268,38 @@ def test_create_forward_backward_kernel_like_reference():
                      1e-6, 'backward')
 
 
+@pytest.mark.parametrize('target', ['cpu', pytest.param('gpu', marks=pytest.mark.gpu)])
+@pytest.mark.parametrize('islice', [(slice(1, -1), slice(2, 5)), (slice(0, 3), 4, slice(None)), (-1,),
+                                    (slice(2, 2),)])
+def test_create_kernel_iteration_slice(target, islice):
+    """create_forward_kernel(iteration_slice=...) like pystencils' create_kernel: only the cells of the slice are
+    written (absolute coordinates, ghost layers ignored), the rest keeps its contents; reads that leave the domain
+    read zeros. CPU (C) and GPU (the one-thread-per-cell HIP schedule)."""
+    from pystencils_autodiff_amd.lbm import make_slice  # noqa: F401 (the same make_slice surface)
+    op = pa.AutoDiffOp(W.asym_7pt(), boundary_handling='zeros')
+    rng = np.random.default_rng(9)
+    u = rng.uniform(-1, 1, (6, 7, 8)).astype(np.float32)
+    k = op.create_forward_kernel(target, iteration_slice=islice)
+    ref_full = OE.evaluate(op.forward_assignments, {'u': u}, boundary_handling='zeros')['out']
+    expect = np.full_like(u, 7.0)
+    sl = tuple(it if isinstance(it, slice) else slice(it, it + 1 if it != -1 else None) for it in islice)
+    expect[sl] = ref_full[sl]
+    if target == 'cpu':
+        out = np.full_like(u, 7.0)
+        k(u=u, out=out)
+    else:
+        import torch
+        ot = torch.full(u.shape, 7.0, device='cuda')
+        k(u=torch.from_numpy(u).cuda(), out=ot)
+        torch.cuda.synchronize()
+        out = ot.cpu().numpy()
+        assert k.last_variant[0] == 'generic'
+    assert np.array_equal(out == 7.0, expect == 7.0) or np.allclose(out, expect, atol=1e-6)
+    assert_close_rel(out, expect, 1e-6, f'slice {islice}')
+    with pytest.raises(NotImplementedError):
+        op.create_forward_kernel(target, iteration_slice=(slice(0, None, 2),))
+
+
 @pytest.mark.parametrize('bmin', [0, 1 << 30])
 @pytest.mark.parametrize('builder', [W.asym_7pt, W.stencil_27pt])
 def test_interior_only_border_allocation(monkeypatch, bmin, builder):
