@@ -64,9 +64,10 @@ def band_esize(ir):
 
 
 def band_geometry(X, TY, R, D, es=2):
-    """Launch / LDS geometry of a band of ``TY`` rows (``R`` per lane) on rows of ``X`` elements of ``es`` bytes."""
+    """Launch / LDS geometry of a band of ``TY`` rows (``R`` per lane) on rows of ``X`` elements of ``es`` bytes.
+    Rows whose pitch is not a multiple of 16 bytes (``X % VE``) take ``ceil(X / VE)`` chunks, the last one partial."""
     VE = 16 // es
-    CPR = X // VE
+    CPR = -(-X // VE)
     G = TY // R
     ntask = G * CPR
     NCT = -(-ntask // 64) * 64
@@ -90,8 +91,8 @@ def band_choice(X, nstore=1, es=2):
     per CU. fp32 rows hold half the cells per 16-byte chunk: 4-row bands of 4 rows per lane first (the loader's
     vmcnt budget and 80 KB of LDS)."""
     VE = 16 // es
-    if X % VE or X < 16 * VE:
-        return None
+    if (X * es) % 4 or X < 16 * VE:
+        return None                     # rows must start on dwords (the LDS-DMA pieces' alignment)
     rmax = 4 if nstore == 1 else 2
     cands = [(8, 4, 2), (4, 2, 3), (8, 2, 3)] if es == 2 else [(4, 4, 2), (8, 4, 2), (4, 2, 2), (8, 2, 2)]
     cands += [(12, 4, 2), (16, 4, 2), (16, 2, 2), (32, 4, 2), (32, 2, 2)]
@@ -119,6 +120,9 @@ def emit_band(ir, name, cfg):
     S = ir.stencil_fields[0]
     half = es == 2
     et = '_Float16' if half else 'float'            # storage element type
+    XP = CPR * VE                                   # row pitch in the LDS image (elements)
+    bu = XP != X                                    # rows not a multiple of 16 bytes: row-wise pieces, zero fill
+    assert not bu or cfg.BMASK, 'rows of a partial last chunk need the masked stores'
     pr = KernelExprPrinter('float', dict(ir.symbol_names))
     W = []
     for pl in plans:
@@ -145,7 +149,8 @@ def emit_band(ir, name, cfg):
                'const int yhi', 'const int xlo', 'const int xhi', 'const int zc', 'const int zstep', 'const int ntx',
                'const int nty']
     params += _scalar_params(ir)
-    L = [PRELUDE, 'typedef unsigned u32x4 __attribute__((ext_vector_type(4)));']
+    L = [PRELUDE, 'typedef unsigned u32x4 __attribute__((ext_vector_type(4)));',
+         'typedef unsigned u32x3 __attribute__((ext_vector_type(3)));', 'typedef unsigned u32x2 __attribute__((ext_vector_type(2)));']
     L.append(f'// band schedule: {TY}-row bands of full {X}-element rows, {R} rows x {VE} cells per lane, {NCT // 64} '
              f'compute waves + LDS-DMA loader wave, {NS}-slot {et} plane ring ({D} planes in flight), z partial sums '
              f'in 3 rotating register sets, LDS {g["lds_bytes"]} B')
@@ -173,7 +178,14 @@ def emit_band(ir, name, cfg):
     L.append('    #pragma unroll')
     L.append(f'    for (int i = 0; i < {NI}; ++i) {{')
     L.append('      const int k = i * 64 + lane;')
-    L.append(f'      vo[i] = k < {NPIECE} ? ((y0 - 1) * {X * es} + 16 * k) : 0x7ffffff0;   // row -1 / past Y: range check')
+    if not bu:
+        L.append(f'      vo[i] = k < {NPIECE} ? ((y0 - 1) * {X * es} + 16 * k) : 0x7ffffff0;   // row -1 / past Y: range '
+                 'check')
+    else:
+        # rows of a pitch that is not a multiple of 16 bytes: each row's pieces start at the row (dword-aligned, the
+        # LDS image keeps a 16-byte row pitch XP); the last piece runs past the row end (zero-filled below)
+        L.append(f'      const int rr = k / {CPR}, pc = k - rr * {CPR}, yy = y0 - 1 + rr;')
+        L.append(f'      vo[i] = (k < {NPIECE} && yy >= 0 && yy < Y) ? (yy * {X * es} + 16 * pc) : 0x7ffffff0;')
     L.append('    }')
     L.append('    auto issue = [&](const int q, const int slot) {')
     L.append(f'      const {et}* pb = {_ws_plane_base(S, 1, "q")};')
@@ -198,6 +210,16 @@ def emit_band(ir, name, cfg):
     for a in range(D):
         L.append(f'        case {a}: asm volatile("s_waitcnt vmcnt({a * NI})" ::: "memory"); break;')
     L.append('      }')
+    if bu:
+        # plane j has landed: zeros over the image columns X .. XP of every row (the straddling last piece brought
+        # the next row's first elements), which the row's last cells read as their right neighbours
+        ndw = (XP - X) * es // 4
+        L.append('      {')
+        L.append(f'        unsigned* img = (unsigned*)(lds + (j % {NS}) * {SLOT});')
+        L.append(f'        for (int i = lane; i < {(TY + 2) * ndw}; i += 64) '
+                 f'img[(i / {ndw}) * {XP * es // 4} + {X * es // 4} + i % {ndw}] = 0u;')
+        L.append('        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
+        L.append('      }')
     L.append('      __builtin_amdgcn_s_barrier();')
     L.append(f'      if (j + {D} < nplanes) issue(zb - 1 + j + {D}, (j + {D}) % {NS});')
     L.append('    }')
@@ -207,11 +229,12 @@ def emit_band(ir, name, cfg):
     L.append(f'  const bool active = tid < {g["ntask"]};')
     L.append(f'  const int t = active ? tid : {g["ntask"] - 1};')
     L.append(f'  const int grp = t / {CPR}, col = t - grp * {CPR};')
-    L.append(f'  const int lofs = grp * {R * X} + col * {VE};          // slot row grp*R = input row y0 + grp*R - 1')
+    L.append(f'  const int lofs = grp * {R * XP} + col * {VE};          // slot row grp*R = input row y0 + grp*R - 1')
     L.append(f'  const int x = col * {VE};')
     L.append(f'  const bool lmask = col == 0, rmask = col == {CPR - 1};')
     if cfg.BMASK:
         L.append(f'  const bool xfull = x >= xlo && x + {VE} <= xhi;')
+        L.append(f'  const bool xtail = x + {VE} > {X};                 // the row\'s partial last chunk (unaligned rows)')
     L.append(f'  const int yrow0 = y0 + grp * {R};')
     L.append(f'  const unsigned sofs = (unsigned)(yrow0 * {X} + x) * {es}u;')
     if cfg.BMASK:
@@ -235,7 +258,7 @@ def emit_band(ir, name, cfg):
     store_field = [pl['field'] for pl in plans]
 
     def row_prologue(ind, r):
-        B = [f'{ind}    const {et}* rp = sl + {r * X};']
+        B = [f'{ind}    const {et}* rp = sl + {r * XP};']
         if half:
             B += [f'{ind}    const f16x8 v = *(const f16x8*)rp;',
                   f'{ind}    const u32x4 d = __builtin_bit_cast(u32x4, v);']
@@ -296,23 +319,64 @@ def emit_band(ir, name, cfg):
             B.append(f'{ind}    if (xfull) {{')
             B.append(f'{ind}      {st}')
             B.append(f'{ind}    }} else {{')
-            if cfg.XB:
+            # not a whole in-range chunk. 'bu' rows: the partial last chunk holds X % VE cells of the row (the rest is
+            # the next row's), stored as whole dwords (X·es is a multiple of 4)
+            ndw_t = (X % VE) * es // 4 if bu else 0
+            dwst = {1: 'b32', 2: 'b64', 3: 'b96'}
+            dwty = {1: 'unsigned', 2: 'u32x2', 3: 'u32x3'}
+
+            def tail_store(vec):
+                sub = {1: f'{vec}.x', 2: f'{vec}.xy', 3: f'{vec}.xyz'}[ndw_t]
+                return (f'__builtin_amdgcn_raw_buffer_store_{dwst[ndw_t]}(({dwty[ndw_t]}){sub}, ors, '
+                        f'sofs + {o * X * es}u, 0, 2);')
+            if cfg.BXW:
+                # the launch's x range is the whole row: the only chunk not stored whole is a 'bu' row's partial last
+                if bu:
+                    B.append(f'{ind}      const u32x4 ow = __builtin_bit_cast(u32x4, ov);')
+                    B.append(f'{ind}      {tail_store("ow")}')
+            elif cfg.XB:
                 # x border cells: zeros (the row is stored whole); each cell selected on its own
                 sel = ', '.join(f'(x + {q} >= xlo && x + {q} < xhi) ? {cell(si, sp, o, q)} : ({et})0' for q in range(VE))
                 B.append(f'{ind}      const {vt} zv = {{{sel}}};')
-                B.append(f'{ind}      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, zv), ors, '
-                         f'sofs + {o * X * es}u, 0, 2);')
+                full = (f'__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, zv), ors, '
+                        f'sofs + {o * X * es}u, 0, 2);')
+                if bu:
+                    B.append(f'{ind}      const u32x4 zw = __builtin_bit_cast(u32x4, zv);')
+                    B.append(f'{ind}      if (xtail) {{ {tail_store("zw")} }} else {{ {full} }}')
+                else:
+                    B.append(f'{ind}      {full}')
             else:
-                # x border: interior cells only, one store per cell, each converted on its own (a lane extracted
-                # from the packed f16x8 was stored as element 0 for every cell by hipcc 7.2)
-                for q in range(VE):
-                    if half:
-                        stq = (f'__builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, '
-                               f'{cell(si, sp, o, q)}), ors, sofs + {o * X * es + es * q}u, 0, 0);')
+                # cells outside [xlo, xhi) keep their contents: read-modify-write of the lane's chunk (the whole chunk,
+                # or the partial last one), cells selected one by one (per-cell stores cost ~30 VGPRs in the loop)
+                B.append(f'{ind}      const u32x4 ow = __builtin_bit_cast(u32x4, ov);')
+                B.append(f'{ind}      u32x4 old;')
+                if bu:
+                    ld = {1: 'b32', 2: 'b64', 3: 'b96'}[ndw_t] if ndw_t else None
+                    B.append(f'{ind}      if (xtail) {{')
+                    if ndw_t == 1:
+                        B.append(f'{ind}        old.x = __builtin_amdgcn_raw_buffer_load_b32(ors, sofs + {o * X * es}u, 0, 0);')
                     else:
-                        stq = (f'__builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, '
-                               f'{cell(si, sp, o, q)}), ors, sofs + {o * X * es + es * q}u, 0, 0);')
-                    B.append(f'{ind}      if (x + {q} >= xlo && x + {q} < xhi) {stq}')
+                        B.append(f'{ind}        const {dwty[ndw_t]} t = __builtin_amdgcn_raw_buffer_load_{ld}(ors, '
+                                 f'sofs + {o * X * es}u, 0, 0);')
+                        B.append(f'{ind}        old.x = t.x; old.y = t.y;' + (' old.z = t.z;' if ndw_t == 3 else ''))
+                    B.append(f'{ind}      }} else old = __builtin_amdgcn_raw_buffer_load_b128(ors, sofs + {o * X * es}u, 0, 0);')
+                else:
+                    B.append(f'{ind}      old = __builtin_amdgcn_raw_buffer_load_b128(ors, sofs + {o * X * es}u, 0, 0);')
+                nw = []
+                for d in range(4):
+                    if half:
+                        lo = f'(x + {2 * d} >= xlo && x + {2 * d} < xhi)'
+                        hi = f'(x + {2 * d + 1} >= xlo && x + {2 * d + 1} < xhi)'
+                        nw.append(f'(({lo} ? ow.{"xyzw"[d]} : old.{"xyzw"[d]}) & 0xffffu) | '
+                                  f'(({hi} ? ow.{"xyzw"[d]} : old.{"xyzw"[d]}) & 0xffff0000u)')
+                    else:
+                        nw.append(f'(x + {d} >= xlo && x + {d} < xhi) ? ow.{"xyzw"[d]} : old.{"xyzw"[d]}')
+                B.append(f'{ind}      const u32x4 nw = {{{", ".join(nw)}}};')
+                full = f'__builtin_amdgcn_raw_buffer_store_b128(nw, ors, sofs + {o * X * es}u, 0, 2);'
+                if bu:
+                    B.append(f'{ind}      if (xtail) {{ {tail_store("nw")} }} else {{ {full} }}')
+                else:
+                    B.append(f'{ind}      {full}')
             B.append(f'{ind}    }}')
             B.append(f'{ind}  }}')
         B.append(f'{ind}}}')

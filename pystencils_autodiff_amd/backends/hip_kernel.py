@@ -631,8 +631,16 @@ class HipStencilKernel:
             return (step != v * esize or X % v == 0) and \
                 all(by_name[f.name].data_ptr() % step == 0 for f in stencil) and \
                 all(h.data_ptr() % step == 0 for h in halo_list if h is not None)
-        xm = False
+        bu = None
         if not fits(ve) and (X * esize) % 4 == 0 and fits(ve, step=4) and not ir.has_index_dims and \
+                all(t.data_ptr() % 4 == 0 for t in tensors) and int(np.prod(shape[1:])) * esize < 2 ** 31 - 1024 and \
+                os.environ.get('PSAD_BAND_UNALIGNED', '1') != '0':
+            # rows whose pitch is not a multiple of 16 bytes on the row-band schedule: row-wise dword-aligned pieces,
+            # a 16-byte row pitch in LDS, the partial last chunk stored cell by cell (hip_band, 'bu')
+            c = self._march_cfg(ve, shape, band=True)
+            bu = c if c.BAND else None
+        xm = False
+        if bu is None and not fits(ve) and (X * esize) % 4 == 0 and fits(ve, step=4) and not ir.has_index_dims and \
                 all(np.dtype(f.dtype.numpy_dtype).itemsize == esize for f in ir.fields) and \
                 int(np.prod(shape[1:])) * esize < 2 ** 31 - 1024:       # (the loader's 32-bit offsets, below)
             # rows whose pitch is not a multiple of 16 bytes but of 4 (fp32 / fp64, fp16 with X even): the LDS-DMA
@@ -650,7 +658,9 @@ class HipStencilKernel:
             probe = self._march_cfg(ve, shape, band=False)
             ws_p = ws_geometry(ir, probe) if probe.WS else None
             xo = ws_p is not None and ws_p['kind'] == 'h'
-        if xm or xo:
+        if bu is not None:
+            cfg = bu
+        elif xm or xo:
             cfg = MarchConfig(**{**self._march_cfg(ve, shape, band=False).__dict__, 'XM': True,
                                  'XO': (1 if X % 2 else 2) if xo else 0})
         else:
@@ -688,8 +698,10 @@ class HipStencilKernel:
         if cfg.BAND:
             # unmasked stores when every band row lies in [ylo, yhi) and the x range is whole rows
             g0 = self.march_launch_geometry(shape, cfg, z_range, z_limits=z_limits)
-            if not (g0['ylo'] == 0 and g0['yhi'] == g0['nty'] * cfg.BTY and g0['xlo'] == 0 and g0['xhi'] == g0['X']):
-                cfg = MarchConfig(**{**cfg.__dict__, 'BMASK': True})
+            if not (g0['ylo'] == 0 and g0['yhi'] == g0['nty'] * cfg.BTY and g0['xlo'] == 0 and g0['xhi'] == g0['X']) or \
+                    g0['X'] % (16 // esize):                          # a partial last chunk per row
+                cfg = MarchConfig(**{**cfg.__dict__, 'BMASK': True,
+                                     'BXW': g0['xlo'] == 0 and g0['xhi'] == g0['X'] and not cfg.XB})
         variant = ('march', cfg)
         fn = self.function(variant, device)
         ws = ws_geometry(ir, cfg)

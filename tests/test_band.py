@@ -99,11 +99,13 @@ CASES = [('27pt', W.stencil_27pt), ('7pt_f16', lambda: W.diffusion_7pt(dtype='fl
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('case', CASES, ids=lambda c: c[0])
-@pytest.mark.parametrize('shape', [(11, 24, 256), (9, 21, 256), (7, 16, 768), (5, 12, 1024)])
+@pytest.mark.parametrize('shape', [(11, 24, 256), (9, 21, 256), (7, 16, 768), (5, 12, 1024),
+                                   (7, 16, 766), (6, 13, 510), (5, 9, 762), (4, 8, 254), (5, 8, 765)])
 @pytest.mark.parametrize('bh', ['zeros', None])
 def test_band_vs_oracle(case, shape, bh):
     """Forward and adjoint sweeps on the band schedule vs the float64 oracle; Y not a multiple of the band height
-    (ragged last band) and interior-only stores take the masked variant."""
+    (ragged last band) and interior-only stores take the masked variant; rows whose pitch is not a multiple of 16
+    bytes (766, 510, 762, 254 fp16; 765 fp32) load row-wise dword-aligned pieces and store a partial last chunk."""
     torch = _torch()
     op = pa.AutoDiffOp(case[1](), boundary_handling=bh)
     rng = np.random.default_rng(sum(shape))
@@ -121,8 +123,9 @@ def test_band_vs_oracle(case, shape, bh):
         torch.cuda.synchronize()
         cfg = k.last_variant[1]
         assert k.last_variant[0] == 'march' and cfg.BAND > 0, cfg
-        whole = bh == 'zeros' and shape[1] % cfg.BTY == 0
+        whole = bh == 'zeros' and shape[1] % cfg.BTY == 0 and shape[2] % (16 // dt.itemsize) == 0
         assert cfg.BMASK == (not whole), cfg
+        assert cfg.BXW == (cfg.BMASK and bh == 'zeros'), cfg          # x range = whole rows: no read-modify-write
         absr = abs_terms(ac, ins, bh)
         for n, t in outs.items():
             assert_close_rel(t.double().cpu().numpy(), ref[n], TOL16 if dt.itemsize == 2 else 1e-6,
@@ -232,7 +235,7 @@ def test_band_two_outputs():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('bh', ['zeros', None])
-def test_band_through_the_op(bh, monkeypatch):
+def test_band_through_the_op(bh, monkeypatch, shape=(12, 24, 256)):
     """The drop-in op (``create_tensorflow_op(backend='torch_native')``) on the band schedule (forced with
     ``PSAD_MARCH=BAND=4``): forward and adjoint vs the oracle; with ``None`` the op asks the kernel for the x ends of
     its rows (x_border, zeros) — the band kernel stores them as part of whole rows."""
@@ -240,7 +243,6 @@ def test_band_through_the_op(bh, monkeypatch):
     monkeypatch.setenv('PSAD_MARCH', 'BAND=4')
     op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling=bh)
     fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
-    shape = (12, 24, 256)
     rng = np.random.default_rng(7)
     u = rng.uniform(-1, 1, shape).astype(np.float16)
     d = rng.uniform(-1, 1, shape).astype(np.float16)
@@ -296,3 +298,31 @@ def test_band_scalar_coefficient():
     ref = OE.evaluate(ps.AssignmentCollection({out.center: ac.main_assignments[0].rhs.subs(a, 0.15)}),
                       {'u': xs}, boundary_handling='zeros')['out']
     assert_close_rel(res.double().cpu().numpy(), ref, TOL16)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('bh', ['zeros', None])
+@pytest.mark.parametrize('shape', [(12, 23, 766), (10, 16, 510)])
+def test_band_unaligned_rows_through_the_op(bh, shape, monkeypatch):
+    """Rows whose pitch is not a multiple of 16 bytes through the drop-in op on the band schedule (the default for
+    them): forward and adjoint vs the oracle, element-wise."""
+    torch = _torch()
+    op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling=bh)
+    fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    rng = np.random.default_rng(17)
+    u = rng.uniform(-1, 1, shape).astype(np.float16)
+    d = rng.uniform(-1, 1, shape).astype(np.float16)
+    monkeypatch.setenv('PSAD_MARCH', 'BAND=4')          # small domains: force the band schedule (BAND_MIN_WG)
+    ut = torch.from_numpy(u).cuda().requires_grad_(True)
+    (out,) = fn.apply(ut)
+    out.backward(torch.from_numpy(d).cuda())
+    torch.cuda.synchronize()
+    cfg = op.forward_ast_gpu.compile().last_variant[1]
+    assert cfg.BAND == 4 and cfg.BX == shape[2], cfg
+    ref = OE.evaluate(op.forward_assignments, {'u': u.astype(np.float64)}, boundary_handling=bh)['out']
+    refb = OE.evaluate(op.backward_assignments, {'diffout': d.astype(np.float64)}, boundary_handling=bh)
+    (gname,) = refb.keys()
+    assert_cells(out.detach().double().cpu().numpy(), ref, abs_terms(op.forward_assignments, {'u': u}, bh)['out'], 27,
+                 np.float16, 'forward')
+    assert_cells(ut.grad.double().cpu().numpy(), refb[gname],
+                 abs_terms(op.backward_assignments, {'diffout': d}, bh)[gname], 27, np.float16, 'adjoint')
