@@ -434,6 +434,32 @@ def emit_band(ir, name, cfg):
         for k in (2, 0, 1):
             L += step(k, '    ', 'full', 'jj < nplanes', '')
         L.append('  }')
+    elif cfg.BTRIM == 3:
+        # chunks of exactly ZMIN planes (every chunk but a ragged last one): peeled first two planes, the main loop
+        # over planes 2 .. ZMIN-1, the last two planes peeled after it at their static set roles (ZMIN is a compile-time
+        # constant here); other chunks run the full loop
+        zc = int(cfg.ZMIN)
+        assert cfg.ZMIN == cfg.ZMAX and zc >= 3, 'BTRIM=3 needs a fixed chunk length of >= 3 planes'
+        L.append(f'  if (nplanes == {zc + 2}) {{')
+        L += step(0, '    ', 'p0', None, None)
+        L += step(1, '    ', 'p1', None, None)
+        L.append('    #pragma unroll 1')
+        L.append(f'    while (jj < {zc}) {{')
+        for k in (2, 0, 1):
+            L += step(k, '      ', 'full', f'jj < {zc}', '')
+        L.append('    }')
+        k_end = zc % 3                     # set role of plane jj = zc (= nplanes - 2)
+        L += step(k_end, '    ', 'e0', None, '')
+        L += step((k_end + 1) % 3, '    ', 'e1', None, '')
+        L.append('  } else {                         // a ragged chunk: peeled first two planes only (BTRIM=1)')
+        L += step(0, '    ', 'p0', None, None)
+        L += step(1, '    ', 'p1', None, None)
+        L.append('    #pragma unroll 1')
+        L.append('    while (jj < nplanes) {')
+        for k in (2, 0, 1):
+            L += step(k, '      ', 'full', 'jj < nplanes', '')
+        L.append('    }')
+        L.append('  }')
     else:
         if cfg.BTRIM == 2:
             # also the last two input planes (the taps of outputs after the chunk; 54 of 27·(zc+2) FMAs per cell

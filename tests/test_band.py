@@ -81,7 +81,8 @@ def test_band_sources_compile():
         cfg = default_march_config(hk.ir, 8, (32, 64, 256), {'BAND': 4})
         for c in (cfg, MarchConfig(**{**cfg.__dict__, 'BMASK': True}),
                   MarchConfig(**{**cfg.__dict__, 'BMASK': True, 'XB': True}),
-                  MarchConfig(**{**cfg.__dict__, 'BTRIM': 1}), MarchConfig(**{**cfg.__dict__, 'BTRIM': 2})):
+                  MarchConfig(**{**cfg.__dict__, 'BTRIM': 1}), MarchConfig(**{**cfg.__dict__, 'BTRIM': 2}),
+                  MarchConfig(**{**cfg.__dict__, 'BTRIM': 3, 'ZMIN': 16, 'ZMAX': 16})):
             src, kname = hk.source(('march', c))
             assert kname.endswith('_band') and 'band schedule' in src
             assert len(rt.compile_hip(src)) > 0
@@ -184,7 +185,10 @@ def test_band_chunk_length_and_band_height_bitwise():
                 {'BAND': 4, 'BTRIM': 1}, {'BAND': 4, 'BTRIM': 1, 'ZMIN': 1, 'ZMAX': 1},
                 {'BAND': 4, 'BTRIM': 1, 'ZMIN': 16, 'ZMAX': 16},
                 {'BAND': 4, 'BTRIM': 2, 'ZMIN': 9, 'ZMAX': 9},
-                {'BAND': 4, 'BTRIM': 2, 'ZMIN': 2, 'ZMAX': 2}):   # chunks of < 3 planes: the untrimmed loop
+                {'BAND': 4, 'BTRIM': 2, 'ZMIN': 2, 'ZMAX': 2},    # chunks of < 3 planes: the untrimmed loop
+                # both chunk ends peeled with a compile-time chunk length (ragged chunks: the BTRIM=1 path)
+                {'BAND': 4, 'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13}, {'BAND': 4, 'BTRIM': 3, 'ZMIN': 37, 'ZMAX': 37},
+                {'BAND': 4, 'BTRIM': 3, 'ZMIN': 3, 'ZMAX': 3}):
         k = _kernel(op.forward_assignments, 'zeros', 'bandc', **tun).compile()
         out = torch.full_like(u, float('nan'))
         k(u=u, out=out)
