@@ -68,15 +68,18 @@ def band_geometry(X, TY, R, D, es=2):
     Rows whose pitch is not a multiple of 16 bytes (``X % VE``) take ``ceil(X / VE)`` chunks, the last one partial."""
     VE = 16 // es
     CPR = -(-X // VE)
+    # LDS image row pitch (elements, 16-byte multiple). Rows starting on half dwords (fp16, X odd) are loaded from the
+    # dword at or below their start, one element early every other row: the image row then needs room for X + 2
+    XP = CPR * VE if (X * es) % 4 == 0 else VE * -(-(X + 2) // VE)
     G = TY // R
     ntask = G * CPR
     NCT = -(-ntask // 64) * 64
-    NPIECE = (TY + 2) * CPR
+    NPIECE = (TY + 2) * (XP // VE)
     NI = -(-NPIECE // 64)
     SLOT = NI * 64 * VE
     NS = D + 1
-    return dict(VE=VE, CPR=CPR, G=G, ntask=ntask, NCT=NCT, NT=NCT + 64, NPIECE=NPIECE, NI=NI, SLOT=SLOT, NS=NS,
-                lds_bytes=(NS * SLOT + 64) * es)
+    return dict(VE=VE, CPR=CPR, XP=XP, G=G, ntask=ntask, NCT=NCT, NT=NCT + 64, NPIECE=NPIECE, NI=NI, SLOT=SLOT,
+                NS=NS, lds_bytes=(NS * SLOT + 64) * es)
 
 
 def _fits(X, TY, R, D, es=2):
@@ -91,8 +94,8 @@ def band_choice(X, nstore=1, es=2):
     per CU. fp32 rows hold half the cells per 16-byte chunk: 4-row bands of 4 rows per lane first (the loader's
     vmcnt budget and 80 KB of LDS)."""
     VE = 16 // es
-    if (X * es) % 4 or X < 16 * VE:
-        return None                     # rows must start on dwords (the LDS-DMA pieces' alignment)
+    if X < 16 * VE:
+        return None
     rmax = 4 if nstore == 1 else 2
     cands = [(8, 4, 2), (4, 2, 3), (8, 2, 3)] if es == 2 else [(4, 4, 2), (8, 4, 2), (4, 2, 2), (8, 2, 2)]
     cands += [(12, 4, 2), (16, 4, 2), (16, 2, 2), (32, 4, 2), (32, 2, 2)]
@@ -120,8 +123,10 @@ def emit_band(ir, name, cfg):
     S = ir.stencil_fields[0]
     half = es == 2
     et = '_Float16' if half else 'float'            # storage element type
-    XP = CPR * VE                                   # row pitch in the LDS image (elements)
+    XP = g['XP']                                    # row pitch in the LDS image (elements)
+    NPR = XP // VE                                  # pieces per image row
     bu = XP != X                                    # rows not a multiple of 16 bytes: row-wise pieces, zero fill
+    bo = (X * es) % 4 != 0                          # rows on half dwords (fp16, X odd): realigned in registers
     assert not bu or cfg.BMASK, 'rows of a partial last chunk need the masked stores'
     pr = KernelExprPrinter('float', dict(ir.symbol_names))
     W = []
@@ -175,27 +180,44 @@ def emit_band(ir, name, cfg):
     # ---- loader wave
     L.append(f'  if (wave == {NCT // 64}) {{')
     L.append(f'    int vo[{NI}];')
+    if bo:
+        L.append(f'    int vo1[{NI}];')
+        L.append('    auto hpar = [&](const void* b) { return b ? (int)(((unsigned long long)b >> 1) & 1) : 0; };')
     L.append('    #pragma unroll')
     L.append(f'    for (int i = 0; i < {NI}; ++i) {{')
     L.append('      const int k = i * 64 + lane;')
     if not bu:
         L.append(f'      vo[i] = k < {NPIECE} ? ((y0 - 1) * {X * es} + 16 * k) : 0x7ffffff0;   // row -1 / past Y: range '
                  'check')
-    else:
+    elif not bo:
         # rows of a pitch that is not a multiple of 16 bytes: each row's pieces start at the row (dword-aligned, the
         # LDS image keeps a 16-byte row pitch XP); the last piece runs past the row end (zero-filled below)
-        L.append(f'      const int rr = k / {CPR}, pc = k - rr * {CPR}, yy = y0 - 1 + rr;')
+        L.append(f'      const int rr = k / {NPR}, pc = k - rr * {NPR}, yy = y0 - 1 + rr;')
         L.append(f'      vo[i] = (k < {NPIECE} && yy >= 0 && yy < Y) ? (yy * {X * es} + 16 * pc) : 0x7ffffff0;')
+    else:
+        # rows on half dwords: a row starting on an odd element (plane parity pp of the plane's first element, the
+        # row's own parity) is loaded from one element early; offsets from the plane's dword-aligned base, one set
+        # per plane parity
+        L.append(f'      const int rr = k / {NPR}, pc = k - rr * {NPR}, yy = y0 - 1 + rr;')
+        L.append(f'      const bool ok = k < {NPIECE} && yy >= 0 && yy < Y;')
+        L.append(f'      const int s0 = yy * {X} - (yy & 1), s1 = 1 + yy * {X} - ((yy & 1) ^ 1);   // even elements')
+        L.append(f'      vo[i] = ok ? 2 * s0 + 16 * pc : 0x7ffffff0;')
+        L.append(f'      vo1[i] = ok ? 2 * s1 + 16 * pc : 0x7ffffff0;')
     L.append('    }')
     L.append('    auto issue = [&](const int q, const int slot) {')
     L.append(f'      const {et}* pb = {_ws_plane_base(S, 1, "q")};')
-    L.append(f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? pb : f_{S.name}), '
-             f'(short)0, pb ? (int)(YX * {es}) : 0, 0x00020000);')
+    if bo:
+        L.append('      const int pp = hpar(pb);')
+        L.append(f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? pb - pp : '
+                 f'f_{S.name}), (short)0, pb ? (int)((YX * 2 + 2 * pp + 3) & ~3ll) : 0, 0x00020000);')
+    else:
+        L.append(f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? pb : '
+                 f'f_{S.name}), (short)0, pb ? (int)(YX * {es}) : 0, 0x00020000);')
     L.append(f'      {et}* dst = lds + slot * {SLOT};')
     L.append('      #pragma unroll')
     L.append(f'      for (int i = 0; i < {NI}; ++i)')
     L.append(f'        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + i * '
-             f'{64 * VE}), 16, vo[i], 0, 0, 0);')
+             f'{64 * VE}), 16, {"pp ? vo1[i] : vo[i]" if bo else "vo[i]"}, 0, 0, 0);')
     L.append('    };')
     if cfg.BSTAG:
         # probe: the co-resident workgroups of a CU's first round start a fraction of a plane apart
@@ -210,7 +232,19 @@ def emit_band(ir, name, cfg):
     for a in range(D):
         L.append(f'        case {a}: asm volatile("s_waitcnt vmcnt({a * NI})" ::: "memory"); break;')
     L.append('      }')
-    if bu:
+    if bo:
+        # plane j has landed: zeros over the image columns past each row's last element (X + the row's parity .. XP)
+        nz = XP - X
+        L.append('      {')
+        L.append(f'        const int ppj = hpar({_ws_plane_base(S, 1, "(zb - 1 + j)")});')
+        L.append(f'        {et}* img = lds + (j % {NS}) * {SLOT};')
+        L.append(f'        for (int i = lane; i < {(TY + 2) * nz}; i += 64) {{')
+        L.append(f'          const int rr = i / {nz}, c = i - rr * {nz}, pos = {X} + (ppj ^ ((y0 - 1 + rr) & 1)) + c;')
+        L.append(f'          if (pos < {XP}) img[rr * {XP} + pos] = ({et})0;')
+        L.append('        }')
+        L.append('        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
+        L.append('      }')
+    elif bu:
         # plane j has landed: zeros over the image columns X .. XP of every row (the straddling last piece brought
         # the next row's first elements), which the row's last cells read as their right neighbours
         ndw = (XP - X) * es // 4
@@ -226,6 +260,8 @@ def emit_band(ir, name, cfg):
     L.append('    return;')
     L.append('  }')
     # ---- compute lanes
+    if bo:
+        L.append('  auto hpar = [&](const void* b) { return b ? (int)(((unsigned long long)b >> 1) & 1) : 0; };')
     L.append(f'  const bool active = tid < {g["ntask"]};')
     L.append(f'  const int t = active ? tid : {g["ntask"] - 1};')
     L.append(f'  const int grp = t / {CPR}, col = t - grp * {CPR};')
@@ -259,6 +295,25 @@ def emit_band(ir, name, cfg):
 
     def row_prologue(ind, r):
         B = [f'{ind}    const {et}* rp = sl + {r * XP};']
+        if bo:
+            # image row r starts one element early when the input row starts on an odd element: realign the lane's
+            # 10 elements x-1 .. x+8 as five dwords (v_perm over adjacent dwords; selector per row and plane parity)
+            sel = 'selA' if r % 2 else 'selB'
+            B += [f'{ind}    const u32x4 d = *(const u32x4*)rp;',
+                  f'{ind}    const unsigned e = *(const unsigned*)(rp + eoff);',
+                  f'{ind}    const unsigned lw = __builtin_amdgcn_update_dpp(e, d.w, 0x138, 0xf, 0xf, false);   // wave_shr:1',
+                  f'{ind}    const unsigned rw = __builtin_amdgcn_update_dpp(e, d.x, 0x130, 0xf, 0xf, false);   // wave_shl:1',
+                  f'{ind}    const f16x2 w0 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.x, lw, {sel})), '
+                  f'w1 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.y, d.x, {sel}));',
+                  f'{ind}    const f16x2 w2 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.z, d.y, {sel})), '
+                  f'w3 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.w, d.z, {sel}));',
+                  f'{ind}    const f16x2 w4 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(rw, d.w, {sel}));',
+                  f'{ind}    const _Float16 l = lmask ? (_Float16)0 : w0[0], rr = rmask ? (_Float16)0 : w4[1];',
+                  f'{ind}    const f32x2 P0 = {{(float)l, (float)w2[0]}}, P1 = {{(float)w0[1], (float)w2[1]}}, '
+                  'P2 = {(float)w1[0], (float)w3[0]};',
+                  f'{ind}    const f32x2 P3 = {{(float)w1[1], (float)w3[1]}}, P4 = {{(float)w2[0], (float)w4[0]}}, '
+                  'P5 = {(float)w2[1], (float)rr};']
+            return B
         if half:
             B += [f'{ind}    const f16x8 v = *(const f16x8*)rp;',
                   f'{ind}    const u32x4 d = __builtin_bit_cast(u32x4, v);']
@@ -321,14 +376,35 @@ def emit_band(ir, name, cfg):
             B.append(f'{ind}    }} else {{')
             # not a whole in-range chunk. 'bu' rows: the partial last chunk holds X % VE cells of the row (the rest is
             # the next row's), stored as whole dwords (X·es is a multiple of 4)
-            ndw_t = (X % VE) * es // 4 if bu else 0
-            dwst = {1: 'b32', 2: 'b64', 3: 'b96'}
-            dwty = {1: 'unsigned', 2: 'u32x2', 3: 'u32x3'}
+            nb_t = (X % VE) * es if bu else 0           # bytes of a row's partial last chunk
+            ndw_t, nh_t = nb_t // 4, (nb_t % 4) // 2       # whole dwords, then one half (X odd)
 
             def tail_store(vec):
-                sub = {1: f'{vec}.x', 2: f'{vec}.xy', 3: f'{vec}.xyz'}[ndw_t]
-                return (f'__builtin_amdgcn_raw_buffer_store_{dwst[ndw_t]}(({dwty[ndw_t]}){sub}, ors, '
-                        f'sofs + {o * X * es}u, 0, 2);')
+                """The partial last chunk of vector ``vec``: whole dwords, then the odd element's half."""
+                out, c = [], 'xyzw'
+                if ndw_t:
+                    ty = {1: 'unsigned', 2: 'u32x2', 3: 'u32x3'}[ndw_t]
+                    out.append(f'__builtin_amdgcn_raw_buffer_store_b{32 * ndw_t}(({ty}){vec}.{c[:ndw_t]}, ors, '
+                               f'sofs + {o * X * es}u, 0, 2);')
+                if nh_t:
+                    out.append(f'__builtin_amdgcn_raw_buffer_store_b16((unsigned short){vec}.{c[ndw_t]}, ors, '
+                               f'sofs + {o * X * es + 4 * ndw_t}u, 0, 2);')
+                return ' '.join(out)
+
+            def tail_load(dst):
+                """Read the current contents of the partial last chunk into ``dst`` (read-modify-write)."""
+                out, c = [], 'xyzw'
+                if ndw_t == 1:
+                    out.append(f'{dst}.x = __builtin_amdgcn_raw_buffer_load_b32(ors, sofs + {o * X * es}u, 0, 0);')
+                elif ndw_t:
+                    ty = {2: 'u32x2', 3: 'u32x3'}[ndw_t]
+                    out.append(f'{{ const {ty} t = __builtin_amdgcn_raw_buffer_load_b{32 * ndw_t}(ors, '
+                               f'sofs + {o * X * es}u, 0, 0); ' + ' '.join(f'{dst}.{c[i]} = t.{c[i]};'
+                                                                        for i in range(ndw_t)) + ' }')
+                if nh_t:
+                    out.append(f'{dst}.{c[ndw_t]} = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(ors, '
+                               f'sofs + {o * X * es + 4 * ndw_t}u, 0, 0);')
+                return ' '.join(out)
             if cfg.BXW:
                 # the launch's x range is the whole row: the only chunk not stored whole is a 'bu' row's partial last
                 if bu:
@@ -351,15 +427,8 @@ def emit_band(ir, name, cfg):
                 B.append(f'{ind}      const u32x4 ow = __builtin_bit_cast(u32x4, ov);')
                 B.append(f'{ind}      u32x4 old;')
                 if bu:
-                    ld = {1: 'b32', 2: 'b64', 3: 'b96'}[ndw_t] if ndw_t else None
-                    B.append(f'{ind}      if (xtail) {{')
-                    if ndw_t == 1:
-                        B.append(f'{ind}        old.x = __builtin_amdgcn_raw_buffer_load_b32(ors, sofs + {o * X * es}u, 0, 0);')
-                    else:
-                        B.append(f'{ind}        const {dwty[ndw_t]} t = __builtin_amdgcn_raw_buffer_load_{ld}(ors, '
-                                 f'sofs + {o * X * es}u, 0, 0);')
-                        B.append(f'{ind}        old.x = t.x; old.y = t.y;' + (' old.z = t.z;' if ndw_t == 3 else ''))
-                    B.append(f'{ind}      }} else old = __builtin_amdgcn_raw_buffer_load_b128(ors, sofs + {o * X * es}u, 0, 0);')
+                    B.append(f'{ind}      if (xtail) {{ old = (u32x4)(0u); {tail_load("old")} }}')
+                    B.append(f'{ind}      else old = __builtin_amdgcn_raw_buffer_load_b128(ors, sofs + {o * X * es}u, 0, 0);')
                 else:
                     B.append(f'{ind}      old = __builtin_amdgcn_raw_buffer_load_b128(ors, sofs + {o * X * es}u, 0, 0);')
                 nw = []
@@ -391,6 +460,12 @@ def emit_band(ir, name, cfg):
                 'e0': ((sp, 1), (s0, 0)), 'e1': ((sp, 1),)}[part]
         B = [f'{ind}if ({guard}) {{' if guard else f'{ind}{{', f'{ind}  __syncthreads();',
              f'{ind}  const {et}* sl = lds + (jj % {NS}) * {SLOT} + lofs;']
+        if bo:
+            # v_perm selectors: input row parity = plane parity ^ (y0 - 1 + row) & 1, y0 and R even -> odd rows r of
+            # the lane take the plane's parity (selA), even rows the other one (selB); 0x05040302 = elements shifted
+            # by one (the row was loaded one element early), 0x07060504 = the dword as it is
+            B += [f'{ind}  const int ppq = hpar({_ws_plane_base(S, 1, "(zb - 1 + jj)")});',
+                  f'{ind}  const unsigned selA = ppq ? 0x07060504u : 0x05040302u, selB = ppq ? 0x05040302u : 0x07060504u;']
         # sets a trimmed step leaves alone are dead (outputs already stored or outside the chunk): overwrite them first
         # so their old values are not live through the step (a full step overwrites its q+1 set; +16-45 VGPRs else)
         for s_ in sorted({sp, s0, sn} - {st for st, _ in sets}):

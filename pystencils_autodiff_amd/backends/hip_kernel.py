@@ -632,11 +632,12 @@ class HipStencilKernel:
                 all(by_name[f.name].data_ptr() % step == 0 for f in stencil) and \
                 all(h.data_ptr() % step == 0 for h in halo_list if h is not None)
         bu = None
-        if not fits(ve) and (X * esize) % 4 == 0 and fits(ve, step=4) and not ir.has_index_dims and \
-                all(t.data_ptr() % 4 == 0 for t in tensors) and int(np.prod(shape[1:])) * esize < 2 ** 31 - 1024 and \
-                os.environ.get('PSAD_BAND_UNALIGNED', '1') != '0':
+        dword_rows = (X * esize) % 4 == 0 and fits(ve, step=4) and all(t.data_ptr() % 4 == 0 for t in tensors)
+        half_rows = esize == 2 and X % 2 == 1          # fp16 rows on half dwords: realigned in registers ('bo')
+        if not fits(ve) and (dword_rows or half_rows) and not ir.has_index_dims and \
+                int(np.prod(shape[1:])) * esize < 2 ** 31 - 1024 and os.environ.get('PSAD_BAND_UNALIGNED', '1') != '0':
             # rows whose pitch is not a multiple of 16 bytes on the row-band schedule: row-wise dword-aligned pieces,
-            # a 16-byte row pitch in LDS, the partial last chunk stored cell by cell (hip_band, 'bu')
+            # a 16-byte row pitch in LDS, the partial last chunk stored as dwords (hip_band, 'bu')
             c = self._march_cfg(ve, shape, band=True)
             bu = c if c.BAND else None
         xm = False

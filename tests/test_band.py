@@ -101,12 +101,14 @@ CASES = [('27pt', W.stencil_27pt), ('7pt_f16', lambda: W.diffusion_7pt(dtype='fl
 @pytest.mark.gpu
 @pytest.mark.parametrize('case', CASES, ids=lambda c: c[0])
 @pytest.mark.parametrize('shape', [(11, 24, 256), (9, 21, 256), (7, 16, 768), (5, 12, 1024),
-                                   (7, 16, 766), (6, 13, 510), (5, 9, 762), (4, 8, 254), (5, 8, 765)])
+                                   (7, 16, 766), (6, 13, 510), (5, 9, 762), (4, 8, 254), (5, 8, 765),
+                                   (6, 12, 767), (5, 9, 511), (7, 8, 255)])
 @pytest.mark.parametrize('bh', ['zeros', None])
 def test_band_vs_oracle(case, shape, bh):
     """Forward and adjoint sweeps on the band schedule vs the float64 oracle; Y not a multiple of the band height
     (ragged last band) and interior-only stores take the masked variant; rows whose pitch is not a multiple of 16
-    bytes (766, 510, 762, 254 fp16; 765 fp32) load row-wise dword-aligned pieces and store a partial last chunk."""
+    bytes (766, 510, 762, 254 fp16; 765 fp32) load row-wise dword-aligned pieces and store a partial last chunk; fp16
+    rows on half dwords (767, 511, 255) are loaded from the dword below and realigned in registers."""
     torch = _torch()
     op = pa.AutoDiffOp(case[1](), boundary_handling=bh)
     rng = np.random.default_rng(sum(shape))
@@ -330,3 +332,31 @@ def test_band_unaligned_rows_through_the_op(bh, shape, monkeypatch):
                  np.float16, 'forward')
     assert_cells(ut.grad.double().cpu().numpy(), refb[gname],
                  abs_terms(op.backward_assignments, {'diffout': d}, bh)[gname], 27, np.float16, 'adjoint')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('off', [0, 1, 3])
+@pytest.mark.parametrize('shape', [(5, 9, 511), (6, 11, 767)])
+def test_band_half_dword_rows_any_base(shape, off):
+    """fp16 rows of odd length on the band schedule from views whose first element sits on any half dword: the plane
+    parity (the plane pointer's bit 1) and the row's own parity pick the realignment per row and plane; vs the oracle,
+    element-wise, forward and adjoint."""
+    torch = _torch()
+    op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
+    n = int(np.prod(shape))
+    rng = np.random.default_rng(off + shape[2])
+    for which, ac in (('f', op.forward_assignments), ('b', op.backward_assignments)):
+        k = _kernel(ac, 'zeros', f'bandodd_{which}', BAND=4).compile()
+        (fin,) = [f.name for f in k.ir.fields_read]
+        (fout,) = [f.name for f in k.ir.fields_written]
+        base = torch.from_numpy(rng.uniform(-1, 1, n + 8).astype(np.float16)).cuda()
+        u = base[off:off + n].view(shape)
+        out = torch.zeros(shape, dtype=torch.float16, device='cuda')
+        k(**{fin: u, fout: out})
+        torch.cuda.synchronize()
+        cfg = k.last_variant[1]
+        assert cfg.BAND == 4 and cfg.BX == shape[2], cfg
+        un = u.cpu().numpy()
+        ref = OE.evaluate(ac, {fin: un.astype(np.float64)}, boundary_handling='zeros')[fout]
+        assert_cells(out.double().cpu().numpy(), ref, abs_terms(ac, {fin: un}, 'zeros')[fout], 27, np.float16,
+                     f'{which} offset {off}')
