@@ -30,6 +30,11 @@ extern "C" {
 /* ABI version of this header; bumped on any signature change. */
 int psad_abi_version(void);
 
+/* The sources the library was built from: 16 hex digits of sha256 over csrc/psad_hip.cpp, csrc/psad_halo.cpp and
+ * this header (pystencils_autodiff_amd/build.py). The Python layer refuses a library whose stamp differs from the
+ * sources of the tree it runs from (a stale build). No reference counterpart (plumbing). */
+const char* psad_source_hash(void);
+
 /* Compile HIP `source` with hiprtc. `options` e.g. {"--offload-arch=gfx950","-O3"}.
  * On success *code / *code_size receive a malloc'ed code object (free with psad_free).
  * The compiler log (possibly empty) is copied, NUL-terminated, into `log` (size `log_size`).

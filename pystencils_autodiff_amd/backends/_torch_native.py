@@ -214,6 +214,9 @@ def native_module():
                         from exc
                 # no GPU here: nothing launches, ops are only built (hiprtc) — the Python Function will do
                 _psad_torch = False
+            if _psad_torch:
+                from .hip_runtime import _check_stamp
+                _check_stamp(_psad_torch.source_hash(), 'torch', _psad_torch.__file__)
             _native = _psad_torch
     return _native or None
 

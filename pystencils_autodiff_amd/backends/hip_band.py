@@ -159,7 +159,8 @@ def emit_band(ir, name, cfg):
     L.append(f'// band schedule: {TY}-row bands of full {X}-element rows, {R} rows x {VE} cells per lane, {NCT // 64} '
              f'compute waves + LDS-DMA loader wave, {NS}-slot {et} plane ring ({D} planes in flight), z partial sums '
              f'in 3 rotating register sets, LDS {g["lds_bytes"]} B')
-    L.append(f'extern "C" __global__ void __launch_bounds__({NT}) {name}({", ".join(params)})\n{{')
+    wpe = f' __attribute__((amdgpu_waves_per_eu({int(cfg.BWPE)}, {int(cfg.BWPE)})))' if cfg.BWPE else ''
+    L.append(f'extern "C" __global__ void __launch_bounds__({NT}){wpe} {name}({", ".join(params)})\n{{')
     L.append(f'  __shared__ __attribute__((aligned(1024))) {et} lds[{NS * SLOT + 64}];')
     L.append('  const int tid = threadIdx.x, lane = tid & 63;')
     L.append('  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);')

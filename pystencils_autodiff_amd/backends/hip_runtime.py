@@ -104,8 +104,23 @@ def lib():
         L.psad_rccl_error_string.restype = cp
         if L.psad_abi_version() != 2:
             raise HipError('libpsad_hip.so ABI mismatch: rebuild the extension')
+        L.psad_source_hash.restype = cp
+        _check_stamp(L.psad_source_hash().decode(), 'lib', library_path)
         _lib = L
         return _lib
+
+
+def _check_stamp(stamp, which, path):
+    """Refuse a native library not built from the sources of this tree (``build.source_hash``): a stale ``.so``
+    shipped next to changed sources would otherwise run silently. Skipped when the sources are not present."""
+    from .. import build
+    srcs = build.lib_sources() if which == 'lib' else build.torch_sources()
+    if not all(os.path.exists(p) for p in srcs) or os.environ.get('PSAD_SKIP_STAMP') == '1':
+        return
+    want = build.source_hash(srcs)
+    if stamp != want:
+        raise HipError(f'{path} was built from other sources (stamp {stamp}, sources {want}): rebuild with '
+                       '`python -m pystencils_autodiff_amd.build`')
 
 
 def _check(code, what):

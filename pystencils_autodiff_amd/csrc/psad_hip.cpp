@@ -31,6 +31,14 @@ extern "C" {
 
 int psad_abi_version(void) { return 2; }
 
+#ifndef PSAD_SOURCE_HASH
+#define PSAD_SOURCE_HASH "0000000000000000"
+#endif
+// the sources this library was built from (build.py: sha256 of csrc/psad_hip.cpp, psad_halo.cpp, include/psad.h),
+// also as a marker in the binary that build.py reads without loading it
+__attribute__((used)) static const char k_source_stamp[] = "PSAD_SOURCE_HASH=" PSAD_SOURCE_HASH;
+const char* psad_source_hash(void) { return k_source_stamp + 17; }
+
 int psad_rtc_version(void) {
     int major = 0, minor = 0;
     if (hiprtcVersion(&major, &minor) != HIPRTC_SUCCESS) return -1;

@@ -183,6 +183,10 @@ struct Exchange {
     std::vector<size_t> bytes;
     int peer_lo = -1, peer_hi = -1;
     bool loopback = false;                // one-rank communicator: both faces to itself (periodic z)
+    // PSAD_SLAB_SYNC=value: the two cross-stream orderings as stream memory operations (hipStreamWriteValue32 /
+    // hipStreamWaitValue32 on a signal-memory word with a sweep counter) instead of event record + wait (A/B)
+    uint32_t* sig = nullptr;              // [0] faces final (compute -> halo stream), [1] halos landed (halo -> compute)
+    mutable uint32_t seq = 0;
 };
 
 struct Sweep {
@@ -221,9 +225,16 @@ void run_sweep(const Sweep& w, const std::vector<at::Tensor>& table, const std::
     hipStream_t cur = c10::hip::getCurrentHIPStream(device).stream();
     const Exchange& ex = w.ex;
     const size_t n = ex.slot.size();
-    if (n) {
+    if (n && ex.sig) ++ex.seq;
+    if (n && ex.sig) {
+        hip_ok(hipStreamWriteValue32(cur, ex.sig, ex.seq, 0), "hipStreamWriteValue32");
+        hip_ok(hipStreamWaitValue32(ex.stream, ex.sig, ex.seq, hipStreamWaitValueGte, 0xffffffffu),
+               "hipStreamWaitValue32");
+    } else if (n) {
         hip_ok(hipEventRecord(ex.ev_faces, cur), "hipEventRecord");           // the faces are final
         hip_ok(hipStreamWaitEvent(ex.stream, ex.ev_faces, 0), "hipStreamWaitEvent");
+    }
+    if (n) {
         std::vector<const void*> send_lo(n), send_hi(n);
         for (size_t i = 0; i < n; ++i) {
             char* base = static_cast<char*>(table[ex.slot[i]].data_ptr());
@@ -240,7 +251,11 @@ void run_sweep(const Sweep& w, const std::vector<at::Tensor>& table, const std::
     if (n && w.faces_on_halo)                                                // faces beside the interior
         for (const auto& f : w.faces) launch_on(f, table, scalars, ex.stream);
     if (w.has_inner) launch(w.inner, table, scalars, device);                // interior overlaps the exchange
-    if (n) {
+    if (n && ex.sig) {
+        hip_ok(hipStreamWriteValue32(ex.stream, ex.sig + 1, ex.seq, 0), "hipStreamWriteValue32");
+        hip_ok(hipStreamWaitValue32(cur, ex.sig + 1, ex.seq, hipStreamWaitValueGte, 0xffffffffu),
+               "hipStreamWaitValue32");
+    } else if (n) {
         hip_ok(hipEventRecord(ex.ev_halos, ex.stream), "hipEventRecord");
         hip_ok(hipStreamWaitEvent(cur, ex.ev_halos, 0), "hipStreamWaitEvent");
     }
@@ -401,6 +416,14 @@ Sweep sweep_from(const py::object& inner, const py::list& faces, const py::tuple
         TORCH_CHECK(w.ex.comm != nullptr, "psad: exchange without a communicator");
         hip_ok(hipEventCreateWithFlags(&w.ex.ev_faces, hipEventDisableTiming), "hipEventCreateWithFlags");
         hip_ok(hipEventCreateWithFlags(&w.ex.ev_halos, hipEventDisableTiming), "hipEventCreateWithFlags");
+        const char* sy = std::getenv("PSAD_SLAB_SYNC");
+        if (sy != nullptr && std::string(sy) == "value") {
+            void* p = nullptr;
+            hip_ok(hipExtMallocWithFlags(&p, 64, hipMallocSignalMemory), "hipExtMallocWithFlags");
+            hip_ok(hipMemset(p, 0, 64), "hipMemset");
+            hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
+            w.ex.sig = static_cast<uint32_t*>(p);
+        }
     }
     return w;
 }
@@ -465,8 +488,15 @@ py::object apply(int64_t id, const std::vector<at::Tensor>& inputs, const std::v
 
 }  // namespace
 
+#ifndef PSAD_SOURCE_HASH
+#define PSAD_SOURCE_HASH "0000000000000000"
+#endif
+__attribute__((used)) static const char k_source_stamp[] = "PSAD_SOURCE_HASH=" PSAD_SOURCE_HASH;
+
 PYBIND11_MODULE(_psad_torch, m) {
     m.doc() = "native autograd node of the torch_native stencil op (see psad_torch.cpp)";
+    m.def("source_hash", []() { return std::string(k_source_stamp + 17); },
+          "sha256 prefix of csrc/psad_torch.cpp + include/psad.h this module was built from (build.py)");
     m.def("register_plan", &register_plan);
     m.def("apply", &apply);
     m.def("register_slab_plan", &register_slab_plan);

@@ -11,4 +11,10 @@ timeout -k 10 400 python -u scripts/probes/op_band_ab.py "s27:1024:BTRIM=1,ZMIN=
 grep -v amdgpu.ids gpurun_out/r04_op_band_ab4.log
 timeout -k 10 400 python -u scripts/probes/op_band_ab.py "f7:512:CX=2:NR=2:ZMIN=64,ZMAX=64:MAP=1:D=3:CX=2,ZMIN=64,ZMAX=64:CX=2,MAP=1" "f7:768:CX=2:MAP=0:D=3:ZMIN=64,ZMAX=64" > gpurun_out/r04_op_f7_ab.log 2>&1 || exit 1
 grep -v amdgpu.ids gpurun_out/r04_op_f7_ab.log
-echo done
+echo done-ab
+timeout -k 10 200 python -u scripts/probes/slab_step.py 96 stencil27 > gpurun_out/r04_slab27_event.log 2>&1 || exit 1
+PSAD_SLAB_SYNC=value timeout -k 10 200 python -u scripts/probes/slab_step.py 96 stencil27 > gpurun_out/r04_slab27_value.log 2>&1 || exit 1
+timeout -k 10 200 python -u scripts/probes/slab_step.py 128 diffusion7 > gpurun_out/r04_slab7_event.log 2>&1 || exit 1
+PSAD_SLAB_SYNC=value timeout -k 10 200 python -u scripts/probes/slab_step.py 128 diffusion7 > gpurun_out/r04_slab7_value.log 2>&1 || exit 1
+for f in gpurun_out/r04_slab*_*.log; do echo "== $f"; grep -v amdgpu.ids $f | tail -6; done
+echo done-slab

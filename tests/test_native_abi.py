@@ -38,6 +38,20 @@ def test_library_exports_header_symbols():
     assert lib.psad_error_string(1)
 
 
+def test_native_libraries_built_from_these_sources():
+    """Both native libraries carry the sha256 stamp of the sources they were built from (build.py), equal to the
+    sources of this tree; the loaders refuse a stale one. On the GPU box this runs against the shipped .so files."""
+    from pystencils_autodiff_amd import build
+    assert build.embedded_hash(build.OUT) == build.source_hash(build.lib_sources())
+    assert rt.lib().psad_source_hash().decode() == build.source_hash(build.lib_sources())
+    assert build.embedded_hash(build.TORCH_OUT) == build.source_hash(build.torch_sources())
+    import torch  # noqa: F401  (the extension resolves torch's symbols)
+    from pystencils_autodiff_amd import _psad_torch
+    assert _psad_torch.source_hash() == build.source_hash(build.torch_sources())
+    with pytest.raises(rt.HipError, match='built from other sources'):
+        rt._check_stamp('0123456789abcdef', 'lib', build.OUT)
+
+
 def test_rtc_compile_error_is_reported():
     with pytest.raises(rt.HipError, match='hiprtc compilation failed'):
         rt.compile_hip('extern "C" __global__ void k() { this is not c++ }')
