@@ -179,7 +179,13 @@ def emit_band(ir, name, cfg):
     L.append(f'  const i64 YX = (i64)Y * {X};')
     L.append('  const int nplanes = ze - zb + 2;')
     # ---- loader wave
-    L.append(f'  if (wave == {NCT // 64}) {{')
+    if cfg.BLDR:
+        # the loader role rotates with the workgroup index: its wave lands on a different SIMD from workgroup to
+        # workgroup even if every workgroup's waves start on the same SIMD
+        L.append(f'  const int ldw = blockIdx.x % {NCT // 64 + 1};')
+    else:
+        L.append(f'  const int ldw = {NCT // 64};')
+    L.append('  if (wave == ldw) {')
     L.append(f'    int vo[{NI}];')
     if bo:
         L.append(f'    int vo1[{NI}];')
@@ -263,8 +269,9 @@ def emit_band(ir, name, cfg):
     # ---- compute lanes
     if bo:
         L.append('  auto hpar = [&](const void* b) { return b ? (int)(((unsigned long long)b >> 1) & 1) : 0; };')
-    L.append(f'  const bool active = tid < {g["ntask"]};')
-    L.append(f'  const int t = active ? tid : {g["ntask"] - 1};')
+    L.append('  const int ctid = (wave - (wave > ldw ? 1 : 0)) * 64 + lane;   // compute task')
+    L.append(f'  const bool active = ctid < {g["ntask"]};')
+    L.append(f'  const int t = active ? ctid : {g["ntask"] - 1};')
     L.append(f'  const int grp = t / {CPR}, col = t - grp * {CPR};')
     L.append(f'  const int lofs = grp * {R * XP} + col * {VE};          // slot row grp*R = input row y0 + grp*R - 1')
     L.append(f'  const int x = col * {VE};')

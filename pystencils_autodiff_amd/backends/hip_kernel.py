@@ -38,7 +38,7 @@ BAND_TRIM = 0
 # describe a one-thread-per-cell launch these schedules do not have, so they are accepted and ignored. Upper-case
 # keys are this layer's tile parameters; an unknown one is a typo and raises.
 TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
-             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE')
+             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE', 'BLDR')
 
 
 def _band_config(ir, ve, shape, over):
@@ -82,7 +82,7 @@ def _band_config(ir, ve, shape, over):
     return MarchConfig(VE=ve, BAND=R, BTY=TY, BX=X, D=D, ZSUM=True, NT_STORE=True, ZMIN=zc,
                        ZMAX=int(over.get('ZMAX', zc)), BLK=int(over.get('BLK', 512)), MAP=int(over.get('MAP', 0)),
                        BTRIM=int(over.get('BTRIM', BAND_TRIM)), BEDGE=int(over.get('BEDGE', 1)),
-                       BSTAG=int(over.get('BSTAG', 0)), BWPE=int(over.get('BWPE', 0)))
+                       BSTAG=int(over.get('BSTAG', 0)), BWPE=int(over.get('BWPE', 0)), BLDR=int(over.get('BLDR', 0)))
 
 
 def default_march_config(ir, ve, shape=None, tuning=None, band=True):

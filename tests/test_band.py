@@ -190,7 +190,8 @@ def test_band_chunk_length_and_band_height_bitwise():
                 {'BAND': 4, 'BTRIM': 2, 'ZMIN': 2, 'ZMAX': 2},    # chunks of < 3 planes: the untrimmed loop
                 # both chunk ends peeled with a compile-time chunk length (ragged chunks: the BTRIM=1 path)
                 {'BAND': 4, 'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13}, {'BAND': 4, 'BTRIM': 3, 'ZMIN': 37, 'ZMAX': 37},
-                {'BAND': 4, 'BTRIM': 3, 'ZMIN': 3, 'ZMAX': 3}):
+                {'BAND': 4, 'BTRIM': 3, 'ZMIN': 3, 'ZMAX': 3},
+                {'BAND': 4, 'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13, 'BLDR': 1}):   # the loader role rotating over waves
         k = _kernel(op.forward_assignments, 'zeros', 'bandc', **tun).compile()
         out = torch.full_like(u, float('nan'))
         k(u=u, out=out)
