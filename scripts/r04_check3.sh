@@ -11,7 +11,7 @@ timeout -k 10 400 python -u scripts/probes/op_band_ab.py "h7:510:BTRIM=1" "s27:7
 grep -v amdgpu.ids gpurun_out/r04_op_unaligned.log
 timeout -k 10 400 python -u scripts/probes/op_band_ab.py "s27:1024:BTRIM=1,ZMIN=32,ZMAX=32:BTRIM=3,ZMIN=32,ZMAX=32:BTRIM=3:BTRIM=3,ZMIN=16,ZMAX=16:BTRIM=1,ZMIN=32,ZMAX=32,BEDGE=0" "h7:768:BTRIM=1,BEDGE=0:BTRIM=1:BTRIM=3:BTRIM=3,ZMIN=16,ZMAX=16" > gpurun_out/r04_op_band_ab4.log 2>&1 || exit 1
 grep -v amdgpu.ids gpurun_out/r04_op_band_ab4.log
-timeout -k 10 400 python -u scripts/probes/op_band_ab.py "f7:512:CX=2:NR=2:ZMIN=64,ZMAX=64:MAP=1:D=3:CX=2,ZMIN=64,ZMAX=64:CX=2,MAP=1" "f7:768:CX=2:MAP=0:D=3:ZMIN=64,ZMAX=64" > gpurun_out/r04_op_f7_ab.log 2>&1 || exit 1
+timeout -k 10 400 python -u scripts/probes/op_band_ab.py "f7:512:CX=2:NR=2:ZMIN=64,ZMAX=64:MAP=1:D=3:CX=2,ZMIN=64,ZMAX=64:CX=2,MAP=1:BAND=4,BTRIM=1:BAND=4,BTRIM=1,ZMIN=16,ZMAX=16" "f7:768:CX=2:MAP=0:D=3:ZMIN=64,ZMAX=64:BAND=4,BTRIM=1" > gpurun_out/r04_op_f7_ab.log 2>&1 || exit 1
 grep -v amdgpu.ids gpurun_out/r04_op_f7_ab.log
 echo done-ab
 timeout -k 10 200 python -u scripts/probes/slab_step.py 96 stencil27 > gpurun_out/r04_slab27_event.log 2>&1 || exit 1
@@ -20,3 +20,6 @@ timeout -k 10 200 python -u scripts/probes/slab_step.py 128 diffusion7 > gpurun_
 PSAD_SLAB_SYNC=value timeout -k 10 200 python -u scripts/probes/slab_step.py 128 diffusion7 > gpurun_out/r04_slab7_value.log 2>&1 || exit 1
 for f in gpurun_out/r04_slab*_*.log; do echo "== $f"; grep -v amdgpu.ids $f | tail -6; done
 echo done-slab
+timeout -k 10 300 python -u scripts/probes/alloc_ab.py > gpurun_out/r04_alloc_ab.log 2>&1 || exit 1
+grep -v amdgpu.ids gpurun_out/r04_alloc_ab.log
+echo done-all
