@@ -315,8 +315,11 @@ def emit_band(ir, name, cfg):
                   f'w1 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.y, d.x, {sel}));',
                   f'{ind}    const f16x2 w2 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.z, d.y, {sel})), '
                   f'w3 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.w, d.z, {sel}));',
-                  f'{ind}    const f16x2 w4 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(rw, d.w, {sel}));',
-                  f'{ind}    const _Float16 l = lmask ? (_Float16)0 : w0[0], rr = rmask ? (_Float16)0 : w4[1];',
+                  # the row's last chunk: x+7 and x+8 both lie at or past X (8·CPR - 1 >= X for odd X) and on a row
+                  # loaded one element early both come from the next lane, which may hold another row: zeros
+                  f'{ind}    const f16x2 w4 = rmask ? (f16x2)((_Float16)0) : '
+                  f'__builtin_bit_cast(f16x2, __builtin_amdgcn_perm(rw, d.w, {sel}));',
+                  f'{ind}    const _Float16 l = lmask ? (_Float16)0 : w0[0], rr = w4[1];',
                   f'{ind}    const f32x2 P0 = {{(float)l, (float)w2[0]}}, P1 = {{(float)w0[1], (float)w2[1]}}, '
                   'P2 = {(float)w1[0], (float)w3[0]};',
                   f'{ind}    const f32x2 P3 = {{(float)w1[1], (float)w3[1]}}, P4 = {{(float)w2[0], (float)w4[0]}}, '
