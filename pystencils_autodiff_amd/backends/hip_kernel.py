@@ -27,11 +27,16 @@ __all__ = ['HipStencilKernel', 'default_march_config']
 # 0.762), star stencils 8-plane chunks (fp16 7-point 1024³ 1.461 vs 1.538, 768³ 0.635 vs 0.682). Launches of fewer
 # than BAND_MIN_WG workgroups (z-slabs of a few planes) keep the zsum ring.
 BAND_ZC_BOX, BAND_ZC_STAR = 48, 8
+# round 4 (profiles/r04_op_band_ab1.log, same process, fwd+bwd through the op): the chunk's first two planes peeled
+# without the taps of outputs before it (BTRIM=1) — 27-point 768³ 0.744 vs 0.768 ms, 1024³ 16-row bands 1.718 vs 1.744
+# (and 1.679 with 32-plane chunks), fp16 7-point 768³ 0.602 vs 0.626
+BAND_ZC_BOX16 = 32
+BAND_TRIM_DEFAULT = 1
 BAND_MIN_WG = 1024
 # fp32 storage (4 cells per 16-byte chunk) measured slower through the op (7-point 512³ 0.387 vs 0.373 ms, 768³
 # 1.325 vs 1.261): opt-in only (BAND=R)
 BAND_F32_MAX_X = 0
-BAND_TRIM = 0
+BAND_TRIM = BAND_TRIM_DEFAULT
 
 # gpu_indexing_params keys of pystencils' own GPU indexing (``block_size``, ``maximum_block_size``, …, e.g.
 # ``gpu_indexing_params={'block_size': (8, 4, 2)}`` in the reference's tests/test_graph_datahandling.py:70): they
@@ -76,7 +81,7 @@ def _band_config(ir, ve, shape, over):
     g = band_geometry(X, TY, R, D, es)
     if TY % R or g['NCT'] > 960 or D * g['NI'] > 63 or g['lds_bytes'] > 160 * 1024:
         raise ValueError(f'band schedule: BTY={TY} BAND={R} D={D} do not fit rows of {X} elements')
-    zc = int(over.get('ZMIN', BAND_ZC_BOX if ntaps > 12 else BAND_ZC_STAR))
+    zc = int(over.get('ZMIN', (BAND_ZC_BOX16 if TY == 16 else BAND_ZC_BOX) if ntaps > 12 else BAND_ZC_STAR))
     if 'BAND' not in over and -(-int(shape[-2]) // TY) * -(-int(shape[0]) // zc) < BAND_MIN_WG:
         return None
     return MarchConfig(VE=ve, BAND=R, BTY=TY, BX=X, D=D, ZSUM=True, NT_STORE=True, ZMIN=zc,
