@@ -224,7 +224,7 @@ def emit_band(ir, name, cfg):
     L.append('      #pragma unroll')
     L.append(f'      for (int i = 0; i < {NI}; ++i)')
     L.append(f'        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + i * '
-             f'{64 * VE}), 16, {"pp ? vo1[i] : vo[i]" if bo else "vo[i]"}, 0, 0, 0);')
+             f'{64 * VE}), 16, {"pp ? vo1[i] : vo[i]" if bo else "vo[i]"}, 0, 0, {int(cfg.BLAUX)});')
     L.append('    };')
     if cfg.BSTAG:
         # probe: the co-resident workgroups of a CU's first round start a fraction of a plane apart

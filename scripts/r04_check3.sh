@@ -5,9 +5,9 @@ timeout -k 10 900 python -u -m pytest tests/test_band.py tests/test_gpu_parity.p
 tail -3 gpurun_out/r04_pytest3.log
 timeout -k 10 60 python -u scripts/probes/simd_place.py > gpurun_out/r04_simd_place.log 2>&1 || exit 1
 grep -v amdgpu.ids gpurun_out/r04_simd_place.log
-timeout -k 10 400 python -u scripts/probes/op_band_ab.py "s27:768:BTRIM=3,BLDR=1:BEDGE=0:BTRIM=1:BTRIM=3:BTRIM=3,ZMIN=24,ZMAX=24:BTRIM=3,ZMIN=16,ZMAX=16:BTRIM=1,BEDGE=0:BTRIM=1,BSTAG=40:BTRIM=1,BSTAG=100:BTRIM=1,MAP=1:BTRIM=1,ZMIN=64,ZMAX=64" > gpurun_out/r04_op_band_ab3.log 2>&1 || exit 1
+timeout -k 10 400 python -u scripts/probes/op_band_ab.py "s27:768:BTRIM=3,BLDR=1:BTRIM=1,BLAUX=2:BTRIM=3,BLDR=1,BLAUX=2:BEDGE=0:BTRIM=1:BTRIM=3:BTRIM=3,ZMIN=24,ZMAX=24:BTRIM=3,ZMIN=16,ZMAX=16:BTRIM=1,BEDGE=0:BTRIM=1,BSTAG=40:BTRIM=1,BSTAG=100:BTRIM=1,MAP=1:BTRIM=1,ZMIN=64,ZMAX=64" > gpurun_out/r04_op_band_ab3.log 2>&1 || exit 1
 grep -v amdgpu.ids gpurun_out/r04_op_band_ab3.log
-timeout -k 10 400 python -u scripts/probes/op_band_ab.py "h7:510:BTRIM=1" "s27:766:BTRIM=1" "s27:510:BAND=4,ZMIN=24,ZMAX=24,BTRIM=1:BAND=4,ZMIN=16,ZMAX=16,BTRIM=1" "s27:512:BAND=4,ZMIN=24,ZMAX=24,BTRIM=1:BAND=4,ZMIN=16,ZMAX=16,BTRIM=1" "h7:512:BTRIM=1" "s27:511:BAND=4,ZMIN=24,ZMAX=24,BTRIM=1:BAND=4,ZMIN=16,ZMAX=16,BTRIM=1" "s27:255:BAND=4,ZMIN=8,ZMAX=8,BTRIM=1:BAND=4,ZMIN=16,ZMAX=16,BTRIM=1" "s27:256:BAND=4,ZMIN=8,ZMAX=8,BTRIM=1" "h7:511" "h7:255" "h7:256" > gpurun_out/r04_op_unaligned.log 2>&1 || exit 1
+timeout -k 10 400 python -u scripts/probes/op_band_ab.py "h7:510:BTRIM=1" "s27:766:BTRIM=1" "s27:510:BAND=4,ZMIN=24,ZMAX=24,BTRIM=1:BAND=4,ZMIN=16,ZMAX=16,BTRIM=1" "s27:512:BAND=4,ZMIN=24,ZMAX=24,BTRIM=1:BAND=4,ZMIN=16,ZMAX=16,BTRIM=1" "h7:512:BTRIM=1" "s27:511:BAND=4,ZMIN=24,ZMAX=24,BTRIM=1:BAND=4,ZMIN=16,ZMAX=16,BTRIM=1" "s27:255:BAND=4,ZMIN=8,ZMAX=8,BTRIM=1:BAND=4,ZMIN=16,ZMAX=16,BTRIM=1" "s27:256:BAND=4,ZMIN=8,ZMAX=8,BTRIM=1" "s27:96x768:BAND=4,ZMIN=12,ZMAX=12,BTRIM=3:BAND=4,ZMIN=8,ZMAX=8,BTRIM=3:BAND=4,ZMIN=24,ZMAX=24,BTRIM=3" "h7:511" "h7:255" "h7:256" > gpurun_out/r04_op_unaligned.log 2>&1 || exit 1
 grep -v amdgpu.ids gpurun_out/r04_op_unaligned.log
 timeout -k 10 400 python -u scripts/probes/op_band_ab.py "s27:1024:BTRIM=1,ZMIN=32,ZMAX=32:BTRIM=3,ZMIN=32,ZMAX=32:BTRIM=3:BTRIM=3,ZMIN=16,ZMAX=16:BTRIM=1,ZMIN=32,ZMAX=32,BEDGE=0" "h7:768:BTRIM=1,BEDGE=0:BTRIM=1:BTRIM=3:BTRIM=3,ZMIN=16,ZMAX=16" > gpurun_out/r04_op_band_ab4.log 2>&1 || exit 1
 grep -v amdgpu.ids gpurun_out/r04_op_band_ab4.log
