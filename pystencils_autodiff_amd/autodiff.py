@@ -27,6 +27,7 @@ import collections
 from enum import Enum
 from typing import List
 
+import numpy as np
 import sympy as sp
 
 from ._adjoint_field import AdjointField
@@ -447,6 +448,16 @@ class AutoDiffOp:
         as in pystencils (ghost layers are then ignored; reads leaving the domain read zeros)."""
         from .backends.kernel_ir import StencilKernel
         ac = self._forward_assignments if which == 'forward' else self._backward_assignments
+        if ghost_layers not in (None, 0) and iteration_slice is None:
+            # pystencils' explicit ghost layers: k per axis, or (lower, upper) per axis -> iterate [lo, N - hi); the
+            # stencil's reads then stay inside the array for a radius up to the layer count, as pystencils' do
+            ndim = ac.main_assignments[0].lhs.field.spatial_dimensions
+            gl = [(int(ghost_layers), int(ghost_layers))] * ndim if isinstance(ghost_layers, (int, np.integer)) \
+                else [(int(g), int(g)) if isinstance(g, (int, np.integer)) else (int(g[0]), int(g[1]))
+                      for g in ghost_layers]
+            if len(gl) != ndim:
+                raise ValueError(f'ghost_layers {ghost_layers}: one entry per spatial axis ({ndim})')
+            iteration_slice = tuple(slice(lo, -hi if hi else None) for lo, hi in gl)
         bh = 'zeros' if ghost_layers == 0 else None
         return StencilKernel(ac, boundary_handling=bh, function_name=f"{self.op_name}_{which}_{target}_custom",
                              target=target, data_type=data_type, iteration_slice=iteration_slice,

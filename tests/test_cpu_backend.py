@@ -300,6 +300,23 @@ def test_create_kernel_iteration_slice(target, islice):
         op.create_forward_kernel(target, iteration_slice=(slice(0, None, 2),))
 
 
+@pytest.mark.parametrize('gl', [2, [(1, 2), 3, (2, 1)]])
+def test_create_kernel_explicit_ghost_layers(gl):
+    """create_forward_kernel(ghost_layers=k | per-axis (lower, upper)) like pystencils: the kernel writes
+    [lower, N - upper) per axis and leaves the rest."""
+    op = pa.AutoDiffOp(W.asym_7pt(), boundary_handling='zeros')
+    u = np.random.default_rng(4).uniform(-1, 1, (7, 8, 9)).astype(np.float32)
+    k = op.create_forward_kernel('cpu', ghost_layers=gl)
+    out = np.full_like(u, 5.0)
+    k(u=u, out=out)
+    gls = [(gl, gl)] * 3 if isinstance(gl, int) else [(g, g) if isinstance(g, int) else g for g in gl]
+    sl = tuple(slice(lo, n - hi) for (lo, hi), n in zip(gls, u.shape))
+    ref = OE.evaluate(op.forward_assignments, {'u': u}, boundary_handling='zeros')['out']
+    expect = np.full_like(u, 5.0)
+    expect[sl] = ref[sl]
+    assert_close_rel(out, expect, 1e-6, f'ghost_layers={gl}')
+
+
 @pytest.mark.parametrize('bmin', [0, 1 << 30])
 @pytest.mark.parametrize('builder', [W.asym_7pt, W.stencil_27pt])
 def test_interior_only_border_allocation(monkeypatch, bmin, builder):
