@@ -185,7 +185,9 @@ struct Exchange {
     bool loopback = false;                // one-rank communicator: both faces to itself (periodic z)
     // PSAD_SLAB_SYNC=value: the two cross-stream orderings as stream memory operations (hipStreamWriteValue32 /
     // hipStreamWaitValue32 on a signal-memory word with a sweep counter) instead of event record + wait (A/B)
-    uint32_t* sig = nullptr;              // [0] faces final (compute -> halo stream), [1] halos landed (halo -> compute)
+    // one HSA signal per ordering (signal memory is allocated 8 bytes at a time)
+    uint32_t* sig = nullptr;              // faces final (compute -> halo stream)
+    uint32_t* sig_halo = nullptr;         // halos landed (halo -> compute)
     mutable uint32_t seq = 0;
 };
 
@@ -252,8 +254,8 @@ void run_sweep(const Sweep& w, const std::vector<at::Tensor>& table, const std::
         for (const auto& f : w.faces) launch_on(f, table, scalars, ex.stream);
     if (w.has_inner) launch(w.inner, table, scalars, device);                // interior overlaps the exchange
     if (n && ex.sig) {
-        hip_ok(hipStreamWriteValue32(ex.stream, ex.sig + 1, ex.seq, 0), "hipStreamWriteValue32");
-        hip_ok(hipStreamWaitValue32(cur, ex.sig + 1, ex.seq, hipStreamWaitValueGte, 0xffffffffu),
+        hip_ok(hipStreamWriteValue32(ex.stream, ex.sig_halo, ex.seq, 0), "hipStreamWriteValue32");
+        hip_ok(hipStreamWaitValue32(cur, ex.sig_halo, ex.seq, hipStreamWaitValueGte, 0xffffffffu),
                "hipStreamWaitValue32");
     } else if (n) {
         hip_ok(hipEventRecord(ex.ev_halos, ex.stream), "hipEventRecord");
@@ -419,10 +421,14 @@ Sweep sweep_from(const py::object& inner, const py::list& faces, const py::tuple
         const char* sy = std::getenv("PSAD_SLAB_SYNC");
         if (sy != nullptr && std::string(sy) == "value") {
             void* p = nullptr;
-            hip_ok(hipExtMallocWithFlags(&p, 64, hipMallocSignalMemory), "hipExtMallocWithFlags");
-            hip_ok(hipMemset(p, 0, 64), "hipMemset");
+            void* q = nullptr;
+            hip_ok(hipExtMallocWithFlags(&p, 8, hipMallocSignalMemory), "hipExtMallocWithFlags");
+            hip_ok(hipExtMallocWithFlags(&q, 8, hipMallocSignalMemory), "hipExtMallocWithFlags");
+            hip_ok(hipMemset(p, 0, 8), "hipMemset");
+            hip_ok(hipMemset(q, 0, 8), "hipMemset");
             hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
             w.ex.sig = static_cast<uint32_t*>(p);
+            w.ex.sig_halo = static_cast<uint32_t*>(q);
         }
     }
     return w;
