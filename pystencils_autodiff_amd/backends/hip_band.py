@@ -63,18 +63,29 @@ def band_esize(ir):
     return np.dtype(ir.fields[0].dtype.numpy_dtype).itemsize
 
 
-def band_geometry(X, TY, R, D, es=2):
+def band_padded(X, es, pad):
+    """Padded image rows (``BPAD``): rows of a 16-byte multiple only."""
+    return bool(pad) and (X * es) % 16 == 0
+
+
+def band_geometry(X, TY, R, D, es=2, pad=0):
     """Launch / LDS geometry of a band of ``TY`` rows (``R`` per lane) on rows of ``X`` elements of ``es`` bytes.
-    Rows whose pitch is not a multiple of 16 bytes (``X % VE``) take ``ceil(X / VE)`` chunks, the last one partial."""
+    Rows whose pitch is not a multiple of 16 bytes (``X % VE``) take ``ceil(X / VE)`` chunks, the last one partial.
+    ``pad``: every image row is preceded by one zero 16-byte piece and the slot ends with one (x neighbours of a row's
+    end chunks read as zeros straight from LDS)."""
     VE = 16 // es
     CPR = -(-X // VE)
+    padded = band_padded(X, es, pad)
     # LDS image row pitch (elements, 16-byte multiple). Rows starting on half dwords (fp16, X odd) are loaded from the
     # dword at or below their start, one element early every other row: the image row then needs room for X + 2
-    XP = CPR * VE if (X * es) % 4 == 0 else VE * -(-(X + 2) // VE)
+    if padded:
+        XP = (CPR + 1) * VE
+    else:
+        XP = CPR * VE if (X * es) % 4 == 0 else VE * -(-(X + 2) // VE)
     G = TY // R
     ntask = G * CPR
     NCT = -(-ntask // 64) * 64
-    NPIECE = (TY + 2) * (XP // VE)
+    NPIECE = (TY + 2) * (XP // VE) + (1 if padded else 0)
     NI = -(-NPIECE // 64)
     SLOT = NI * 64 * VE
     NS = D + 1
@@ -82,12 +93,12 @@ def band_geometry(X, TY, R, D, es=2):
                 NS=NS, lds_bytes=(NS * SLOT + 64) * es)
 
 
-def _fits(X, TY, R, D, es=2):
-    g = band_geometry(X, TY, R, D, es)
+def _fits(X, TY, R, D, es=2, pad=0):
+    g = band_geometry(X, TY, R, D, es, pad)
     return g['ntask'] % 64 == 0 and g['NCT'] <= 960 and D * g['NI'] <= 63 and g['lds_bytes'] <= 80 * 1024
 
 
-def band_choice(X, nstore=1, es=2):
+def band_choice(X, nstore=1, es=2, pad=0):
     """(TY, R, D) for rows of X elements, or None. fp16, measured (scripts/probes/band_ab.py,
     profiles/r03_band_ab*.log): 8-row bands of 4 rows per lane with 2 planes in flight at X = 768 and 1024
     (27-point 1024³: 0.895 ms vs 0.921 for 4-row bands of 2 rows per lane, 3 planes in flight); three workgroups
@@ -100,7 +111,7 @@ def band_choice(X, nstore=1, es=2):
     cands = [(8, 4, 2), (4, 2, 3), (8, 2, 3)] if es == 2 else [(4, 4, 2), (8, 4, 2), (4, 2, 2), (8, 2, 2)]
     cands += [(12, 4, 2), (16, 4, 2), (16, 2, 2), (32, 4, 2), (32, 2, 2)]
     for TY, R, D in cands:
-        if R <= rmax and _fits(X, TY, R, D, es):
+        if R <= rmax and _fits(X, TY, R, D, es, pad):
             return TY, R, D
     return None
 
@@ -115,7 +126,8 @@ def emit_band(ir, name, cfg):
     es = band_esize(ir)
     X = cfg.BX
     TY, R, D = cfg.BTY, cfg.BAND, cfg.D
-    g = band_geometry(X, TY, R, D, es)
+    padded = band_padded(X, es, cfg.BPAD)
+    g = band_geometry(X, TY, R, D, es, padded)
     VE, CPR, G, NCT, NT, NPIECE, NI, SLOT, NS = (g[k] for k in ('VE', 'CPR', 'G', 'NCT', 'NT', 'NPIECE', 'NI', 'SLOT',
                                                                  'NS'))
     assert D * NI <= 63 and NCT <= 960, (X, TY, R, D)
@@ -125,7 +137,8 @@ def emit_band(ir, name, cfg):
     et = '_Float16' if half else 'float'            # storage element type
     XP = g['XP']                                    # row pitch in the LDS image (elements)
     NPR = XP // VE                                  # pieces per image row
-    bu = XP != X                                    # rows not a multiple of 16 bytes: row-wise pieces, zero fill
+    bu = not padded and XP != X                     # rows not a multiple of 16 bytes: row-wise pieces, zero fill
+    c0 = VE if padded else 0                        # image column of a row's first element
     bo = (X * es) % 4 != 0                          # rows on half dwords (fp16, X odd): realigned in registers
     assert not bu or cfg.BMASK, 'rows of a partial last chunk need the masked stores'
     pr = KernelExprPrinter('float', dict(ir.symbol_names))
@@ -193,7 +206,13 @@ def emit_band(ir, name, cfg):
     L.append('    #pragma unroll')
     L.append(f'    for (int i = 0; i < {NI}; ++i) {{')
     L.append('      const int k = i * 64 + lane;')
-    if not bu:
+    if padded:
+        # image row rr = one zero piece (out of range: the DMA writes zeros) + the row's pieces; one zero piece ends
+        # the slot (the right neighbour of the last row's end)
+        L.append(f'      const int rr = k / {NPR}, pc = k - rr * {NPR}, yy = y0 - 1 + rr;')
+        L.append(f'      vo[i] = (pc > 0 && rr < {TY + 2} && yy >= 0 && yy < Y) ? (yy * {X * es} + 16 * (pc - 1)) : '
+                 '0x7ffffff0;')
+    elif not bu:
         L.append(f'      vo[i] = k < {NPIECE} ? ((y0 - 1) * {X * es} + 16 * k) : 0x7ffffff0;   // row -1 / past Y: range '
                  'check')
     elif not bo:
@@ -273,7 +292,7 @@ def emit_band(ir, name, cfg):
     L.append(f'  const bool active = ctid < {g["ntask"]};')
     L.append(f'  const int t = active ? ctid : {g["ntask"] - 1};')
     L.append(f'  const int grp = t / {CPR}, col = t - grp * {CPR};')
-    L.append(f'  const int lofs = grp * {R * XP} + col * {VE};          // slot row grp*R = input row y0 + grp*R - 1')
+    L.append(f'  const int lofs = grp * {R * XP} + {c0} + col * {VE};   // slot row grp*R = input row y0 + grp*R - 1')
     L.append(f'  const int x = col * {VE};')
     L.append(f'  const bool lmask = col == 0, rmask = col == {CPR - 1};')
     if cfg.BMASK:
@@ -290,7 +309,9 @@ def emit_band(ir, name, cfg):
     L.append("  // column 0 (x boundary, masked) reads its own first dword instead of the one before the slot.")
     dw = 4 // es                                          # elements per dword
     # dword targets relative to the wave's block (64 chunks of 4 dwords): -1, 0 .. 30 | 33 .. 63, 256
-    if cfg.BEDGE:
+    if padded:
+        pass                                              # x neighbours read from the image (zero pads at row ends)
+    elif cfg.BEDGE:
         L.append(f'  const int eoff = {dw} * (lane == 0 ? (col == 0 ? 0 : -1) : (lane == 63 ? 256 : (lane < 32 ? lane - 1 '
                  f': lane + 1))) - {VE} * lane;')
     else:
@@ -324,6 +345,22 @@ def emit_band(ir, name, cfg):
                   'P2 = {(float)w1[0], (float)w3[0]};',
                   f'{ind}    const f32x2 P3 = {{(float)w1[1], (float)w3[1]}}, P4 = {{(float)w2[0], (float)w4[0]}}, '
                   'P5 = {(float)w2[1], (float)rr};']
+            return B
+        if padded:
+            # the dwords left and right of the lane's chunk straight from the image (a row's end chunks meet the zero
+            # pads): no DPP, no boundary selects (one ds_read2_b32 per row)
+            B += [f'{ind}    const unsigned el = *(const unsigned*)(rp - {dw}), er = *(const unsigned*)(rp + {VE});']
+            if half:
+                B += [f'{ind}    const f16x8 v = *(const f16x8*)rp;',
+                      f'{ind}    const _Float16 l = __builtin_bit_cast(f16x2, el)[1], rr = __builtin_bit_cast(f16x2, er)[0];',
+                      f'{ind}    const f32x2 P0 = {{(float)l, (float)v[3]}}, P1 = {{(float)v[0], (float)v[4]}}, '
+                      'P2 = {(float)v[1], (float)v[5]};',
+                      f'{ind}    const f32x2 P3 = {{(float)v[2], (float)v[6]}}, P4 = {{(float)v[3], (float)v[7]}}, '
+                      'P5 = {(float)v[4], (float)rr};']
+            else:
+                B += [f'{ind}    const f32x4 v = *(const f32x4*)rp;',
+                      f'{ind}    const float H0 = __builtin_bit_cast(float, el), H5 = __builtin_bit_cast(float, er);',
+                      f'{ind}    const float H1 = v.x, H2 = v.y, H3 = v.z, H4 = v.w;']
             return B
         if half:
             B += [f'{ind}    const f16x8 v = *(const f16x8*)rp;',

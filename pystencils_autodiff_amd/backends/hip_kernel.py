@@ -31,19 +31,27 @@ BAND_ZC_BOX, BAND_ZC_STAR = 48, 8
 # without the taps of outputs before it (BTRIM=1) — 27-point 768³ 0.744 vs 0.768 ms, 1024³ 16-row bands 1.718 vs 1.744
 # (and 1.679 with 32-plane chunks), fp16 7-point 768³ 0.602 vs 0.626
 BAND_ZC_BOX16 = 32
-BAND_TRIM_DEFAULT = 1
-BAND_MIN_WG = 1024
+# round 4 (profiles/r04_op_band_ab3.log .. _ab5.log): both chunk ends peeled at a compile-time chunk length (BTRIM=3)
+# — 27-point 768³ 0.715 vs 0.724 ms (BTRIM=1), 1024³ 1.617 vs 1.640, fp16 7-point 768³ 0.594 vs 0.595-0.633
+BAND_TRIM_DEFAULT = 3
+# box-stencil chunk length: the longest of BAND_ZC_BOX_LADDER that still gives BAND_ROUND_WG workgroups (one
+# round of three per CU; profiles/r04_op_zc_sweep.log): 27-point 512³ 32 planes 0.209 ms vs 16 0.243, 8 0.235;
+# 256³ 8 planes 0.028 vs 11 0.036, 16 0.045; a 96×768² slab 12 planes 0.091 vs 8 0.095, 24 0.109
+BAND_ZC_BOX_LADDER = (48, 32, 24, 16, 12, 8)
+BAND_ROUND_WG = 768
+BAND_MIN_WG = 768
 # fp32 storage (4 cells per 16-byte chunk) measured slower through the op (7-point 512³ 0.387 vs 0.373 ms, 768³
 # 1.325 vs 1.261): opt-in only (BAND=R)
 BAND_F32_MAX_X = 0
 BAND_TRIM = BAND_TRIM_DEFAULT
+BAND_PAD = 0
 
 # gpu_indexing_params keys of pystencils' own GPU indexing (``block_size``, ``maximum_block_size``, …, e.g.
 # ``gpu_indexing_params={'block_size': (8, 4, 2)}`` in the reference's tests/test_graph_datahandling.py:70): they
 # describe a one-thread-per-cell launch these schedules do not have, so they are accepted and ignored. Upper-case
 # keys are this layer's tile parameters; an unknown one is a typo and raises.
 TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
-             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE', 'BLDR', 'BLAUX')
+             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE', 'BLDR', 'BLAUX', 'BPAD')
 
 
 def _band_config(ir, ve, shape, over):
@@ -78,17 +86,31 @@ def _band_config(ir, ve, shape, over):
         R = int(over['BAND'])
     TY = int(over.get('BTY', TY if TY % R == 0 else R * max(1, TY // R)))
     D = int(over.get('D', D))
-    g = band_geometry(X, TY, R, D, es)
+    pad = int(over.get('BPAD', BAND_PAD))
+    g = band_geometry(X, TY, R, D, es, pad)
     if TY % R or g['NCT'] > 960 or D * g['NI'] > 63 or g['lds_bytes'] > 160 * 1024:
         raise ValueError(f'band schedule: BTY={TY} BAND={R} D={D} do not fit rows of {X} elements')
-    zc = int(over.get('ZMIN', (BAND_ZC_BOX16 if TY == 16 else BAND_ZC_BOX) if ntaps > 12 else BAND_ZC_STAR))
-    if 'BAND' not in over and -(-int(shape[-2]) // TY) * -(-int(shape[0]) // zc) < BAND_MIN_WG:
+    nty, Z = -(-int(shape[-2]) // TY), int(shape[0])
+    if ntaps <= 12:
+        zc = BAND_ZC_STAR
+    elif TY == 16:
+        zc = BAND_ZC_BOX16
+    else:
+        zc = next((c for c in BAND_ZC_BOX_LADDER if nty * -(-Z // c) >= BAND_ROUND_WG), BAND_ZC_BOX_LADDER[-1])
+    zc = int(over.get('ZMIN', zc))
+    if 'BAND' not in over and nty * -(-Z // zc) < BAND_MIN_WG:
         return None
+    zmax = int(over.get('ZMAX', zc))
+    btrim = int(over.get('BTRIM', BAND_TRIM))
+    if btrim == 3 and (zmax != zc or zc < 3):
+        if 'BTRIM' in over:
+            raise ValueError('band schedule: BTRIM=3 needs ZMIN == ZMAX >= 3')
+        btrim = 1                       # chunk length not fixed at compile time: peel the chunk's first planes only
     return MarchConfig(VE=ve, BAND=R, BTY=TY, BX=X, D=D, ZSUM=True, NT_STORE=True, ZMIN=zc,
-                       ZMAX=int(over.get('ZMAX', zc)), BLK=int(over.get('BLK', 512)), MAP=int(over.get('MAP', 0)),
-                       BTRIM=int(over.get('BTRIM', BAND_TRIM)), BEDGE=int(over.get('BEDGE', 1)),
+                       ZMAX=zmax, BLK=int(over.get('BLK', 512)), MAP=int(over.get('MAP', 0)),
+                       BTRIM=btrim, BEDGE=int(over.get('BEDGE', 1)),
                        BSTAG=int(over.get('BSTAG', 0)), BWPE=int(over.get('BWPE', 0)), BLDR=int(over.get('BLDR', 0)),
-                       BLAUX=int(over.get('BLAUX', 0)))
+                       BLAUX=int(over.get('BLAUX', 0)), BPAD=pad)
 
 
 def default_march_config(ir, ve, shape=None, tuning=None, band=True):
@@ -730,7 +752,7 @@ class HipStencilKernel:
                                           'nty')]
         kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics) + \
             [self._scalar_kind()] * len(ir.scalars)
-        block = ws['block'] if ws else (band_geometry(cfg.BX, cfg.BTY, cfg.BAND, cfg.D, esize)['NT'] if cfg.BAND else
+        block = ws['block'] if ws else (band_geometry(cfg.BX, cfg.BTY, cfg.BAND, cfg.D, esize, cfg.BPAD)['NT'] if cfg.BAND else
                                         cfg.NT)
         return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics, xb=cfg.XB, block=block)
 

@@ -183,8 +183,8 @@ struct Exchange {
     std::vector<size_t> bytes;
     int peer_lo = -1, peer_hi = -1;
     bool loopback = false;                // one-rank communicator: both faces to itself (periodic z)
-    // PSAD_SLAB_SYNC=value: the two cross-stream orderings as stream memory operations (hipStreamWriteValue32 /
-    // hipStreamWaitValue32 on a signal-memory word with a sweep counter) instead of event record + wait (A/B)
+    // the two cross-stream orderings as stream memory operations (hipStreamWriteValue32 / hipStreamWaitValue32 on a
+    // signal-memory word with a sweep counter; PSAD_SLAB_SYNC=event: event record + wait instead)
     // one HSA signal per ordering (signal memory is allocated 8 bytes at a time)
     uint32_t* sig = nullptr;              // faces final (compute -> halo stream)
     uint32_t* sig_halo = nullptr;         // halos landed (halo -> compute)
@@ -398,8 +398,11 @@ Sweep sweep_from(const py::object& inner, const py::list& faces, const py::tuple
     w.ex.peer_lo = ex[5].cast<int>();
     w.ex.peer_hi = ex[6].cast<int>();
     w.ex.loopback = ex[7].cast<bool>();
-    const char* fo = std::getenv("PSAD_SLAB_FACES");      // 'halo': faces on the halo stream (A/B, probes)
-    w.faces_on_halo = fo != nullptr && std::string(fo) == "halo";
+    // face launches on the halo stream right behind the exchange (default; 'compute': after the interior on the
+    // compute stream). Loopback proxy, one MI355X (profiles/r04_slab_sync_ab.log): 27-point 96x768^2 fp16 0.120 vs
+    // 0.128-0.132 ms per step, 7-point 128x1024^2 fp32 0.398 vs 0.419 (with the stream-memory-op sync below)
+    const char* fo = std::getenv("PSAD_SLAB_FACES");
+    w.faces_on_halo = !(fo != nullptr && std::string(fo) == "compute");
     const size_t n = w.ex.slot.size();
     TORCH_CHECK(w.ex.last_off.size() == n && w.ex.recv_lo.size() == n && w.ex.recv_hi.size() == n &&
                     w.ex.bytes.size() == n, "psad: exchange spec lengths differ");
@@ -418,8 +421,10 @@ Sweep sweep_from(const py::object& inner, const py::list& faces, const py::tuple
         TORCH_CHECK(w.ex.comm != nullptr, "psad: exchange without a communicator");
         hip_ok(hipEventCreateWithFlags(&w.ex.ev_faces, hipEventDisableTiming), "hipEventCreateWithFlags");
         hip_ok(hipEventCreateWithFlags(&w.ex.ev_halos, hipEventDisableTiming), "hipEventCreateWithFlags");
+        // the two cross-stream orderings as stream memory operations on signal memory (default) or, with
+        // PSAD_SLAB_SYNC=event, event record + wait
         const char* sy = std::getenv("PSAD_SLAB_SYNC");
-        if (sy != nullptr && std::string(sy) == "value") {
+        if (!(sy != nullptr && std::string(sy) == "event")) {
             void* p = nullptr;
             void* q = nullptr;
             hip_ok(hipExtMallocWithFlags(&p, 8, hipMallocSignalMemory), "hipExtMallocWithFlags");

@@ -61,12 +61,18 @@ def test_band_choice_and_geometry():
         assert g['ntask'] % 64 == 0 and g['NCT'] <= 960 and D * g['NI'] <= 63 and g['lds_bytes'] <= 80 * 1024
 
 
-@pytest.mark.parametrize('shape,expect', [((768, 768, 768), 4), ((1024, 1024, 1024), 4), ((96, 768, 768), 0),
-                                          ((64, 256, 256), 0), ((40, 40, 264), 0), ((512, 1024, 1024), 4)])
-def test_band_default_selection(shape, expect):
+@pytest.mark.parametrize('shape,expect,zc', [((768, 768, 768), 4, 48), ((1024, 1024, 1024), 4, 32),
+                                             ((96, 768, 768), 4, 12), ((512, 512, 512), 4, 32), ((256, 256, 256), 4, 8),
+                                             ((255, 255, 255), 4, 8), ((64, 256, 256), 0, 0), ((40, 40, 264), 0, 0),
+                                             ((512, 1024, 1024), 4, 48)])
+def test_band_default_selection(shape, expect, zc):
+    """Box stencils: the band schedule with the longest chunk of the ladder that still fills one round of three
+    workgroups per CU (BAND_ROUND_WG), both chunk ends peeled at that compile-time length (BTRIM=3)."""
     op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
     cfg = default_march_config(HipStencilKernel(_kernel(op.forward_assignments)).ir, 8, shape)
     assert cfg.BAND == expect, cfg
+    if expect:
+        assert cfg.ZMIN == cfg.ZMAX == zc and cfg.BTRIM == 3, cfg
     # overrides of the zsum tile (or BAND=0) keep the zsum schedule
     cfg = default_march_config(HipStencilKernel(_kernel(op.forward_assignments)).ir, 8, shape, {'BAND': 0})
     assert cfg.BAND == 0
@@ -82,7 +88,8 @@ def test_band_sources_compile():
         for c in (cfg, MarchConfig(**{**cfg.__dict__, 'BMASK': True}),
                   MarchConfig(**{**cfg.__dict__, 'BMASK': True, 'XB': True}),
                   MarchConfig(**{**cfg.__dict__, 'BTRIM': 1}), MarchConfig(**{**cfg.__dict__, 'BTRIM': 2}),
-                  MarchConfig(**{**cfg.__dict__, 'BTRIM': 3, 'ZMIN': 16, 'ZMAX': 16})):
+                  MarchConfig(**{**cfg.__dict__, 'BTRIM': 3, 'ZMIN': 16, 'ZMAX': 16}),
+                  MarchConfig(**{**cfg.__dict__, 'BPAD': 1}), MarchConfig(**{**cfg.__dict__, 'BPAD': 1, 'BMASK': True})):
             src, kname = hk.source(('march', c))
             assert kname.endswith('_band') and 'band schedule' in src
             assert len(rt.compile_hip(src)) > 0
@@ -106,6 +113,20 @@ def test_band_vs_oracle(case, shape, bh):
     """Forward and adjoint sweeps on the band schedule vs the float64 oracle; Y not a multiple of the band height
     (ragged last band) and interior-only stores take the masked variant; rows whose pitch is not a multiple of 16
     bytes (``test_band_unaligned_vs_oracle``) load row-wise pieces and store a partial last chunk."""
+    _band_vs_oracle(case, shape, bh)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', CASES, ids=lambda c: c[0])
+@pytest.mark.parametrize('shape', [(9, 21, 256), (7, 16, 768)])
+@pytest.mark.parametrize('bh', ['zeros', None])
+def test_band_padded_rows_vs_oracle(case, shape, bh):
+    """Zero-padded LDS image rows (``BPAD=1``: x neighbours of every chunk read from the image, row ends meet the
+    zero pads) vs the oracle, forward and adjoint, whole and masked stores."""
+    _band_vs_oracle(case, shape, bh, BPAD=1)
+
+
+def _band_vs_oracle(case, shape, bh, **extra):
     torch = _torch()
     op = pa.AutoDiffOp(case[1](), boundary_handling=bh)
     rng = np.random.default_rng(sum(shape))
@@ -115,14 +136,14 @@ def test_band_vs_oracle(case, shape, bh):
         choice = band_choice(shape[-1], 1, dt.itemsize)
         if choice is None:
             pytest.skip(f'no band geometry for rows of {shape[-1]} {dt}')
-        k = _kernel(ac, bh, f'band_{which}', BAND=choice[1]).compile()
+        k = _kernel(ac, bh, f'band_{which}', BAND=choice[1], **extra).compile()
         ins = {f.name: rng.uniform(-1, 1, shape).astype(dt) for f in k.ir.fields_read}
         ref = OE.evaluate(ac, {n: a.astype(np.float64) for n, a in ins.items()}, boundary_handling=bh)
         outs = {f.name: torch.zeros(shape, dtype=getattr(torch, dt.name), device='cuda') for f in k.ir.fields_written}
         k(**{n: torch.from_numpy(a).cuda() for n, a in ins.items()}, **outs)
         torch.cuda.synchronize()
         cfg = k.last_variant[1]
-        assert k.last_variant[0] == 'march' and cfg.BAND > 0, cfg
+        assert k.last_variant[0] == 'march' and cfg.BAND > 0 and cfg.BPAD == extra.get('BPAD', cfg.BPAD), cfg
         whole = bh == 'zeros' and shape[1] % cfg.BTY == 0 and shape[2] % (16 // dt.itemsize) == 0
         assert cfg.BMASK == (not whole), cfg
         assert cfg.BXW == (cfg.BMASK and bh == 'zeros'), cfg          # x range = whole rows: no read-modify-write
@@ -203,7 +224,10 @@ def test_band_chunk_length_and_band_height_bitwise():
                 # both chunk ends peeled with a compile-time chunk length (ragged chunks: the BTRIM=1 path)
                 {'BAND': 4, 'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13}, {'BAND': 4, 'BTRIM': 3, 'ZMIN': 37, 'ZMAX': 37},
                 {'BAND': 4, 'BTRIM': 3, 'ZMIN': 3, 'ZMAX': 3},
-                {'BAND': 4, 'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13, 'BLDR': 1}):   # the loader role rotating over waves
+                {'BAND': 4, 'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13, 'BLDR': 1},    # the loader role rotating over waves
+                # zero-padded image rows: x neighbours from LDS instead of DPP, the same values in the same FMAs
+                {'BAND': 4, 'BPAD': 1}, {'BAND': 4, 'BPAD': 1, 'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13},
+                {'BAND': 4, 'BPAD': 1, 'BTY': 12}):
         k = _kernel(op.forward_assignments, 'zeros', 'bandc', **tun).compile()
         out = torch.full_like(u, float('nan'))
         k(u=u, out=out)
