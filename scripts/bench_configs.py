@@ -294,6 +294,13 @@ def main():
         ('veclaplace7_f32_384^3x3', lambda: W.vector_laplace_7pt(), (384, 384, 384, 3), torch.float32, 'zeros', 1,
          24, 24),
     ]
+    # row pitch: extents that are not a multiple of 16 bytes next to their power-of-two neighbours (VERDICT r03 item
+    # 5: within 15 %)
+    for n in (510, 512):
+        cfgs.append((f'pitch_diffusion7_f16_{n}^3', lambda: W.diffusion_7pt(dtype='float16'), (n, n, n), torch.float16,
+                     'zeros', 1, 4, 4))
+    for n in (255, 256, 511, 512):
+        cfgs.append((f'pitch_stencil27_f16_{n}^3', lambda: W.stencil_27pt(), (n, n, n), torch.float16, 'zeros', 1, 4, 4))
     if not only or 'readme_op_f32_20x30_cpu' in only:
         run_cpu('readme_op_f32_20x30_cpu', W.readme_op, (20, 30), None, 2)
     for name, b, shape, dt, bh, nin, bf, bb in cfgs:
