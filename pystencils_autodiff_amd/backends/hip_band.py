@@ -141,6 +141,7 @@ def emit_band(ir, name, cfg):
     c0 = VE if padded else 0                        # image column of a row's first element
     bo = (X * es) % 4 != 0                          # rows on half dwords (fp16, X odd): realigned in registers
     assert not bu or cfg.BMASK, 'rows of a partial last chunk need the masked stores'
+    czf = bu and not cfg.BZF                        # BZF=0: the first element past a row zeroed in registers
     pr = KernelExprPrinter('float', dict(ir.symbol_names))
     W = []
     for pl in plans:
@@ -258,7 +259,7 @@ def emit_band(ir, name, cfg):
     for a in range(D):
         L.append(f'        case {a}: asm volatile("s_waitcnt vmcnt({a * NI})" ::: "memory"); break;')
     L.append('      }')
-    if bo:
+    if bo and not czf:
         # plane j has landed: zeros over the image columns past each row's last element (X + the row's parity .. XP)
         nz = XP - X
         L.append('      {')
@@ -270,7 +271,7 @@ def emit_band(ir, name, cfg):
         L.append('        }')
         L.append('        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
         L.append('      }')
-    elif bu:
+    elif bu and not czf:
         # plane j has landed: zeros over the image columns X .. XP of every row (the straddling last piece brought
         # the next row's first elements), which the row's last cells read as their right neighbours
         ndw = (XP - X) * es // 4
@@ -328,19 +329,23 @@ def emit_band(ir, name, cfg):
             # image row r starts one element early when the input row starts on an odd element: realign the lane's
             # 10 elements x-1 .. x+8 as five dwords (v_perm over adjacent dwords; selector per row and plane parity)
             sel = 'selA' if r % 2 else 'selB'
+            cq = '' if czf else 'const '
             B += [f'{ind}    const u32x4 d = *(const u32x4*)rp;',
                   f'{ind}    const unsigned e = *(const unsigned*)(rp + eoff);',
                   f'{ind}    const unsigned lw = __builtin_amdgcn_update_dpp(e, d.w, 0x138, 0xf, 0xf, false);   // wave_shr:1',
                   f'{ind}    const unsigned rw = __builtin_amdgcn_update_dpp(e, d.x, 0x130, 0xf, 0xf, false);   // wave_shl:1',
-                  f'{ind}    const f16x2 w0 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.x, lw, {sel})), '
+                  f'{ind}    {cq}f16x2 w0 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.x, lw, {sel})), '
                   f'w1 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.y, d.x, {sel}));',
-                  f'{ind}    const f16x2 w2 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.z, d.y, {sel})), '
+                  f'{ind}    {cq}f16x2 w2 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.z, d.y, {sel})), '
                   f'w3 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.w, d.z, {sel}));',
                   # the row's last chunk: x+7 and x+8 both lie at or past X (8·CPR - 1 >= X for odd X) and on a row
                   # loaded one element early both come from the next lane, which may hold another row: zeros
                   f'{ind}    const f16x2 w4 = rmask ? (f16x2)((_Float16)0) : '
                   f'__builtin_bit_cast(f16x2, __builtin_amdgcn_perm(rw, d.w, {sel}));',
                   f'{ind}    const _Float16 l = lmask ? (_Float16)0 : w0[0], rr = w4[1];',
+                  *([f'{ind}    w{(X % VE + 1) // 2}[0] = rmask ? (_Float16)0 : w{(X % VE + 1) // 2}[0];   '
+                     '// the first element past the row end (no loader zero fill)']
+                    if czf and (X % VE + 1) // 2 < 4 else []),
                   f'{ind}    const f32x2 P0 = {{(float)l, (float)w2[0]}}, P1 = {{(float)w0[1], (float)w2[1]}}, '
                   'P2 = {(float)w1[0], (float)w3[0]};',
                   f'{ind}    const f32x2 P3 = {{(float)w1[1], (float)w3[1]}}, P4 = {{(float)w2[0], (float)w4[0]}}, '
@@ -362,11 +367,15 @@ def emit_band(ir, name, cfg):
                       f'{ind}    const float H0 = __builtin_bit_cast(float, el), H5 = __builtin_bit_cast(float, er);',
                       f'{ind}    const float H1 = v.x, H2 = v.y, H3 = v.z, H4 = v.w;']
             return B
-        if half:
-            B += [f'{ind}    const f16x8 v = *(const f16x8*)rp;',
+        vt = 'f16x8' if half else 'f32x4'
+        if czf:
+            # the last chunk's element X % VE is the next row's first (no loader zero fill): zero, as the right
+            # neighbour of cell X-1
+            B += [f'{ind}    {vt} v = *(const {vt}*)rp;',
+                  f'{ind}    v[{X % VE}] = rmask ? ({et})0 : v[{X % VE}];',
                   f'{ind}    const u32x4 d = __builtin_bit_cast(u32x4, v);']
         else:
-            B += [f'{ind}    const f32x4 v = *(const f32x4*)rp;',
+            B += [f'{ind}    const {vt} v = *(const {vt}*)rp;',
                   f'{ind}    const u32x4 d = __builtin_bit_cast(u32x4, v);']
         B += [f'{ind}    const unsigned e = *(const unsigned*)(rp + eoff);',
               f'{ind}    const unsigned lw = __builtin_amdgcn_update_dpp(e, d.w, 0x138, 0xf, 0xf, false);   // wave_shr:1',

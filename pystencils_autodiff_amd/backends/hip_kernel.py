@@ -40,18 +40,25 @@ BAND_TRIM_DEFAULT = 3
 BAND_ZC_BOX_LADDER = (48, 32, 24, 16, 12, 8)
 BAND_ROUND_WG = 768
 BAND_MIN_WG = 768
+# star stencils: 8-plane chunks, but 64-plane chunks on rows of <= 512 elements when that still gives >= 512
+# workgroups (profiles/r04_op_zc_sweep.log, _ab6.log): fp16 7-point 512³ 0.184 vs 0.197 ms, 510³ 0.204 vs 0.229;
+# 768³ keeps 8 (0.629 vs 0.675 at 96 planes, 0.699 at 64), 256³ too (0.024 vs 0.038 at 32)
+BAND_ZC_STAR_LONG, BAND_STAR_LONG_MAX_X, BAND_STAR_LONG_MIN_WG = 64, 512, 512
 # fp32 storage (4 cells per 16-byte chunk) measured slower through the op (7-point 512³ 0.387 vs 0.373 ms, 768³
 # 1.325 vs 1.261): opt-in only (BAND=R)
 BAND_F32_MAX_X = 0
 BAND_TRIM = BAND_TRIM_DEFAULT
-BAND_PAD = 0
+# zero-padded image rows (x neighbours read from LDS, no DPP / boundary selects) for box stencils
+# (profiles/r04_op_band_ab6.log): 27-point 768³ 0.699 vs 0.715 ms, 1024³ 1.581 vs 1.603, 512³ 0.198 vs 0.201;
+# fp16 7-point 768³ 0.631 vs 0.629, 1024³ 1.444 vs 1.438 (not for star stencils)
+BAND_PAD_BOX = 1
 
 # gpu_indexing_params keys of pystencils' own GPU indexing (``block_size``, ``maximum_block_size``, …, e.g.
 # ``gpu_indexing_params={'block_size': (8, 4, 2)}`` in the reference's tests/test_graph_datahandling.py:70): they
 # describe a one-thread-per-cell launch these schedules do not have, so they are accepted and ignored. Upper-case
 # keys are this layer's tile parameters; an unknown one is a typo and raises.
 TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
-             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE', 'BLDR', 'BLAUX', 'BPAD')
+             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE', 'BLDR', 'BLAUX', 'BPAD', 'BZF')
 
 
 def _band_config(ir, ve, shape, over):
@@ -86,13 +93,14 @@ def _band_config(ir, ve, shape, over):
         R = int(over['BAND'])
     TY = int(over.get('BTY', TY if TY % R == 0 else R * max(1, TY // R)))
     D = int(over.get('D', D))
-    pad = int(over.get('BPAD', BAND_PAD))
+    pad = int(over.get('BPAD', BAND_PAD_BOX if ntaps > 12 else 0))
     g = band_geometry(X, TY, R, D, es, pad)
     if TY % R or g['NCT'] > 960 or D * g['NI'] > 63 or g['lds_bytes'] > 160 * 1024:
         raise ValueError(f'band schedule: BTY={TY} BAND={R} D={D} do not fit rows of {X} elements')
     nty, Z = -(-int(shape[-2]) // TY), int(shape[0])
     if ntaps <= 12:
-        zc = BAND_ZC_STAR
+        long_ok = X <= BAND_STAR_LONG_MAX_X and nty * -(-Z // BAND_ZC_STAR_LONG) >= BAND_STAR_LONG_MIN_WG
+        zc = BAND_ZC_STAR_LONG if long_ok else BAND_ZC_STAR
     elif TY == 16:
         zc = BAND_ZC_BOX16
     else:
@@ -110,7 +118,7 @@ def _band_config(ir, ve, shape, over):
                        ZMAX=zmax, BLK=int(over.get('BLK', 512)), MAP=int(over.get('MAP', 0)),
                        BTRIM=btrim, BEDGE=int(over.get('BEDGE', 1)),
                        BSTAG=int(over.get('BSTAG', 0)), BWPE=int(over.get('BWPE', 0)), BLDR=int(over.get('BLDR', 0)),
-                       BLAUX=int(over.get('BLAUX', 0)), BPAD=pad)
+                       BLAUX=int(over.get('BLAUX', 0)), BPAD=pad, BZF=int(over.get('BZF', 1)))
 
 
 def default_march_config(ir, ve, shape=None, tuning=None, band=True):
