@@ -515,7 +515,12 @@ def emit_band(ir, name, cfg):
         sp, s0, sn = (k + 2) % 3, k, (k + 1) % 3
         sets = {'full': ((sp, 1), (s0, 0), (sn, -1)), 'p0': ((sn, -1),), 'p1': ((s0, 0), (sn, -1)),
                 'e0': ((sp, 1), (s0, 0)), 'e1': ((sp, 1),)}[part]
-        B = [f'{ind}if ({guard}) {{' if guard else f'{ind}{{', f'{ind}  __syncthreads();',
+        # the plane barrier as one asm statement with a memory clobber: the previous plane's LDS reads complete
+        # (lgkmcnt) before it and none of them moves past it, none of this plane's moves above it (with
+        # __syncthreads() hipcc 7.2 sank a peeled step's reads below the next step's barrier on the padded-row
+        # image: the loader had already refilled that slot; scripts/probes/band_determinism.py)
+        B = [f'{ind}if ({guard}) {{' if guard else f'{ind}{{',
+             f'{ind}  asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");',
              f'{ind}  const {et}* sl = lds + (jj % {NS}) * {SLOT} + lofs;']
         if bo:
             # v_perm selectors: input row parity = plane parity ^ (y0 - 1 + row) & 1, y0 and R even -> odd rows r of
