@@ -98,15 +98,17 @@ def _band_config(ir, ve, shape, over):
     if TY % R or g['NCT'] > 960 or D * g['NI'] > 63 or g['lds_bytes'] > 160 * 1024:
         raise ValueError(f'band schedule: BTY={TY} BAND={R} D={D} do not fit rows of {X} elements')
     nty, Z = -(-int(shape[-2]) // TY), int(shape[0])
+    min_wg = BAND_MIN_WG
     if ntaps <= 12:
         long_ok = X <= BAND_STAR_LONG_MAX_X and nty * -(-Z // BAND_ZC_STAR_LONG) >= BAND_STAR_LONG_MIN_WG
         zc = BAND_ZC_STAR_LONG if long_ok else BAND_ZC_STAR
+        min_wg = BAND_STAR_LONG_MIN_WG if long_ok else BAND_MIN_WG
     elif TY == 16:
         zc = BAND_ZC_BOX16
     else:
         zc = next((c for c in BAND_ZC_BOX_LADDER if nty * -(-Z // c) >= BAND_ROUND_WG), BAND_ZC_BOX_LADDER[-1])
     zc = int(over.get('ZMIN', zc))
-    if 'BAND' not in over and nty * -(-Z // zc) < BAND_MIN_WG:
+    if 'BAND' not in over and nty * -(-Z // zc) < min_wg:
         return None
     zmax = int(over.get('ZMAX', zc))
     btrim = int(over.get('BTRIM', BAND_TRIM))
