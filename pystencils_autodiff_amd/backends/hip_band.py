@@ -68,14 +68,16 @@ def band_padded(X, es, pad):
     return bool(pad) and (X * es) % 16 == 0
 
 
-def band_geometry(X, TY, R, D, es=2, pad=0):
+def band_geometry(X, TY, R, D, es=2, pad=0, reg=0):
     """Launch / LDS geometry of a band of ``TY`` rows (``R`` per lane) on rows of ``X`` elements of ``es`` bytes.
     Rows whose pitch is not a multiple of 16 bytes (``X % VE``) take ``ceil(X / VE)`` chunks, the last one partial.
     ``pad``: every image row is preceded by one zero 16-byte piece and the slot ends with one (x neighbours of a row's
-    end chunks read as zeros straight from LDS)."""
+    end chunks read as zeros straight from LDS). ``reg``: rows of a partial last chunk on a padded image filled through
+    registers (``BREG``, two slots)."""
     VE = 16 // es
     CPR = -(-X // VE)
-    padded = band_padded(X, es, pad)
+    reg = bool(reg) and X % VE != 0
+    padded = reg or band_padded(X, es, pad)
     # LDS image row pitch (elements, 16-byte multiple). Rows starting on half dwords (fp16, X odd) are loaded from the
     # dword at or below their start, one element early every other row: the image row then needs room for X + 2
     if padded:
@@ -88,17 +90,17 @@ def band_geometry(X, TY, R, D, es=2, pad=0):
     NPIECE = (TY + 2) * (XP // VE) + (1 if padded else 0)
     NI = -(-NPIECE // 64)
     SLOT = NI * 64 * VE
-    NS = D + 1
+    NS = 2 if reg else D + 1
     return dict(VE=VE, CPR=CPR, XP=XP, G=G, ntask=ntask, NCT=NCT, NT=NCT + 64, NPIECE=NPIECE, NI=NI, SLOT=SLOT,
                 NS=NS, lds_bytes=(NS * SLOT + 64) * es)
 
 
-def _fits(X, TY, R, D, es=2, pad=0):
-    g = band_geometry(X, TY, R, D, es, pad)
+def _fits(X, TY, R, D, es=2, pad=0, reg=0):
+    g = band_geometry(X, TY, R, D, es, pad, reg)
     return g['ntask'] % 64 == 0 and g['NCT'] <= 960 and D * g['NI'] <= 63 and g['lds_bytes'] <= 80 * 1024
 
 
-def band_choice(X, nstore=1, es=2, pad=0):
+def band_choice(X, nstore=1, es=2, pad=0, reg=0):
     """(TY, R, D) for rows of X elements, or None. fp16, measured (scripts/probes/band_ab.py,
     profiles/r03_band_ab*.log): 8-row bands of 4 rows per lane with 2 planes in flight at X = 768 and 1024
     (27-point 1024³: 0.895 ms vs 0.921 for 4-row bands of 2 rows per lane, 3 planes in flight); three workgroups
@@ -111,7 +113,7 @@ def band_choice(X, nstore=1, es=2, pad=0):
     cands = [(8, 4, 2), (4, 2, 3), (8, 2, 3)] if es == 2 else [(4, 4, 2), (8, 4, 2), (4, 2, 2), (8, 2, 2)]
     cands += [(12, 4, 2), (16, 4, 2), (16, 2, 2), (32, 4, 2), (32, 2, 2)]
     for TY, R, D in cands:
-        if R <= rmax and _fits(X, TY, R, D, es, pad):
+        if R <= rmax and _fits(X, TY, R, D, es, pad, reg):
             return TY, R, D
     return None
 
@@ -126,8 +128,9 @@ def emit_band(ir, name, cfg):
     es = band_esize(ir)
     X = cfg.BX
     TY, R, D = cfg.BTY, cfg.BAND, cfg.D
-    padded = band_padded(X, es, cfg.BPAD)
-    g = band_geometry(X, TY, R, D, es, padded)
+    breg = bool(cfg.BREG) and X % (16 // es) != 0     # partial rows on a padded image filled through registers
+    padded = breg or band_padded(X, es, cfg.BPAD)
+    g = band_geometry(X, TY, R, D, es, padded, breg)
     VE, CPR, G, NCT, NT, NPIECE, NI, SLOT, NS = (g[k] for k in ('VE', 'CPR', 'G', 'NCT', 'NT', 'NPIECE', 'NI', 'SLOT',
                                                                  'NS'))
     assert D * NI <= 63 and NCT <= 960, (X, TY, R, D)
@@ -137,10 +140,11 @@ def emit_band(ir, name, cfg):
     et = '_Float16' if half else 'float'            # storage element type
     XP = g['XP']                                    # row pitch in the LDS image (elements)
     NPR = XP // VE                                  # pieces per image row
+    partial = X % VE != 0                           # a row's last chunk is partial (stores: tail of X % VE cells)
     bu = not padded and XP != X                     # rows not a multiple of 16 bytes: row-wise pieces, zero fill
     c0 = VE if padded else 0                        # image column of a row's first element
-    bo = (X * es) % 4 != 0                          # rows on half dwords (fp16, X odd): realigned in registers
-    assert not bu or cfg.BMASK, 'rows of a partial last chunk need the masked stores'
+    bo = not breg and (X * es) % 4 != 0             # rows on half dwords (fp16, X odd): realigned in registers
+    assert not partial or cfg.BMASK, 'rows of a partial last chunk need the masked stores'
     czf = bu and not cfg.BZF                        # BZF=0: the first element past a row zeroed in registers
     pr = KernelExprPrinter('float', dict(ir.symbol_names))
     W = []
@@ -200,92 +204,182 @@ def emit_band(ir, name, cfg):
     else:
         L.append(f'  const int ldw = {NCT // 64};')
     L.append('  if (wave == ldw) {')
-    L.append(f'    int vo[{NI}];')
-    if bo:
-        L.append(f'    int vo1[{NI}];')
-        L.append('    auto hpar = [&](const void* b) { return b ? (int)(((unsigned long long)b >> 1) & 1) : 0; };')
-    L.append('    #pragma unroll')
-    L.append(f'    for (int i = 0; i < {NI}; ++i) {{')
-    L.append('      const int k = i * 64 + lane;')
-    if padded:
-        # image row rr = one zero piece (out of range: the DMA writes zeros) + the row's pieces; one zero piece ends
-        # the slot (the right neighbour of the last row's end)
-        L.append(f'      const int rr = k / {NPR}, pc = k - rr * {NPR}, yy = y0 - 1 + rr;')
-        L.append(f'      vo[i] = (pc > 0 && rr < {TY + 2} && yy >= 0 && yy < Y) ? (yy * {X * es} + 16 * (pc - 1)) : '
-                 '0x7ffffff0;')
-    elif not bu:
-        L.append(f'      vo[i] = k < {NPIECE} ? ((y0 - 1) * {X * es} + 16 * k) : 0x7ffffff0;   // row -1 / past Y: range '
-                 'check')
-    elif not bo:
-        # rows of a pitch that is not a multiple of 16 bytes: each row's pieces start at the row (dword-aligned, the
-        # LDS image keeps a 16-byte row pitch XP); the last piece runs past the row end (zero-filled below)
-        L.append(f'      const int rr = k / {NPR}, pc = k - rr * {NPR}, yy = y0 - 1 + rr;')
-        L.append(f'      vo[i] = (k < {NPIECE} && yy >= 0 && yy < Y) ? (yy * {X * es} + 16 * pc) : 0x7ffffff0;')
-    else:
-        # rows on half dwords: a row starting on an odd element (plane parity pp of the plane's first element, the
-        # row's own parity) is loaded from one element early; offsets from the plane's dword-aligned base, one set
-        # per plane parity
-        L.append(f'      const int rr = k / {NPR}, pc = k - rr * {NPR}, yy = y0 - 1 + rr;')
-        L.append(f'      const bool ok = k < {NPIECE} && yy >= 0 && yy < Y;')
-        L.append(f'      const int s0 = yy * {X} - (yy & 1), s1 = 1 + yy * {X} - ((yy & 1) ^ 1);   // even elements')
-        L.append(f'      vo[i] = ok ? 2 * s0 + 16 * pc : 0x7ffffff0;')
-        L.append(f'      vo1[i] = ok ? 2 * s1 + 16 * pc : 0x7ffffff0;')
-    L.append('    }')
-    L.append('    auto issue = [&](const int q, const int slot) {')
-    L.append(f'      const {et}* pb = {_ws_plane_base(S, 1, "q")};')
-    if bo:
-        L.append('      const int pp = hpar(pb);')
-        L.append(f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? pb - pp : '
-                 f'f_{S.name}), (short)0, pb ? (int)((YX * 2 + 2 * pp + 3) & ~3ll) : 0, 0x00020000);')
-    else:
-        L.append(f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? pb : '
-                 f'f_{S.name}), (short)0, pb ? (int)(YX * {es}) : 0, 0x00020000);')
-    L.append(f'      {et}* dst = lds + slot * {SLOT};')
-    L.append('      #pragma unroll')
-    L.append(f'      for (int i = 0; i < {NI}; ++i)')
-    L.append(f'        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + i * '
-             f'{64 * VE}), 16, {"pp ? vo1[i] : vo[i]" if bo else "vo[i]"}, 0, 0, {int(cfg.BLAUX)});')
-    L.append('    };')
-    if cfg.BSTAG:
-        # probe: the co-resident workgroups of a CU's first round start a fraction of a plane apart
-        L.append(f'    {{ const int st = (blockIdx.x >> 8) % 3; for (int i = 0; i < st; ++i) '
-                 f'__builtin_amdgcn_s_sleep({int(cfg.BSTAG)}); }}')
-    L.append(f'    for (int i = 0; i < {D}; ++i)')
-    L.append('      if (i < nplanes) issue(zb - 1 + i, i);')
-    L.append('    for (int j = 0; j < nplanes; ++j) {')
-    L.append('      // barrier j publishes plane j: the planes issued after it stay in flight')
-    L.append(f'      const int after = min({D - 1}, nplanes - 1 - j);')
-    L.append('      switch (after) {')
-    for a in range(D):
-        L.append(f'        case {a}: asm volatile("s_waitcnt vmcnt({a * NI})" ::: "memory"); break;')
-    L.append('      }')
-    if bo and not czf:
-        # plane j has landed: zeros over the image columns past each row's last element (X + the row's parity .. XP)
-        nz = XP - X
-        L.append('      {')
-        L.append(f'        const int ppj = hpar({_ws_plane_base(S, 1, "(zb - 1 + j)")});')
-        L.append(f'        {et}* img = lds + (j % {NS}) * {SLOT};')
-        L.append(f'        for (int i = lane; i < {(TY + 2) * nz}; i += 64) {{')
-        L.append(f'          const int rr = i / {nz}, c = i - rr * {nz}, pos = {X} + (ppj ^ ((y0 - 1 + rr) & 1)) + c;')
-        L.append(f'          if (pos < {XP}) img[rr * {XP} + pos] = ({et})0;')
-        L.append('        }')
-        L.append('        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
+    if not breg:
+        L.append(f'    int vo[{NI}];')
+        if bo:
+            L.append(f'    int vo1[{NI}];')
+            L.append('    auto hpar = [&](const void* b) { return b ? (int)(((unsigned long long)b >> 1) & 1) : 0; };')
+        L.append('    #pragma unroll')
+        L.append(f'    for (int i = 0; i < {NI}; ++i) {{')
+        L.append('      const int k = i * 64 + lane;')
+        if padded:
+            # image row rr = one zero piece (out of range: the DMA writes zeros) + the row's pieces; one zero piece ends
+            # the slot (the right neighbour of the last row's end)
+            L.append(f'      const int rr = k / {NPR}, pc = k - rr * {NPR}, yy = y0 - 1 + rr;')
+            L.append(f'      vo[i] = (pc > 0 && rr < {TY + 2} && yy >= 0 && yy < Y) ? (yy * {X * es} + 16 * (pc - 1)) : '
+                     '0x7ffffff0;')
+        elif not bu:
+            L.append(f'      vo[i] = k < {NPIECE} ? ((y0 - 1) * {X * es} + 16 * k) : 0x7ffffff0;   // row -1 / past Y: range '
+                     'check')
+        elif not bo:
+            # rows of a pitch that is not a multiple of 16 bytes: each row's pieces start at the row (dword-aligned, the
+            # LDS image keeps a 16-byte row pitch XP); the last piece runs past the row end (zero-filled below)
+            L.append(f'      const int rr = k / {NPR}, pc = k - rr * {NPR}, yy = y0 - 1 + rr;')
+            L.append(f'      vo[i] = (k < {NPIECE} && yy >= 0 && yy < Y) ? (yy * {X * es} + 16 * pc) : 0x7ffffff0;')
+        else:
+            # rows on half dwords: a row starting on an odd element (plane parity pp of the plane's first element, the
+            # row's own parity) is loaded from one element early; offsets from the plane's dword-aligned base, one set
+            # per plane parity
+            L.append(f'      const int rr = k / {NPR}, pc = k - rr * {NPR}, yy = y0 - 1 + rr;')
+            L.append(f'      const bool ok = k < {NPIECE} && yy >= 0 && yy < Y;')
+            L.append(f'      const int s0 = yy * {X} - (yy & 1), s1 = 1 + yy * {X} - ((yy & 1) ^ 1);   // even elements')
+            L.append(f'      vo[i] = ok ? 2 * s0 + 16 * pc : 0x7ffffff0;')
+            L.append(f'      vo1[i] = ok ? 2 * s1 + 16 * pc : 0x7ffffff0;')
+        L.append('    }')
+        L.append('    auto issue = [&](const int q, const int slot) {')
+        L.append(f'      const {et}* pb = {_ws_plane_base(S, 1, "q")};')
+        if bo:
+            L.append('      const int pp = hpar(pb);')
+            L.append(f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? pb - pp : '
+                     f'f_{S.name}), (short)0, pb ? (int)((YX * 2 + 2 * pp + 3) & ~3ll) : 0, 0x00020000);')
+        else:
+            L.append(f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? pb : '
+                     f'f_{S.name}), (short)0, pb ? (int)(YX * {es}) : 0, 0x00020000);')
+        L.append(f'      {et}* dst = lds + slot * {SLOT};')
+        L.append('      #pragma unroll')
+        L.append(f'      for (int i = 0; i < {NI}; ++i)')
+        L.append(f'        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + i * '
+                 f'{64 * VE}), 16, {"pp ? vo1[i] : vo[i]" if bo else "vo[i]"}, 0, 0, {int(cfg.BLAUX)});')
+        L.append('    };')
+        if cfg.BSTAG:
+            # probe: the co-resident workgroups of a CU's first round start a fraction of a plane apart
+            L.append(f'    {{ const int st = (blockIdx.x >> 8) % 3; for (int i = 0; i < st; ++i) '
+                     f'__builtin_amdgcn_s_sleep({int(cfg.BSTAG)}); }}')
+        L.append(f'    for (int i = 0; i < {D}; ++i)')
+        L.append('      if (i < nplanes) issue(zb - 1 + i, i);')
+        L.append('    for (int j = 0; j < nplanes; ++j) {')
+        L.append('      // barrier j publishes plane j: the planes issued after it stay in flight')
+        L.append(f'      const int after = min({D - 1}, nplanes - 1 - j);')
+        L.append('      switch (after) {')
+        for a in range(D):
+            L.append(f'        case {a}: asm volatile("s_waitcnt vmcnt({a * NI})" ::: "memory"); break;')
         L.append('      }')
-    elif bu and not czf:
-        # plane j has landed: zeros over the image columns X .. XP of every row (the straddling last piece brought
-        # the next row's first elements), which the row's last cells read as their right neighbours
-        ndw = (XP - X) * es // 4
-        L.append('      {')
-        L.append(f'        unsigned* img = (unsigned*)(lds + (j % {NS}) * {SLOT});')
-        L.append(f'        for (int i = lane; i < {(TY + 2) * ndw}; i += 64) '
-                 f'img[(i / {ndw}) * {XP * es // 4} + {X * es // 4} + i % {ndw}] = 0u;')
-        L.append('        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
-        L.append('      }')
-    L.append('      __builtin_amdgcn_s_barrier();')
-    L.append(f'      if (j + {D} < nplanes) issue(zb - 1 + j + {D}, (j + {D}) % {NS});')
-    L.append('    }')
-    L.append('    return;')
-    L.append('  }')
+        if bo and not czf:
+            # plane j has landed: zeros over the image columns past each row's last element (X + the row's parity .. XP)
+            nz = XP - X
+            L.append('      {')
+            L.append(f'        const int ppj = hpar({_ws_plane_base(S, 1, "(zb - 1 + j)")});')
+            L.append(f'        {et}* img = lds + (j % {NS}) * {SLOT};')
+            L.append(f'        for (int i = lane; i < {(TY + 2) * nz}; i += 64) {{')
+            L.append(f'          const int rr = i / {nz}, c = i - rr * {nz}, pos = {X} + (ppj ^ ((y0 - 1 + rr) & 1)) + c;')
+            L.append(f'          if (pos < {XP}) img[rr * {XP} + pos] = ({et})0;')
+            L.append('        }')
+            L.append('        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
+            L.append('      }')
+        elif bu and not czf:
+            # plane j has landed: zeros over the image columns X .. XP of every row (the straddling last piece brought
+            # the next row's first elements), which the row's last cells read as their right neighbours
+            ndw = (XP - X) * es // 4
+            L.append('      {')
+            L.append(f'        unsigned* img = (unsigned*)(lds + (j % {NS}) * {SLOT});')
+            L.append(f'        for (int i = lane; i < {(TY + 2) * ndw}; i += 64) '
+                     f'img[(i / {ndw}) * {XP * es // 4} + {X * es // 4} + i % {ndw}] = 0u;')
+            L.append('        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
+            L.append('      }')
+        L.append('      __builtin_amdgcn_s_barrier();')
+        L.append(f'      if (j + {D} < nplanes) issue(zb - 1 + j + {D}, (j + {D}) % {NS});')
+        L.append('    }')
+        L.append('    return;')
+        L.append('  }')
+    if breg:
+        # register-staged loader for rows whose pitch is not a multiple of 16 bytes: each lane owns 16-byte image
+        # pieces (pads, rows outside the plane: zeros); a row piece is read with 16-byte (and, on half-dword rows,
+        # one more 4-byte) buffer loads at the dword at or below it, realigned by v_alignbyte, its cells past X
+        # zeroed, and written to the padded image with ds_write_b128 -- aligned image, no zero fill, no DMA at a
+        # row's misaligned start. Two register sets (planes j, j+1 in flight), two image slots.
+        # two register sets unless they would crowd the compute waves' registers (odd rows of ~600+ halves)
+        nrs_ok = D >= 2 and 2 * NI * (5 if half else 4) + NI <= 140
+        nrs = 2 if nrs_ok else 1
+        L.append(f'    int go[{NI}];                        // byte offset of the piece in its plane (row piece)')
+        L.append('    unsigned okm = 0u, lastm = 0u;       // pieces that are row data / a row\'s partial last piece')
+        L.append('    #pragma unroll')
+        L.append(f'    for (int i = 0; i < {NI}; ++i) {{')
+        L.append('      const int k = i * 64 + lane;')
+        L.append(f'      const int rr = k / {NPR}, pc = k - rr * {NPR}, yy = y0 - 1 + rr;')
+        L.append(f'      const bool ok = pc > 0 && rr < {TY + 2} && yy >= 0 && yy < Y;')
+        L.append(f'      go[i] = ok ? (yy * {X} + (pc - 1) * {VE}) * {es} : 0;')
+        L.append('      okm |= ok ? (1u << i) : 0u;')
+        L.append(f'      lastm |= (ok && pc == {CPR}) ? (1u << i) : 0u;')
+        L.append('    }')
+        for sname in ('a', 'b')[:nrs]:
+            L.append(f'    u32x4 r{sname}[{NI}];')
+            if half:
+                L.append(f'    unsigned e{sname}[{NI}];')
+            L.append(f'    int a{sname} = 0;')
+
+        def load(sname, q):
+            B = ['    {',
+                 f'      const {et}* pb = {_ws_plane_base(S, 1, q)};',
+                 f'      a{sname} = pb ? (int)((unsigned long long)pb & 3ull) : 0;',
+                 f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? '
+                 f'(const char*)pb - a{sname} : (const char*)f_{S.name}), (short)0, pb ? (int)((a{sname} + YX * {es} + 3) '
+                 f'& ~3ll) : 0, 0x00020000);',
+                 '      #pragma unroll',
+                 f'      for (int i = 0; i < {NI}; ++i) {{',
+                 f'        const int o = ((okm >> i) & 1u) ? ((a{sname} + go[i]) & ~3) : 0x7ffffff0;',
+                 f'        r{sname}[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, {int(cfg.BLAUX)});']
+            if half:
+                B.append(f'        e{sname}[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 16, 0, {int(cfg.BLAUX)});')
+            B += ['      }', '    }']
+            return B
+
+        kx = X % VE                                      # valid cells of a row's last piece
+        keep = []                                        # per dword of the last piece: mask of the bits kept
+        for dwi in range(4):
+            lo_el, hi_el = dwi * (4 // es), dwi * (4 // es) + (4 // es) - 1
+            if hi_el < kx:
+                keep.append(0xffffffff)
+            elif lo_el < kx:
+                keep.append(0x0000ffff)
+            else:
+                keep.append(0)
+
+        def store(sname, slot):
+            B = ['    {',
+                 f'      {et}* img = lds + {slot} * {SLOT};',
+                 '      #pragma unroll',
+                 f'      for (int i = 0; i < {NI}; ++i) {{',
+                 f'        u32x4 v = r{sname}[i];']
+            if half:
+                B += [f'        if ((a{sname} + go[i]) & 2) {{            // the piece starts on a half dword',
+                      f'          v = (u32x4){{__builtin_amdgcn_alignbyte(v.y, v.x, 2u), __builtin_amdgcn_alignbyte(v.z, v.y, 2u), '
+                      f'__builtin_amdgcn_alignbyte(v.w, v.z, 2u), __builtin_amdgcn_alignbyte(e{sname}[i], v.w, 2u)}};',
+                      '        }']
+            B += ['        if ((lastm >> i) & 1u) {                // cells past X: zeros (right neighbour of cell X-1)',
+                  '          ' + ' '.join(f'v.{"xyzw"[d]} &= {keep[d]:#x}u;' for d in range(4) if keep[d] != 0xffffffff),
+                  '        }',
+                  f'        *(u32x4*)(img + (i * 64 + lane) * {VE}) = v;',
+                  '      }',
+                  '    }']
+            return B
+        # the loop: plane j from register set j % 2 into slot j % 2 (two slots: the loader writes plane j after barrier
+        # j-1, when every compute wave is done with plane j-2)
+        L += load('a', 'zb - 1')
+        if nrs == 2:
+            L.append('    if (nplanes > 1)')
+            L += load('b', 'zb')
+        L.append('    for (int j = 0; j < nplanes; j += ' + str(nrs) + ') {')
+        for t in range(nrs):
+            sname = 'ab'[t]
+            if t:
+                L.append('      if (j + 1 >= nplanes) break;')
+            L += store(sname, f'((j + {t}) % {NS})')
+            L.append('      asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");')
+            L.append(f'      if (j + {t} + {nrs} < nplanes)')
+            L += load(sname, f'(zb - 1 + j + {t} + {nrs})')
+        L.append('    }')
+        L.append('    return;')
+        L.append('  }')
     # ---- compute lanes
     if bo:
         L.append('  auto hpar = [&](const void* b) { return b ? (int)(((unsigned long long)b >> 1) & 1) : 0; };')
@@ -433,7 +527,7 @@ def emit_band(ir, name, cfg):
             B.append(f'{ind}    }} else {{')
             # not a whole in-range chunk. 'bu' rows: the partial last chunk holds X % VE cells of the row (the rest is
             # the next row's), stored as whole dwords (X·es is a multiple of 4)
-            nb_t = (X % VE) * es if bu else 0           # bytes of a row's partial last chunk
+            nb_t = (X % VE) * es if partial else 0           # bytes of a row's partial last chunk
             ndw_t, nh_t = nb_t // 4, (nb_t % 4) // 2       # whole dwords, then one half (X odd)
 
             def tail_store(vec):
@@ -464,7 +558,7 @@ def emit_band(ir, name, cfg):
                 return ' '.join(out)
             if cfg.BXW:
                 # the launch's x range is the whole row: the only chunk not stored whole is a 'bu' row's partial last
-                if bu:
+                if partial:
                     B.append(f'{ind}      const u32x4 ow = __builtin_bit_cast(u32x4, ov);')
                     B.append(f'{ind}      {tail_store("ow")}')
             elif cfg.XB:
@@ -473,7 +567,7 @@ def emit_band(ir, name, cfg):
                 B.append(f'{ind}      const {vt} zv = {{{sel}}};')
                 full = (f'__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, zv), ors, '
                         f'sofs + {o * X * es}u, 0, 2);')
-                if bu:
+                if partial:
                     B.append(f'{ind}      const u32x4 zw = __builtin_bit_cast(u32x4, zv);')
                     B.append(f'{ind}      if (xtail) {{ {tail_store("zw")} }} else {{ {full} }}')
                 else:
@@ -483,7 +577,7 @@ def emit_band(ir, name, cfg):
                 # or the partial last one), cells selected one by one (per-cell stores cost ~30 VGPRs in the loop)
                 B.append(f'{ind}      const u32x4 ow = __builtin_bit_cast(u32x4, ov);')
                 B.append(f'{ind}      u32x4 old;')
-                if bu:
+                if partial:
                     B.append(f'{ind}      if (xtail) {{ old = (u32x4)(0u); {tail_load("old")} }}')
                     B.append(f'{ind}      else old = __builtin_amdgcn_raw_buffer_load_b128(ors, sofs + {o * X * es}u, 0, 0);')
                 else:
@@ -499,7 +593,7 @@ def emit_band(ir, name, cfg):
                         nw.append(f'(x + {d} >= xlo && x + {d} < xhi) ? ow.{"xyzw"[d]} : old.{"xyzw"[d]}')
                 B.append(f'{ind}      const u32x4 nw = {{{", ".join(nw)}}};')
                 full = f'__builtin_amdgcn_raw_buffer_store_b128(nw, ors, sofs + {o * X * es}u, 0, 2);'
-                if bu:
+                if partial:
                     B.append(f'{ind}      if (xtail) {{ {tail_store("nw")} }} else {{ {full} }}')
                 else:
                     B.append(f'{ind}      {full}')

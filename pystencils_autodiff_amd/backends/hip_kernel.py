@@ -52,13 +52,14 @@ BAND_TRIM = BAND_TRIM_DEFAULT
 # (profiles/r04_op_band_ab6.log): 27-point 768³ 0.699 vs 0.715 ms, 1024³ 1.581 vs 1.603, 512³ 0.198 vs 0.201;
 # fp16 7-point 768³ 0.631 vs 0.629, 1024³ 1.444 vs 1.438 (not for star stencils)
 BAND_PAD_BOX = 1
+BAND_REG = 0
 
 # gpu_indexing_params keys of pystencils' own GPU indexing (``block_size``, ``maximum_block_size``, …, e.g.
 # ``gpu_indexing_params={'block_size': (8, 4, 2)}`` in the reference's tests/test_graph_datahandling.py:70): they
 # describe a one-thread-per-cell launch these schedules do not have, so they are accepted and ignored. Upper-case
 # keys are this layer's tile parameters; an unknown one is a typo and raises.
 TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
-             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE', 'BLDR', 'BLAUX', 'BPAD', 'BZF')
+             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE', 'BLDR', 'BLAUX', 'BPAD', 'BZF', 'BREG')
 
 
 def _band_config(ir, ve, shape, over):
@@ -94,7 +95,8 @@ def _band_config(ir, ve, shape, over):
     TY = int(over.get('BTY', TY if TY % R == 0 else R * max(1, TY // R)))
     D = int(over.get('D', D))
     pad = int(over.get('BPAD', BAND_PAD_BOX if ntaps > 12 else 0))
-    g = band_geometry(X, TY, R, D, es, pad)
+    reg = int(over.get('BREG', BAND_REG))
+    g = band_geometry(X, TY, R, D, es, pad, reg)
     if TY % R or g['NCT'] > 960 or D * g['NI'] > 63 or g['lds_bytes'] > 160 * 1024:
         raise ValueError(f'band schedule: BTY={TY} BAND={R} D={D} do not fit rows of {X} elements')
     nty, Z = -(-int(shape[-2]) // TY), int(shape[0])
@@ -120,7 +122,7 @@ def _band_config(ir, ve, shape, over):
                        ZMAX=zmax, BLK=int(over.get('BLK', 512)), MAP=int(over.get('MAP', 0)),
                        BTRIM=btrim, BEDGE=int(over.get('BEDGE', 1)),
                        BSTAG=int(over.get('BSTAG', 0)), BWPE=int(over.get('BWPE', 0)), BLDR=int(over.get('BLDR', 0)),
-                       BLAUX=int(over.get('BLAUX', 0)), BPAD=pad, BZF=int(over.get('BZF', 1)))
+                       BLAUX=int(over.get('BLAUX', 0)), BPAD=pad, BZF=int(over.get('BZF', 1)), BREG=reg)
 
 
 def default_march_config(ir, ve, shape=None, tuning=None, band=True):
@@ -762,7 +764,7 @@ class HipStencilKernel:
                                           'nty')]
         kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics) + \
             [self._scalar_kind()] * len(ir.scalars)
-        block = ws['block'] if ws else (band_geometry(cfg.BX, cfg.BTY, cfg.BAND, cfg.D, esize, cfg.BPAD)['NT'] if cfg.BAND else
+        block = ws['block'] if ws else (band_geometry(cfg.BX, cfg.BTY, cfg.BAND, cfg.D, esize, cfg.BPAD, cfg.BREG)['NT'] if cfg.BAND else
                                         cfg.NT)
         return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics, xb=cfg.XB, block=block)
 
