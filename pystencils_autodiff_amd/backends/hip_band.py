@@ -319,7 +319,7 @@ def emit_band(ir, name, cfg):
 
         def load(sname, q):
             B = ['    {',
-                 f'      const {et}* pb = {_ws_plane_base(S, 1, q)};',
+                 f'      const {et}* pb = {_ws_plane_base(S, 1, "(" + q + ")")};',
                  f'      a{sname} = pb ? (int)((unsigned long long)pb & 3ull) : 0;',
                  f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? '
                  f'(const char*)pb - a{sname} : (const char*)f_{S.name}), (short)0, pb ? (int)((a{sname} + YX * {es} + 3) '

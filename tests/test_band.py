@@ -165,7 +165,8 @@ def _band_vs_oracle(case, shape, bh, **extra):
 
 
 UNALIGNED = [('27pt', (7, 16, 766)), ('7pt_f16', (6, 13, 510)), ('27pt', (5, 9, 762)), ('asym_f16', (4, 8, 254)),
-             ('27pt_f32', (5, 8, 765)), ('27pt', (6, 12, 767)), ('7pt_f16', (5, 9, 511)), ('27pt', (7, 8, 255))]
+             ('27pt_f32', (5, 8, 765)), ('27pt', (6, 12, 767)), ('7pt_f16', (5, 9, 511)), ('27pt', (7, 8, 255)),
+             ('27pt', (19, 9, 510)), ('7pt_f16', (21, 8, 511))]          # several z chunks
 
 
 @pytest.mark.gpu
