@@ -73,7 +73,7 @@ def band_geometry(X, TY, R, D, es=2, pad=0, reg=0):
     Rows whose pitch is not a multiple of 16 bytes (``X % VE``) take ``ceil(X / VE)`` chunks, the last one partial.
     ``pad``: every image row is preceded by one zero 16-byte piece and the slot ends with one (x neighbours of a row's
     end chunks read as zeros straight from LDS). ``reg``: rows of a partial last chunk on a padded image filled through
-    registers (``BREG``, two slots)."""
+    registers (``BREG``)."""
     VE = 16 // es
     CPR = -(-X // VE)
     reg = bool(reg) and X % VE != 0
@@ -90,7 +90,7 @@ def band_geometry(X, TY, R, D, es=2, pad=0, reg=0):
     NPIECE = (TY + 2) * (XP // VE) + (1 if padded else 0)
     NI = -(-NPIECE // 64)
     SLOT = NI * 64 * VE
-    NS = 2 if reg else D + 1
+    NS = 3 if reg else D + 1
     return dict(VE=VE, CPR=CPR, XP=XP, G=G, ntask=ntask, NCT=NCT, NT=NCT + 64, NPIECE=NPIECE, NI=NI, SLOT=SLOT,
                 NS=NS, lds_bytes=(NS * SLOT + 64) * es)
 
@@ -296,10 +296,8 @@ def emit_band(ir, name, cfg):
         # pieces (pads, rows outside the plane: zeros); a row piece is read with 16-byte (and, on half-dword rows,
         # one more 4-byte) buffer loads at the dword at or below it, realigned by v_alignbyte, its cells past X
         # zeroed, and written to the padded image with ds_write_b128 -- aligned image, no zero fill, no DMA at a
-        # row's misaligned start. Two register sets (planes j, j+1 in flight), two image slots.
-        # two register sets unless they would crowd the compute waves' registers (odd rows of ~600+ halves)
-        nrs_ok = D >= 2 and 2 * NI * (5 if half else 4) + NI <= 140
-        nrs = 2 if nrs_ok else 1
+        # row's misaligned start.
+        nrs = 1
         L.append(f'    int go[{NI}];                        // byte offset of the piece in its plane (row piece)')
         L.append('    unsigned okm = 0u, lastm = 0u;       // pieces that are row data / a row\'s partial last piece')
         L.append('    #pragma unroll')
@@ -362,21 +360,22 @@ def emit_band(ir, name, cfg):
                   '      }',
                   '    }']
             return B
-        # the loop: plane j from register set j % 2 into slot j % 2 (two slots: the loader writes plane j after barrier
-        # j-1, when every compute wave is done with plane j-2)
+        # planes 0 and 1 before the first barrier, then plane j+2 between barriers j and j+1 (loads, wait, writes:
+        # the load latency is the loader's alone, hidden behind the compute of plane j; three slots: slot (j+2) % 3
+        # held plane j-1, which every compute wave finished before barrier j). No registers live across a barrier
+        # or the loop's back edge, so the compiler's own vmcnt waits are exact.
         L += load('a', 'zb - 1')
-        if nrs == 2:
-            L.append('    if (nplanes > 1)')
-            L += load('b', 'zb')
-        L.append('    for (int j = 0; j < nplanes; j += ' + str(nrs) + ') {')
-        for t in range(nrs):
-            sname = 'ab'[t]
-            if t:
-                L.append('      if (j + 1 >= nplanes) break;')
-            L += store(sname, f'((j + {t}) % {NS})')
-            L.append('      asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");')
-            L.append(f'      if (j + {t} + {nrs} < nplanes)')
-            L += load(sname, f'(zb - 1 + j + {t} + {nrs})')
+        L += store('a', '0')
+        L.append('    if (nplanes > 1) {')
+        L += load('a', 'zb')
+        L += store('a', '1')
+        L.append('    }')
+        L.append('    for (int j = 0; j < nplanes; ++j) {')
+        L.append('      asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");')
+        L.append('      if (j + 2 < nplanes) {')
+        L += load('a', '(zb + 1 + j)')
+        L += store('a', f'((j + 2) % {NS})')
+        L.append('      }')
         L.append('    }')
         L.append('    return;')
         L.append('  }')
