@@ -52,7 +52,10 @@ BAND_TRIM = BAND_TRIM_DEFAULT
 # (profiles/r04_op_band_ab6.log): 27-point 768³ 0.699 vs 0.715 ms, 1024³ 1.581 vs 1.603, 512³ 0.198 vs 0.201;
 # fp16 7-point 768³ 0.631 vs 0.629, 1024³ 1.444 vs 1.438 (not for star stencils)
 BAND_PAD_BOX = 1
-BAND_REG = 0
+# partial rows on a padded image filled through registers (BREG) for star stencils on fp16 rows of odd length
+# (profiles/r04_op_band_ab9.log): 7-point 511³ 0.210 vs 0.217 ms (DMA row pieces + v_perm realignment); even rows
+# (510³ 0.207 vs 0.201) and box stencils (27-point 510³ 0.259 vs 0.245, 511³ 0.259 vs 0.252) keep the DMA pieces
+BAND_REG_STAR_ODD = 1
 
 # gpu_indexing_params keys of pystencils' own GPU indexing (``block_size``, ``maximum_block_size``, …, e.g.
 # ``gpu_indexing_params={'block_size': (8, 4, 2)}`` in the reference's tests/test_graph_datahandling.py:70): they
@@ -95,7 +98,7 @@ def _band_config(ir, ve, shape, over):
     TY = int(over.get('BTY', TY if TY % R == 0 else R * max(1, TY // R)))
     D = int(over.get('D', D))
     pad = int(over.get('BPAD', BAND_PAD_BOX if ntaps > 12 else 0))
-    reg = int(over.get('BREG', BAND_REG))
+    reg = int(over.get('BREG', BAND_REG_STAR_ODD if ntaps <= 12 and es == 2 and X % 2 else 0))
     g = band_geometry(X, TY, R, D, es, pad, reg)
     if TY % R or g['NCT'] > 960 or D * g['NI'] > 63 or g['lds_bytes'] > 160 * 1024:
         raise ValueError(f'band schedule: BTY={TY} BAND={R} D={D} do not fit rows of {X} elements')

@@ -78,13 +78,15 @@ def test_band_default_selection(shape, expect, zc):
     assert cfg.BAND == 0
 
 
-@pytest.mark.parametrize('shape,zc', [((512, 512, 512), 64), ((510, 510, 510), 64), ((768, 768, 768), 8),
+@pytest.mark.parametrize('shape,zc', [((512, 512, 512), 64), ((510, 510, 510), 64), ((511, 511, 511), 64),
+                                      ((768, 768, 768), 8),
                                       ((1024, 1024, 1024), 8), ((256, 256, 256), 8)])
 def test_band_default_selection_star(shape, zc):
     """fp16 7-point: 8-plane chunks, 64-plane ones on rows of <= 512 elements (>= 512 workgroups)."""
     op = pa.AutoDiffOp(W.diffusion_7pt(dtype='float16'), boundary_handling='zeros')
     cfg = default_march_config(HipStencilKernel(_kernel(op.forward_assignments)).ir, 8, shape)
     assert cfg.BAND == 4 and cfg.ZMIN == cfg.ZMAX == zc and cfg.BPAD == 0, cfg
+    assert cfg.BREG == shape[-1] % 2, cfg                      # odd rows: the register-staged padded image
 
 
 def test_band_sources_compile():
