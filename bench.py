@@ -143,6 +143,11 @@ def load_traffic(workload, kernel):
     return (k['total'] if k else None), entry.get('source')
 
 
+def _sig(x, n=4):
+    """``x`` to ``n`` significant digits (a fraction of the peak stays readable at small N=2 rehearsal sizes)."""
+    return float(f'{x:.{n}g}')
+
+
 def roofline(name, r, world):
     """The line's ``roofline`` object: ``achieved`` = algorithmic bytes of one step (forward + adjoint sweep over the
     whole domain) ÷ the step time (barrier-bracketed, max over ranks) ÷ GPUs, so ``frac`` is the
@@ -156,9 +161,9 @@ def roofline(name, r, world):
     tb, _ = load_traffic(key, r['kname'].replace('_forward_', '_backward_'))
     traffic = tf + tb if tf is not None and tb is not None else None      # per step, like ``achieved``
     return {'bound': 'hbm', 'achieved': round(r['achieved'], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-            'frac': round(r['achieved'] / HBM_PEAK_GBS, 4),
-            'frac_fwd': round(r['achieved_fwd'] / HBM_PEAK_GBS, 4),
-            'frac_bwd': round(r['achieved_bwd'] / HBM_PEAK_GBS, 4),
+            'frac': _sig(r['achieved'] / HBM_PEAK_GBS),
+            'frac_fwd': _sig(r['achieved_fwd'] / HBM_PEAK_GBS),
+            'frac_bwd': _sig(r['achieved_bwd'] / HBM_PEAK_GBS),
             'achieved_fwd': round(r['achieved_fwd'], 1), 'achieved_bwd': round(r['achieved_bwd'], 1),
             'traffic': traffic, 'traffic_fwd_launch': tf,
             'traffic_source': src or f'no PMC entry for the launch shape {key}',

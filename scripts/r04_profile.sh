@@ -8,6 +8,8 @@ OUT="$ROOT/gpurun_out"; mkdir -p "$OUT"
 export TMPDIR=/tmp PSAD_CACHE_DIR=/tmp/psad_cache
 TAG="${1:-r04}"
 fatal() { echo "[$2] rc=$1" | tee -a "$OUT/status_$TAG.log"; if [ "$1" -ne 0 ]; then exit "$1"; fi; }
+timeout -k 10 300 python -u -m pytest tests/test_bench_rehearsal.py -m gpu -q --timeout 250 --timeout-method thread > "$OUT/pytest_rehearsal_$TAG.log" 2>&1; fatal $? rehearsal
+tail -2 "$OUT/pytest_rehearsal_$TAG.log"
 timeout -k 10 200 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/warm_$TAG.log" 2>&1; fatal $? warm
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o trace -- \
