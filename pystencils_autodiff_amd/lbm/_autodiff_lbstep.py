@@ -299,6 +299,7 @@ class AutoDiffLatticeBoltzmannStep:
     def _flags_changed(self):
         self._flag_dev = None
         self._ids_dev = None
+        self._links_cached = None
         self._records = None
 
     def _flag_arg(self):
@@ -316,8 +317,14 @@ class AutoDiffLatticeBoltzmannStep:
         return self._flag_dev
 
     def _links(self):
-        """The wall kernels' link tables (None: every wall a plain bounce-back, or no walls)."""
-        return self._boundary.link_tables(self.method) if self._boundary.has_walls else None
+        """The wall kernels' link tables (None: every wall a plain bounce-back, or no walls), derived once per
+        boundary change (``link_coefficients`` differentiates each boundary's sympy link: milliseconds, not per
+        step)."""
+        cached = getattr(self, '_links_cached', None)
+        if cached is None:
+            cached = self._links_cached = (self._boundary.link_tables(self.method) if self._boundary.has_walls
+                                           else None,)
+        return cached[0]
 
     def _ids_arg(self):
         """The cells' wall ids for kernels with link tables (the flag array on the kernels' device), else None."""

@@ -492,6 +492,31 @@ def test_lbm_lid_driven_cavity_cpu(adjoint, compressible):
     assert np.abs(step.adjoint_pdf_array - gref.numpy()).max() <= 1e-12 * np.abs(gref.numpy()).max()
 
 
+def test_lbm_link_tables_derived_once_per_boundary_change(monkeypatch):
+    """The wall kernels' link tables (sympy AD of each boundary's link, ~20 ms) are derived once per boundary change,
+    not per time step (a per-step derivation made the walled LBM configs 19x slower)."""
+    calls = []
+    from pystencils_autodiff_amd.lbm.boundaries import BoundaryHandling
+    orig = BoundaryHandling.link_tables
+
+    def counted(self, method):
+        calls.append(1)
+        return orig(self, method)
+    monkeypatch.setattr(BoundaryHandling, "link_tables", counted)
+    shape = (14, 11)
+    step = lbm.AutoDiffLatticeBoltzmannStep(lbm.create_lb_update_rule('D2Q9'), domain_size=shape,
+                                            relaxation_rate=1.3, target='cpu')
+    _set_cavity(step, shape, None)
+    step.set_pdfs(_init('D2Q9', shape, False, seed=3))
+    step.run(4, record=True)
+    step.set_adjoint_pdfs(np.ones_like(step.pdf_array))
+    step.run_backward(4)
+    assert len(calls) == 1
+    step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[:, 1])    # a boundary change: derived again
+    step.run(1)
+    assert len(calls) == 2
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize('dtype', ['float64', 'float32'])
 def test_lbm_lid_driven_cavity_gpu(dtype):
