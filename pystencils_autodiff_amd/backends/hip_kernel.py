@@ -44,9 +44,13 @@ BAND_MIN_WG = 768
 # workgroups (profiles/r04_op_zc_sweep.log, _ab6.log): fp16 7-point 512³ 0.184 vs 0.197 ms, 510³ 0.204 vs 0.229;
 # 768³ keeps 8 (0.629 vs 0.675 at 96 planes, 0.699 at 64), 256³ too (0.024 vs 0.038 at 32)
 BAND_ZC_STAR_LONG, BAND_STAR_LONG_MAX_X, BAND_STAR_LONG_MIN_WG = 64, 512, 512
-# fp32 storage (4 cells per 16-byte chunk) measured slower through the op (7-point 512³ 0.387 vs 0.373 ms, 768³
-# 1.325 vs 1.261): opt-in only (BAND=R)
-BAND_F32_MAX_X = 0
+# fp32 storage (4 cells per 16-byte chunk): 4-row bands measured slower through the op (7-point 512³ 0.387 vs
+# 0.373 ms, 768³ 1.325 vs 1.261); 8-row bands of 4 rows per lane (4-6 compute waves, 60-90 KB of LDS) faster for
+# star stencils on rows of <= 768 (profiles/r04_op_f7_ab2.log, _ab3.log, shared inputs): 512³ 0.365-0.368 vs
+# 0.373-0.389 ms (16-plane chunks), 768³ 1.189 vs 1.219; 1024-wide rows do not fit the loader's vmcnt budget.
+# Box stencils in fp32 stay on zsum unless BAND=R asks.
+BAND_F32_STAR_MAX_X = 768
+BAND_ZC_STAR_F32 = 16
 BAND_TRIM = BAND_TRIM_DEFAULT
 # zero-padded image rows (x neighbours read from LDS, no DPP / boundary selects) for box stencils
 # (profiles/r04_op_band_ab6.log): 27-point 768³ 0.699 vs 0.715 ms, 1024³ 1.581 vs 1.603, 512³ 0.198 vs 0.201;
@@ -79,13 +83,17 @@ def _band_config(ir, ve, shape, over):
     plans = band_plans(ir)
     X = int(shape[-1])
     es = band_esize(ir) if plans else 0
-    if plans and es == 4 and X > BAND_F32_MAX_X and 'BAND' not in over:
+    ntaps = max(len(pl['w']) for pl in plans) if plans else 0
+    if plans and es == 4 and not (ntaps <= 12 and X <= BAND_F32_STAR_MAX_X) and 'BAND' not in over:
         return None
     choice = band_choice(X, len(plans), es) if plans else None
     if choice is None:
         return None
     TY, R, D = choice
-    ntaps = max(len(pl['w']) for pl in plans)
+    g8 = band_geometry(X, 8, 4, 2, 4) if es == 4 else None
+    if g8 and ntaps <= 12 and 'BAND' not in over and g8['ntask'] % 64 == 0 and g8['NCT'] <= 960 and \
+            2 * g8['NI'] <= 63 and g8['lds_bytes'] <= 160 * 1024:
+        TY, R, D = 8, 4, 2              # fp32 star stencils: 8-row bands (see BAND_F32_STAR_MAX_X)
     zc0 = int(over.get('ZMIN', BAND_ZC_BOX if ntaps > 12 else BAND_ZC_STAR))
     if ntaps > 12 and es == 2 and (X // 8) % 128 == 0 and R == 4 and \
             -(-int(shape[-2]) // 16) * -(-int(shape[0]) // zc0) >= BAND_MIN_WG:
@@ -104,7 +112,9 @@ def _band_config(ir, ve, shape, over):
         raise ValueError(f'band schedule: BTY={TY} BAND={R} D={D} do not fit rows of {X} elements')
     nty, Z = -(-int(shape[-2]) // TY), int(shape[0])
     min_wg = BAND_MIN_WG
-    if ntaps <= 12:
+    if ntaps <= 12 and es == 4:
+        zc = BAND_ZC_STAR_F32
+    elif ntaps <= 12:
         long_ok = X <= BAND_STAR_LONG_MAX_X and nty * -(-Z // BAND_ZC_STAR_LONG) >= BAND_STAR_LONG_MIN_WG
         zc = BAND_ZC_STAR_LONG if long_ok else BAND_ZC_STAR
         min_wg = BAND_STAR_LONG_MIN_WG if long_ok else BAND_MIN_WG
