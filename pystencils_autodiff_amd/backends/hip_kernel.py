@@ -45,11 +45,11 @@ BAND_MIN_WG = 768
 # 768³ keeps 8 (0.629 vs 0.675 at 96 planes, 0.699 at 64), 256³ too (0.024 vs 0.038 at 32)
 BAND_ZC_STAR_LONG, BAND_STAR_LONG_MAX_X, BAND_STAR_LONG_MIN_WG = 64, 512, 512
 # fp32 storage (4 cells per 16-byte chunk): 4-row bands measured slower through the op (7-point 512³ 0.387 vs
-# 0.373 ms, 768³ 1.325 vs 1.261); 8-row bands of 4 rows per lane (4-6 compute waves, 60-90 KB of LDS) faster for
-# star stencils on rows of <= 768 (profiles/r04_op_f7_ab2.log, _ab3.log, shared inputs): 512³ 0.365-0.368 vs
-# 0.373-0.389 ms (16-plane chunks), 768³ 1.189 vs 1.219; 1024-wide rows do not fit the loader's vmcnt budget.
-# Box stencils in fp32 stay on zsum unless BAND=R asks.
-BAND_F32_STAR_MAX_X = 768
+# 0.373 ms, 768³ 1.325 vs 1.261); 8-row bands of 4 rows per lane (4 compute waves, 60 KB of LDS) faster for star
+# stencils on rows of <= 512 on every box (profiles/r04_op_f7_ab2.log .. _ab4.log, shared inputs): 512³
+# 0.365-0.368 vs 0.373-0.389 ms; at 768 (6 compute waves, one workgroup per CU) it won on one box (1.189 vs 1.219)
+# and lost on another (1.283-1.318 vs 1.261): zsum there. Box stencils in fp32 stay on zsum unless BAND=R asks.
+BAND_F32_STAR_MAX_X = 512
 BAND_ZC_STAR_F32 = 16
 BAND_TRIM = BAND_TRIM_DEFAULT
 # zero-padded image rows (x neighbours read from LDS, no DPP / boundary selects) for box stencils
