@@ -189,11 +189,6 @@ struct Exchange {
     uint32_t* sig = nullptr;              // faces final (compute -> halo stream)
     uint32_t* sig_halo = nullptr;         // halos landed (halo -> compute)
     mutable uint32_t seq = 0;
-    // PSAD_SLAB_CUMASK=K (> 0, with the stream-memory-op sync): the exchange and the face launch on a stream masked
-    // to K CUs, the interior on a stream masked to the others, so the RCCL kernel and the faces never queue behind
-    // the interior's workgroups; the compute stream waits on both
-    hipStream_t halo_masked = nullptr, inner_stream = nullptr;
-    uint32_t* sig_inner = nullptr;        // interior done (inner -> compute)
 };
 
 struct Sweep {
@@ -227,49 +222,11 @@ void hip_ok(hipError_t e, const char* what) {
     TORCH_CHECK(e == hipSuccess, "psad: ", what, " failed: ", hipGetErrorString(e));
 }
 
-void exchange_on(const Exchange& ex, const std::vector<at::Tensor>& table, hipStream_t s) {
-    const size_t n = ex.slot.size();
-    std::vector<const void*> send_lo(n), send_hi(n);
-    for (size_t i = 0; i < n; ++i) {
-        char* base = static_cast<char*>(table[ex.slot[i]].data_ptr());
-        send_lo[i] = base;
-        send_hi[i] = base + ex.last_off[i];
-        // RCCL pairs a peer's sends and receives in issue order: on a loopback communicator the lower halo
-        // receives the far (upper) face, as with real neighbours — a periodic z boundary
-        if (ex.loopback) std::swap(send_lo[i], send_hi[i]);
-    }
-    int rc = psad_halo_exchange(ex.comm, static_cast<int>(n), send_lo.data(), ex.recv_lo.data(), send_hi.data(),
-                                ex.recv_hi.data(), ex.bytes.data(), ex.peer_lo, ex.peer_hi, s);
-    TORCH_CHECK(rc == 0, "psad: RCCL halo exchange failed: ", psad_rccl_error_string(rc), " (code ", rc, ")");
-}
-
-// PSAD_SLAB_CUMASK: exchange + faces and the interior on streams masked to disjoint CU sets, joined on the compute
-// stream by stream memory operations
-void run_sweep_masked(const Sweep& w, const std::vector<at::Tensor>& table, const std::vector<double>& scalars,
-                      hipStream_t cur) {
-    const Exchange& ex = w.ex;
-    const uint32_t q = ++ex.seq;
-    hip_ok(hipStreamWriteValue32(cur, ex.sig, q, 0), "hipStreamWriteValue32");
-    hip_ok(hipStreamWaitValue32(ex.halo_masked, ex.sig, q, hipStreamWaitValueGte, 0xffffffffu), "hipStreamWaitValue32");
-    hip_ok(hipStreamWaitValue32(ex.inner_stream, ex.sig, q, hipStreamWaitValueGte, 0xffffffffu), "hipStreamWaitValue32");
-    exchange_on(ex, table, ex.halo_masked);
-    for (const auto& f : w.faces) launch_on(f, table, scalars, ex.halo_masked);
-    launch_on(w.inner, table, scalars, ex.inner_stream);
-    hip_ok(hipStreamWriteValue32(ex.halo_masked, ex.sig_halo, q, 0), "hipStreamWriteValue32");
-    hip_ok(hipStreamWriteValue32(ex.inner_stream, ex.sig_inner, q, 0), "hipStreamWriteValue32");
-    hip_ok(hipStreamWaitValue32(cur, ex.sig_halo, q, hipStreamWaitValueGte, 0xffffffffu), "hipStreamWaitValue32");
-    hip_ok(hipStreamWaitValue32(cur, ex.sig_inner, q, hipStreamWaitValueGte, 0xffffffffu), "hipStreamWaitValue32");
-}
-
 void run_sweep(const Sweep& w, const std::vector<at::Tensor>& table, const std::vector<double>& scalars, int device) {
     c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
     hipStream_t cur = c10::hip::getCurrentHIPStream(device).stream();
     const Exchange& ex = w.ex;
     const size_t n = ex.slot.size();
-    if (n && ex.sig_inner) {
-        run_sweep_masked(w, table, scalars, cur);
-        return;
-    }
     if (n && ex.sig) ++ex.seq;
     if (n && ex.sig) {
         hip_ok(hipStreamWriteValue32(cur, ex.sig, ex.seq, 0), "hipStreamWriteValue32");
@@ -425,7 +382,7 @@ Launch launch_from(const py::tuple& t, int64_t n_scalars) {
 // inner (launch spec or None), faces [launch spec], exchange (slot, last_off, recv_lo, recv_hi, bytes, peer_lo,
 // peer_hi, loopback), comm, halo stream
 Sweep sweep_from(const py::object& inner, const py::list& faces, const py::tuple& ex, uint64_t comm, uint64_t stream,
-                 int64_t n_scalars, int64_t n_table, int device) {
+                 int64_t n_scalars, int64_t n_table) {
     Sweep w;
     if (!inner.is_none()) {
         w.has_inner = true;
@@ -477,29 +434,6 @@ Sweep sweep_from(const py::object& inner, const py::list& faces, const py::tuple
             hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
             w.ex.sig = static_cast<uint32_t*>(p);
             w.ex.sig_halo = static_cast<uint32_t*>(q);
-            const char* cm = std::getenv("PSAD_SLAB_CUMASK");
-            const int k = cm != nullptr ? std::atoi(cm) : 0;
-            int ncu = 0;
-            hip_ok(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device),
-                   "hipDeviceGetAttribute");
-            if (k > 0 && k < ncu && w.has_inner) {
-                // the reserved CUs spread evenly over the CU index range (every ncu/k-th)
-                const int nw = (ncu + 31) / 32, step = ncu / k;
-                std::vector<uint32_t> halo_mask(nw, 0u), inner_mask(nw, 0u);
-                int taken = 0;
-                for (int c = 0; c < ncu; ++c) {
-                    const bool res = taken < k && c % step == 0;
-                    taken += res ? 1 : 0;
-                    (res ? halo_mask : inner_mask)[c / 32] |= 1u << (c % 32);
-                }
-                hip_ok(hipExtStreamCreateWithCUMask(&w.ex.halo_masked, nw, halo_mask.data()), "hipExtStreamCreateWithCUMask");
-                hip_ok(hipExtStreamCreateWithCUMask(&w.ex.inner_stream, nw, inner_mask.data()), "hipExtStreamCreateWithCUMask");
-                void* r = nullptr;
-                hip_ok(hipExtMallocWithFlags(&r, 8, hipMallocSignalMemory), "hipExtMallocWithFlags");
-                hip_ok(hipMemset(r, 0, 8), "hipMemset");
-                hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
-                w.ex.sig_inner = static_cast<uint32_t*>(r);
-            }
         }
     }
     return w;
@@ -529,8 +463,8 @@ int64_t register_slab_plan(const std::string& name, int64_t device, std::vector<
     const int64_t n_bwd = static_cast<int64_t>(p->saved.size() + p->fwd_out.size() + p->bwd_out.size());
     for (auto i : p->grad_of_input) TORCH_CHECK(i >= -1 && i < n_bwd, "psad: gradient index out of range");
     c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
-    p->fwd = sweep_from(fwd_inner, fwd_faces, fwd_ex, comm, stream, n_scalars, n_fwd, static_cast<int>(device));
-    p->bwd = sweep_from(bwd_inner, bwd_faces, bwd_ex, comm, stream, n_scalars, n_bwd, static_cast<int>(device));
+    p->fwd = sweep_from(fwd_inner, fwd_faces, fwd_ex, comm, stream, n_scalars, n_fwd);
+    p->bwd = sweep_from(bwd_inner, bwd_faces, bwd_ex, comm, stream, n_scalars, n_bwd);
     std::lock_guard<std::mutex> lock(g_mutex);
     g_slab_plans.push_back(std::move(p));
     return static_cast<int64_t>(g_slab_plans.size()) - 1;
