@@ -98,7 +98,8 @@ def band_geometry(X, TY, R, D, es=2, pad=0, reg=0):
         # BREG=2: the band's rows as one block from a 128-byte aligned start, LDS-DMA'd into D+1 staging slots (up to
         # 127 bytes ahead of row y0-1, the last row's overhang), realigned into two padded image slots by the loader
         nis = -(-(-(-(128 + (TY + 2) * X * es + 32) // 16)) // 64)
-        g.update(NIS=nis, SSLOT=nis * 64 * VE, NSS=2, lds_bytes=(NS * SLOT + 2 * nis * 64 * VE + 64) * es)
+        g.update(NIS=nis, SSLOT=nis * 64 * VE, NSS=D + 1,
+                 lds_bytes=(NS * SLOT + (D + 1) * nis * 64 * VE + 64) * es)
     return g
 
 
@@ -780,7 +781,6 @@ def _staged_loader(g, cfg, S, TY, X, VE, CPR, NPR, SLOT, NS, STG0, D, es, et):
     L.append('      const int sh = pb ? fshift(pb) : 0;')
     L.append(f'      const char* st = (const char*)(lds + {STG0} + sslot * {SSLOT});')
     L.append(f'      {et}* img = lds + islot * {SLOT};')
-    L.append('      #pragma unroll')
     L.append(f'      for (int r = 0; r < {TY + 2}; ++r) {{')
     L.append('        const int yy = y0 - 1 + r;')
     L.append('        const bool rowok = yy >= 0 && yy < Y;')
@@ -809,20 +809,17 @@ def _staged_loader(g, cfg, S, TY, X, VE, CPR, NPR, SLOT, NS, STG0, D, es, et):
     L.append('        }')
     L.append('      }')
     L.append('    };')
-    # plane 0 converted before the first barrier; after barrier j the loader converts plane j+1 (its DMA issued one
-    # interval earlier) into the image slot plane j-1 used, overlapping the compute of plane j, then issues the DMA
-    # of plane j+2 into the staging slot plane j used
-    L.append('    issue(zb - 1, 0);')
-    L.append('    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
-    L.append('    convert(zb - 1, 0, 0);')
-    L.append('    if (nplanes > 1) issue(zb, 1);')
+    L.append(f'    for (int i = 0; i < {D}; ++i)')
+    L.append(f'      if (i < nplanes) issue(zb - 1 + i, i % {NSS});')
     L.append('    for (int j = 0; j < nplanes; ++j) {')
-    L.append('      asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");')
-    L.append('      if (j + 1 < nplanes) {')
-    L.append('        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
-    L.append('        convert(zb + j, (j + 1) & 1, (j + 1) & 1);')
-    L.append('        if (j + 2 < nplanes) issue(zb + 1 + j, j & 1);')
+    L.append(f'      const int after = min({D - 1}, nplanes - 1 - j);')
+    L.append('      switch (after) {')
+    for a in range(D):
+        L.append(f'        case {a}: asm volatile("s_waitcnt vmcnt({a * NIS})" ::: "memory"); break;')
     L.append('      }')
+    L.append(f'      convert(zb - 1 + j, j % {NSS}, j % {NS});')
+    L.append('      asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");')
+    L.append(f'      if (j + {D} < nplanes) issue(zb - 1 + j + {D}, (j + {D}) % {NSS});')
     L.append('    }')
     L.append('    return;')
     L.append('  }')
