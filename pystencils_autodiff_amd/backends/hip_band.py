@@ -755,21 +755,18 @@ def _staged_loader(g, cfg, S, TY, X, VE, CPR, NPR, SLOT, NS, STG0, D, es, et):
     L.append(f'      if (kk % {NPR} == 0) *(u32x4*)(lds + sl * {SLOT} + kk * {VE}) = (u32x4)(0u);')
     L.append('    }')
     L.append(f'    const int rowb = (y0 - 1) * {X * es};')
+    L.append('    auto fbase = [&](const void* b) { const int a = (int)((unsigned long long)b & 127ull); '
+             'return ((a + rowb) & ~127) - a; };')
     L.append('    auto fshift = [&](const void* b) { const int a = (int)((unsigned long long)b & 127ull); '
              'return (a + rowb) - ((a + rowb) & ~127); };')
     L.append(f'    int vo[{NIS}];')
     L.append('    #pragma unroll')
     L.append(f'    for (int i = 0; i < {NIS}; ++i) {{ const int k = i * 64 + lane; vo[i] = k < {nsp} ? 16 * k : 0x40000000; }}')
-    # the resource starts at the 128-byte boundary at or below the plane pointer (a tensor's first plane is
-    # 512-byte aligned, any other plane has its predecessor there), so every 16-byte piece lies wholly before or
-    # wholly inside the range: a piece straddling offset 0 read as zeros where the plane pointer itself was not
-    # 16-byte aligned (the range check of a 16-byte access at a negative offset is not per dword)
     L.append('    auto issue = [&](const int q, const int slot) {')
     L.append(f'      const {et}* pb = {_ws_plane_base(S, 1, "q")};')
-    L.append('      const int a = pb ? (int)((unsigned long long)pb & 127ull) : 0;')
-    L.append('      const int b0 = pb ? ((a + rowb) & ~127) : 0;')
-    L.append(f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? (const char*)pb - a : '
-             f'(const char*)f_{S.name}), (short)0, pb ? (int)((a + YX * {es} + 3) & ~3ll) : 0, 0x00020000);')
+    L.append('      const int b0 = pb ? fbase(pb) : 0;')
+    L.append(f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? pb : f_{S.name}), '
+             f'(short)0, pb ? (int)((YX * {es} + 3) & ~3ll) : 0, 0x00020000);')
     L.append(f'      {et}* dst = lds + {STG0} + slot * {SSLOT};')
     L.append('      #pragma unroll')
     L.append(f'      for (int i = 0; i < {NIS}; ++i)')
