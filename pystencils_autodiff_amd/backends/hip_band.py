@@ -76,7 +76,6 @@ def band_geometry(X, TY, R, D, es=2, pad=0, reg=0):
     registers (``BREG``)."""
     VE = 16 // es
     CPR = -(-X // VE)
-    stg = int(reg) == 2 and X % VE != 0
     reg = bool(reg) and X % VE != 0
     padded = reg or band_padded(X, es, pad)
     # LDS image row pitch (elements, 16-byte multiple). Rows starting on half dwords (fp16, X odd) are loaded from the
@@ -91,21 +90,14 @@ def band_geometry(X, TY, R, D, es=2, pad=0, reg=0):
     NPIECE = (TY + 2) * (XP // VE) + (1 if padded else 0)
     NI = -(-NPIECE // 64)
     SLOT = NI * 64 * VE
-    NS = 2 if stg else (3 if reg else D + 1)
-    g = dict(VE=VE, CPR=CPR, XP=XP, G=G, ntask=ntask, NCT=NCT, NT=NCT + 64, NPIECE=NPIECE, NI=NI, SLOT=SLOT,
-             NS=NS, lds_bytes=(NS * SLOT + 64) * es)
-    if stg:
-        # BREG=2: the band's rows as one block from a 128-byte aligned start, LDS-DMA'd into D+1 staging slots (up to
-        # 127 bytes ahead of row y0-1, the last row's overhang), realigned into two padded image slots by the loader
-        nis = -(-(-(-(128 + (TY + 2) * X * es + 32) // 16)) // 64)
-        g.update(NIS=nis, SSLOT=nis * 64 * VE, NSS=D + 1,
-                 lds_bytes=(NS * SLOT + (D + 1) * nis * 64 * VE + 64) * es)
-    return g
+    NS = 3 if reg else D + 1
+    return dict(VE=VE, CPR=CPR, XP=XP, G=G, ntask=ntask, NCT=NCT, NT=NCT + 64, NPIECE=NPIECE, NI=NI, SLOT=SLOT,
+                NS=NS, lds_bytes=(NS * SLOT + 64) * es)
 
 
 def _fits(X, TY, R, D, es=2, pad=0, reg=0):
     g = band_geometry(X, TY, R, D, es, pad, reg)
-    return g['ntask'] % 64 == 0 and g['NCT'] <= 960 and D * g.get('NIS', g['NI']) <= 63 and g['lds_bytes'] <= 80 * 1024
+    return g['ntask'] % 64 == 0 and g['NCT'] <= 960 and D * g['NI'] <= 63 and g['lds_bytes'] <= 80 * 1024
 
 
 def band_choice(X, nstore=1, es=2, pad=0, reg=0):
@@ -137,12 +129,11 @@ def emit_band(ir, name, cfg):
     X = cfg.BX
     TY, R, D = cfg.BTY, cfg.BAND, cfg.D
     breg = bool(cfg.BREG) and X % (16 // es) != 0     # partial rows on a padded image filled through registers
-    stg = breg and int(cfg.BREG) == 2                 # ... from aligned LDS-DMA staging (realigned in the loader)
     padded = breg or band_padded(X, es, cfg.BPAD)
-    g = band_geometry(X, TY, R, D, es, padded, int(cfg.BREG) if breg else 0)
+    g = band_geometry(X, TY, R, D, es, padded, breg)
     VE, CPR, G, NCT, NT, NPIECE, NI, SLOT, NS = (g[k] for k in ('VE', 'CPR', 'G', 'NCT', 'NT', 'NPIECE', 'NI', 'SLOT',
                                                                  'NS'))
-    assert D * g.get('NIS', NI) <= 63 and NCT <= 960, (X, TY, R, D)
+    assert D * NI <= 63 and NCT <= 960, (X, TY, R, D)
     assert not fixed or int(fixed[0].spatial_shape[-1]) == X, 'band kernel compiled for another row length'
     S = ir.stencil_fields[0]
     half = es == 2
@@ -188,8 +179,7 @@ def emit_band(ir, name, cfg):
              f'in 3 rotating register sets, LDS {g["lds_bytes"]} B')
     wpe = f' __attribute__((amdgpu_waves_per_eu({int(cfg.BWPE)}, {int(cfg.BWPE)})))' if cfg.BWPE else ''
     L.append(f'extern "C" __global__ void __launch_bounds__({NT}){wpe} {name}({", ".join(params)})\n{{')
-    STG0 = NS * SLOT                                # staging slots start here (elements; BREG=2)
-    L.append(f'  __shared__ __attribute__((aligned(1024))) {et} lds[{STG0 + (g["NSS"] * g["SSLOT"] if stg else 0) + 64}];')
+    L.append(f'  __shared__ __attribute__((aligned(1024))) {et} lds[{NS * SLOT + 64}];')
     L.append('  const int tid = threadIdx.x, lane = tid & 63;')
     L.append('  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);')
     if cfg.MAP == 1:
@@ -301,9 +291,7 @@ def emit_band(ir, name, cfg):
         L.append('    }')
         L.append('    return;')
         L.append('  }')
-    if stg:
-        L += _staged_loader(g, cfg, S, TY, X, VE, CPR, NPR, SLOT, NS, STG0, D, es, et)
-    if breg and not stg:
+    if breg:
         # register-staged loader for rows whose pitch is not a multiple of 16 bytes: each lane owns 16-byte image
         # pieces (pads, rows outside the plane: zeros); a row piece is read with 16-byte (and, on half-dword rows,
         # one more 4-byte) buffer loads at the dword at or below it, realigned by v_alignbyte, its cells past X
@@ -731,93 +719,3 @@ def emit_band(ir, name, cfg):
             L.append('  }')
     L.append('}')
     return '\n'.join(L) + '\n'
-
-
-def _staged_loader(g, cfg, S, TY, X, VE, CPR, NPR, SLOT, NS, STG0, D, es, et):
-    """Loader wave for BREG=2: the band's rows y0-1 .. y0+TY of a plane as ONE block from the 128-byte aligned
-    address at or below row y0-1, LDS-DMA'd (aligned 1-KiB wave pieces: no row-start misalignment on the read side)
-    into D+1 staging slots; each landed plane is then realigned row by row into one of two zero-padded image slots
-    (per row the byte shift m of its start is uniform: two aligned ds_read_b128 per lane, a scalar switch on m/4,
-    v_alignbyte by m%4, one ds_write_b128), cells past X zeroed, rows outside the plane zeros."""
-    L = []
-    NIS, SSLOT, NSS = g['NIS'], g['SSLOT'], g['NSS']
-    NPIECE = g['NPIECE']
-    nsp = -(-(128 + (TY + 2) * X * es + 32) // 16)        # staging pieces that can hold data
-    ncc = -(-CPR // 64)                                   # wave instructions per image row
-    kx = X % VE
-    keep = []
-    for dwi in range(4):
-        lo_el, hi_el = dwi * (4 // es), dwi * (4 // es) + (4 // es) - 1
-        keep.append(0xffffffff if hi_el < kx else (0x0000ffff if lo_el < kx else 0))
-    L.append('    // zero pads of both image slots (row starts and the slot end; never written again)')
-    L.append(f'    for (int k = lane; k < {2 * NPIECE}; k += 64) {{')
-    L.append(f'      const int sl = k / {NPIECE}, kk = k - sl * {NPIECE};')
-    L.append(f'      if (kk % {NPR} == 0) *(u32x4*)(lds + sl * {SLOT} + kk * {VE}) = (u32x4)(0u);')
-    L.append('    }')
-    L.append(f'    const int rowb = (y0 - 1) * {X * es};')
-    L.append('    auto fbase = [&](const void* b) { const int a = (int)((unsigned long long)b & 127ull); '
-             'return ((a + rowb) & ~127) - a; };')
-    L.append('    auto fshift = [&](const void* b) { const int a = (int)((unsigned long long)b & 127ull); '
-             'return (a + rowb) - ((a + rowb) & ~127); };')
-    L.append(f'    int vo[{NIS}];')
-    L.append('    #pragma unroll')
-    L.append(f'    for (int i = 0; i < {NIS}; ++i) {{ const int k = i * 64 + lane; vo[i] = k < {nsp} ? 16 * k : 0x40000000; }}')
-    L.append('    auto issue = [&](const int q, const int slot) {')
-    L.append(f'      const {et}* pb = {_ws_plane_base(S, 1, "q")};')
-    L.append('      const int b0 = pb ? fbase(pb) : 0;')
-    L.append(f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? pb : f_{S.name}), '
-             f'(short)0, pb ? (int)((YX * {es} + 3) & ~3ll) : 0, 0x00020000);')
-    L.append(f'      {et}* dst = lds + {STG0} + slot * {SSLOT};')
-    L.append('      #pragma unroll')
-    L.append(f'      for (int i = 0; i < {NIS}; ++i)')
-    L.append(f'        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + i * '
-             f'{64 * VE}), 16, vo[i] + b0, 0, 0, {int(cfg.BLAUX)});')
-    L.append('    };')
-    L.append('    auto convert = [&](const int q, const int sslot, const int islot) {')
-    L.append(f'      const {et}* pb = {_ws_plane_base(S, 1, "q")};')
-    L.append('      const int sh = pb ? fshift(pb) : 0;')
-    L.append(f'      const char* st = (const char*)(lds + {STG0} + sslot * {SSLOT});')
-    L.append(f'      {et}* img = lds + islot * {SLOT};')
-    L.append(f'      for (int r = 0; r < {TY + 2}; ++r) {{')
-    L.append('        const int yy = y0 - 1 + r;')
-    L.append('        const bool rowok = yy >= 0 && yy < Y;')
-    L.append(f'        const int rb = __builtin_amdgcn_readfirstlane(sh + r * {X * es}), m = rb & 15, base = rb - m;')
-    L.append('        #pragma unroll')
-    L.append(f'        for (int cc = 0; cc < {ncc}; ++cc) {{')
-    L.append('          const int c = cc * 64 + lane;')
-    L.append(f'          if (c < {CPR}) {{')
-    L.append('            const u32x4 v0 = *(const u32x4*)(st + base + 16 * c), v1 = *(const u32x4*)(st + base + 16 * c + 16);')
-    L.append('            unsigned w0, w1, w2, w3, w4;')
-    L.append('            switch (m >> 2) {')
-    L.append('              case 0: w0 = v0.x; w1 = v0.y; w2 = v0.z; w3 = v0.w; w4 = v1.x; break;')
-    L.append('              case 1: w0 = v0.y; w1 = v0.z; w2 = v0.w; w3 = v1.x; w4 = v1.y; break;')
-    L.append('              case 2: w0 = v0.z; w1 = v0.w; w2 = v1.x; w3 = v1.y; w4 = v1.z; break;')
-    L.append('              default: w0 = v0.w; w1 = v1.x; w2 = v1.y; w3 = v1.z; w4 = v1.w; break;')
-    L.append('            }')
-    L.append('            const unsigned b = (unsigned)(m & 3);')
-    L.append('            u32x4 o = {__builtin_amdgcn_alignbyte(w1, w0, b), __builtin_amdgcn_alignbyte(w2, w1, b), '
-             '__builtin_amdgcn_alignbyte(w3, w2, b), __builtin_amdgcn_alignbyte(w4, w3, b)};')
-    L.append('            if (!rowok) o = (u32x4)(0u);')
-    if kx:
-        L.append(f'            if (c == {CPR - 1}) {{ ' + ' '.join(f'o.{"xyzw"[d]} &= {keep[d]:#x}u;' for d in range(4)
-                                                             if keep[d] != 0xffffffff) + ' }')
-    L.append(f'            *(u32x4*)(img + r * {NPR * VE} + {VE} + c * {VE}) = o;')
-    L.append('          }')
-    L.append('        }')
-    L.append('      }')
-    L.append('    };')
-    L.append(f'    for (int i = 0; i < {D}; ++i)')
-    L.append(f'      if (i < nplanes) issue(zb - 1 + i, i % {NSS});')
-    L.append('    for (int j = 0; j < nplanes; ++j) {')
-    L.append(f'      const int after = min({D - 1}, nplanes - 1 - j);')
-    L.append('      switch (after) {')
-    for a in range(D):
-        L.append(f'        case {a}: asm volatile("s_waitcnt vmcnt({a * NIS})" ::: "memory"); break;')
-    L.append('      }')
-    L.append(f'      convert(zb - 1 + j, j % {NSS}, j % {NS});')
-    L.append('      asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");')
-    L.append(f'      if (j + {D} < nplanes) issue(zb - 1 + j + {D}, (j + {D}) % {NSS});')
-    L.append('    }')
-    L.append('    return;')
-    L.append('  }')
-    return L

@@ -108,7 +108,7 @@ def _band_config(ir, ve, shape, over):
     pad = int(over.get('BPAD', BAND_PAD_BOX if ntaps > 12 else 0))
     reg = int(over.get('BREG', BAND_REG_STAR_ODD if ntaps <= 12 and es == 2 and X % 2 else 0))
     g = band_geometry(X, TY, R, D, es, pad, reg)
-    if TY % R or g['NCT'] > 960 or D * g.get('NIS', g['NI']) > 63 or g['lds_bytes'] > 160 * 1024:
+    if TY % R or g['NCT'] > 960 or D * g['NI'] > 63 or g['lds_bytes'] > 160 * 1024:
         raise ValueError(f'band schedule: BTY={TY} BAND={R} D={D} do not fit rows of {X} elements')
     nty, Z = -(-int(shape[-2]) // TY), int(shape[0])
     min_wg = BAND_MIN_WG

@@ -196,14 +196,12 @@ def test_band_unaligned_vs_oracle(case_shape, bh):
 @pytest.mark.gpu
 @pytest.mark.parametrize('case_shape', UNALIGNED, ids=lambda c: f'{c[0]}-{c[1][2]}')
 @pytest.mark.parametrize('bh', ['zeros', None])
-@pytest.mark.parametrize('knob', [{'BZF': 0}, {'BREG': 1}, {'BREG': 2}, {'BREG': 2, 'D': 1}],
-                         ids=['BZF0', 'BREG1', 'BREG2', 'BREG2D1'])
+@pytest.mark.parametrize('knob', [{'BZF': 0}, {'BREG': 1}], ids=['BZF0', 'BREG1'])
 def test_band_unaligned_variants_vs_oracle(case_shape, bh, knob):
     """Unaligned rows, forward and adjoint vs the oracle: ``BZF=0`` (no loader zero fill past each row end; the
     compute lanes of a row's last chunk zero its first element past X in registers) and ``BREG=1`` (a padded image
     filled through registers: row pieces read at the dword at or below them, realigned by v_alignbyte, cells past X
-    zeroed, written with ds_write_b128) and ``BREG=2`` (the band's rows as one block LDS-DMA'd from a 128-byte aligned
-    start into staging slots, realigned row by row into the padded image by the loader wave)."""
+    zeroed, written with ds_write_b128)."""
     name, shape = case_shape
     _band_vs_oracle(next(c for c in CASES if c[0] == name), shape, bh, **knob)
 
