@@ -43,13 +43,17 @@ def stream(f, stencil, xp):
     return xp.stack(comps, -1) if xp.__name__ != 'torch' else xp.stack(comps, dim=-1)
 
 
-def collide(f, omega, stencil, compressible, xp):
+def collide(f, omega, stencil, compressible, xp, force_model=None, force=None):
+    """SRT collision; ``force_model`` 'simple' (+3 w_i c_i·F) or 'guo' (velocity shifted by F/2, + w_i (1 − ω/2)
+    (3 (c_i − u)·F + 9 (c_i·u)(c_i·F))) with a constant body force ``force`` (lbmpy's published force models)."""
     dirs, w = SETS[stencil]
     D = len(dirs[0])
     rho = f.sum(-1)
     u = []
     for a in range(D):
         m = sum(c[a] * f[..., i] for i, c in enumerate(dirs) if c[a])
+        if force_model == 'guo':
+            m = m + force[a] / 2
         u.append(m / rho if compressible else m)
     usq = sum(ua * ua for ua in u)
     out = []
@@ -57,20 +61,28 @@ def collide(f, omega, stencil, compressible, xp):
         cu = sum(ca * ua for ca, ua in zip(c, u) if ca)
         poly = 3 * cu + 4.5 * cu * cu - 1.5 * usq
         feq = float(w[i]) * rho * (1 + poly) if compressible else float(w[i]) * (rho + poly)
-        out.append(f[..., i] + omega * (feq - f[..., i]))
+        g = f[..., i] + omega * (feq - f[..., i])
+        if force_model is not None:
+            cF = sum(ca * Fa for ca, Fa in zip(c, force) if ca)
+            if force_model == 'simple':
+                g = g + 3 * float(w[i]) * cF
+            else:
+                cmuF = sum((ca - ua) * Fa for ca, ua, Fa in zip(c, u, force))
+                g = g + float(w[i]) * (1 - omega / 2) * (3 * cmuF + 9 * cu * cF)
+        out.append(g)
     return xp.stack(out, -1) if xp.__name__ != 'torch' else xp.stack(out, dim=-1)
 
 
-def step(f, omega, stencil='D2Q9', compressible=False, xp=None):
+def step(f, omega, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None):
     """One stream-pull-collide time step on a periodic domain (``f``: ``[*spatial, q]``)."""
     if xp is None:
         import numpy as xp
-    return collide(stream(f, stencil, xp), omega, stencil, compressible, xp)
+    return collide(stream(f, stencil, xp), omega, stencil, compressible, xp, force_model, force)
 
 
-def run(f, omega, steps, stencil='D2Q9', compressible=False, xp=None):
+def run(f, omega, steps, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None):
     for _ in range(steps):
-        f = step(f, omega, stencil, compressible, xp)
+        f = step(f, omega, stencil, compressible, xp, force_model, force)
     return f
 
 

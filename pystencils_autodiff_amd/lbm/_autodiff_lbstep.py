@@ -138,7 +138,10 @@ class AutoDiffLatticeBoltzmannStep:
         # periodic kernels (wrapped reads, every cell written) and the transposed adjoint — for the rules of
         # ``create_lb_update_rule`` written through the collision's structure (``create_lb_adjoint_rule``)
         backward = None
-        if getattr(update_rule, 'stencil', None) is not None and not time_constant_fields:
+        # (a force term that depends on the pdfs — Guo's, through u — is not in that structure: the generic
+        # transposed derivation then; the 'simple' term is a constant and changes no derivative)
+        if getattr(update_rule, 'stencil', None) is not None and not time_constant_fields and \
+                getattr(update_rule, 'force_model', None) in (None, 'simple'):
             from ._method import create_lb_adjoint_rule
             backward = create_lb_adjoint_rule(update_rule)
         self._autodiff = AutoDiffOp(update_rule, 'LBM', boundary_handling='periodic', diff_mode='transposed',
@@ -164,6 +167,7 @@ class AutoDiffLatticeBoltzmannStep:
             ((lambda v=rr: float(v)) if rr is not None else None)
         # (PSAD_LBM_LATTICE=0: the AutoDiffOp kernels instead — tests of that path, A/B probes)
         self._lattice = {} if (getattr(update_rule, 'stencil', None) is not None and not time_constant_fields
+                               and getattr(update_rule, 'force_model', None) is None
                                and os.environ.get('PSAD_LBM_LATTICE', '1') != '0'
                                and not self._additional_fields and self._omega_of is not None
                                and np.dtype(src.dtype.numpy_dtype) in (np.float32, np.float64)) else None
@@ -517,7 +521,8 @@ class AutoDiffLatticeBoltzmannStep:
         if str(backend).lower() not in ('torch_native', 'torch'):
             raise NotImplementedError(f"backend '{backend}': only the torch backends are built")
         if force_input_tensor is not None:
-            raise NotImplementedError('force models are not built (SRT without forcing)')
+            raise NotImplementedError('a per-cell force field is not built (constant body forces: the update '
+                                      "rule's force_model / force)")
         if additional_fields_to_tensor_map:
             raise NotImplementedError('additional fields of the update rule are not built')
         setter = self._e2e_ops.get('setter') if hasattr(self, '_e2e_ops') else None
@@ -545,7 +550,8 @@ class AutoDiffLatticeBoltzmannStep:
         from ._method import macroscopic_getter
         rho, vel = self._macroscopic_fields()
         pdf = self._pdf_io_field()
-        ac = macroscopic_getter(self.method, pdf, rho, vel, getattr(self._update_rule, 'compressible', False))
+        ac = macroscopic_getter(self.method, pdf, rho, vel, getattr(self._update_rule, 'compressible', False),
+                                getattr(self._update_rule, 'force_model', None), getattr(self._update_rule, 'force', None))
         op = AutoDiffOp(ac, 'LBM_GetMacroscopicValues', diff_mode='transposed', **kernel_compilation_kwargs)
         return op.create_tensorflow_op(use_cuda=self._gpu, backend=backend)
 

@@ -13,7 +13,12 @@ incompressible form with reference density 1), and the ``stream_pull_collide`` k
     dst_i(x) = f_i + ω (feq_i − f_i)
 
 plus the macroscopic getter (ρ, u from the pdfs) and setter (pdfs = feq(ρ, u)) the step's
-``create_macroscopic_*_op`` wrap. Parity with lbmpy is unpinned (lbmpy is absent); the oracle
+``create_macroscopic_*_op`` wrap. A constant body force F (``force_model``, lbmpy's ``forcemodels`` [ext]):
+
+    'simple':  dst_i += 3 w_i (c_i·F)
+    'guo':     u = (Σ_i c_i f_i + F/2) (/ρ),   dst_i += w_i (1 − ω/2) (3 (c_i − u)·F + 9 (c_i·u)(c_i·F))
+
+(the getter reports Guo's shifted velocity). Parity with lbmpy is unpinned (lbmpy is absent); the oracle
 (``oracle/lbm.py``) restates the same equations independently with array rolls.
 """
 import sympy as sp
@@ -65,14 +70,46 @@ class LBStencil:
         return self.directions.index(tuple(-c for c in self.directions[i]))
 
 
-def _moments(stencil, f, compressible):
+def _moments(stencil, f, compressible, shift=None):
+    """ρ and u of the pdfs ``f``; ``shift``: a velocity shift per axis added to the momentum (Guo's F/2)."""
     rho = sp.Symbol('rho')
     us = sp.symbols(f'u_:{stencil.D}')
     subs = [ps.Assignment(rho, sum(f))]
     for a in range(stencil.D):
         mom = sum(c[a] * fi for c, fi in zip(stencil.directions, f) if c[a])
+        if shift is not None:
+            mom = mom + shift[a]
         subs.append(ps.Assignment(us[a], mom / rho if compressible else mom))
     return rho, us, subs
+
+
+FORCE_MODELS = ('simple', 'guo')
+
+
+def _force(force_model, force, stencil):
+    """(velocity shift or None, per-direction force term builder) of a constant body force."""
+    if force_model is None:
+        if force is not None:
+            raise ValueError('force given without force_model')
+        return None, None
+    fm = str(force_model).lower()
+    if fm not in FORCE_MODELS:
+        raise NotImplementedError(f"force_model '{force_model}': one of {FORCE_MODELS}")
+    F = [sp.sympify(v) for v in force]
+    if len(F) != stencil.D:
+        raise ValueError(f'force needs {stencil.D} components')
+
+    def term(i, us, omega):
+        c = stencil.directions[i]
+        w = stencil.weights[i]
+        cF = sum(ca * Fa for ca, Fa in zip(c, F) if ca)
+        if fm == 'simple':
+            return 3 * w * cF
+        cu = sum(ca * ua for ca, ua in zip(c, us) if ca)
+        cmu_F = sum((ca - ua) * Fa for ca, ua, Fa in zip(c, us, F))
+        return w * (1 - omega / 2) * (3 * cmu_F + 9 * cu * cF)
+    shift = [Fa / 2 for Fa in F] if fm == 'guo' else None
+    return shift, term
 
 
 def _feq(stencil, i, rho, us, compressible):
@@ -85,12 +122,14 @@ def _feq(stencil, i, rho, us, compressible):
 
 
 def create_lb_update_rule(stencil='D2Q9', relaxation_rate=None, compressible=False, src_field=None, dst_field=None,
-                          data_type='float64', layout='fzyx', kernel_type='stream_pull_collide'):
+                          data_type='float64', layout='fzyx', kernel_type='stream_pull_collide', force_model=None,
+                          force=None):
     """SRT (BGK) ``stream_pull_collide`` update rule (lbmpy ``create_lb_update_rule(stencil=…, method='srt',
     relaxation_rate=…, compressible=…, kernel_type='stream_pull_collide')`` [ext]). ``relaxation_rate`` =
     ω: a number, or a sympy symbol left as a kernel parameter (default: the symbol ``omega``). Fields:
     ``src(q)``/``dst(q)`` vector fields in ``layout`` (``'fzyx'``: components slowest, lbmpy's default)
-    unless given."""
+    unless given. ``force_model`` ('simple' or 'guo') with ``force``: a constant body force (numbers or symbols per
+    axis) — such rules run on the rule's own AutoDiffOp kernels, not the lattice schedule."""
     if kernel_type != 'stream_pull_collide':
         raise NotImplementedError("only kernel_type='stream_pull_collide' is restated")
     st = stencil if isinstance(stencil, LBStencil) else LBStencil(stencil)
@@ -98,13 +137,17 @@ def create_lb_update_rule(stencil='D2Q9', relaxation_rate=None, compressible=Fal
         src_field, dst_field = ps.fields(f"src({st.Q}), dst({st.Q}): {data_type}[{st.D}D]", layout=layout)
     omega = sp.Symbol('omega') if relaxation_rate is None else sp.sympify(relaxation_rate)
     f = [src_field[tuple(-c for c in st.directions[i])](i) for i in range(st.Q)]
-    rho, us, subs = _moments(st, f, compressible)
-    main = [ps.Assignment(dst_field.center(i), f[i] + omega * (_feq(st, i, rho, us, compressible) - f[i]))
+    shift, term = _force(force_model, force, st)
+    rho, us, subs = _moments(st, f, compressible, shift)
+    main = [ps.Assignment(dst_field.center(i), f[i] + omega * (_feq(st, i, rho, us, compressible) - f[i]) +
+                          (term(i, us, omega) if term else 0))
             for i in range(st.Q)]
     ac = ps.AssignmentCollection(main, subs)
     ac.stencil = st
     ac.compressible = compressible
     ac.relaxation_rate = omega
+    ac.force_model = None if force_model is None else str(force_model).lower()
+    ac.force = None if force is None else tuple(sp.sympify(v) for v in force)
     return ac
 
 
@@ -147,11 +190,14 @@ def create_lb_adjoint_rule(update_rule, diff_fields_prefix='diff'):
     return ps.AssignmentCollection(main, subs)
 
 
-def macroscopic_getter(stencil, pdf_field, density_field, velocity_field, compressible=False):
-    """ρ = Σ f_i, u = Σ c_i f_i (/ρ): lbmpy's ``macroscopic_values_getter`` [ext] for the SRT method."""
+def macroscopic_getter(stencil, pdf_field, density_field, velocity_field, compressible=False, force_model=None,
+                       force=None):
+    """ρ = Σ f_i, u = Σ c_i f_i (/ρ): lbmpy's ``macroscopic_values_getter`` [ext] for the SRT method (Guo's
+    forcing: the velocity shifted by F/2)."""
     st = stencil if isinstance(stencil, LBStencil) else LBStencil(stencil)
     f = [pdf_field.center(i) for i in range(st.Q)]
-    rho, us, subs = _moments(st, f, compressible)
+    shift, _ = _force(force_model, force, st)
+    rho, us, subs = _moments(st, f, compressible, shift)
     main = [ps.Assignment(density_field.center, rho)] + \
         [ps.Assignment(velocity_field.center(a), us[a]) for a in range(st.D)]
     return ps.AssignmentCollection(main, subs)

@@ -542,3 +542,75 @@ def test_lbm_lid_driven_cavity_gpu(dtype):
     out.backward(g.to(tdt))
     (gref,) = torch.autograd.grad(ref, ft, g)
     assert float((x.grad.double() - gref).abs().max()) <= 10 * tol * float(gref.abs().max())
+
+
+FORCE_CASES = [('D2Q9', (10, 7), False, 'guo'), ('D2Q9', (9, 12), True, 'guo'), ('D2Q9', (8, 6), True, 'simple'),
+               ('D3Q19', (6, 5, 4), False, 'guo')]
+
+
+def _forced(stencil, shape, compressible, model, target, dtype='float64'):
+    force = (1e-3, -2e-3, 5e-4)[:len(shape)]
+    rule = lbm.create_lb_update_rule(stencil, compressible=compressible, force_model=model, force=force,
+                                     data_type=dtype)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.4, target=target)
+    assert step._lattice is None                     # forced rules: the rule's own AutoDiffOp kernels
+    return step, force
+
+
+@pytest.mark.parametrize('stencil,shape,compressible,model', FORCE_CASES)
+def test_lbm_force_models_cpu_vs_oracle(stencil, shape, compressible, model):
+    """A constant body force (lbmpy's 'simple' / 'guo' force models restated; parity unpinned vs lbmpy): T steps
+    and the adjoint of T steps on the C kernels vs the oracle's forced collision and torch's reverse mode."""
+    import torch
+    step, force = _forced(stencil, shape, compressible, model, 'cpu')
+    f0 = _init(stencil, shape, compressible, seed=5)
+    T = 3
+    step.set_pdfs(f0)
+    step.run(T, record=True)
+    ft = torch.tensor(f0, requires_grad=True)
+    ref = OL.run(ft, 1.4, T, stencil, compressible, xp=torch, force_model=model, force=force)
+    assert np.abs(step.pdf_array - ref.detach().numpy()).max() <= 1e-13 * np.abs(f0).max()
+    unforced = OL.run(torch.tensor(f0), 1.4, T, stencil, compressible, xp=torch)
+    assert float((ref - unforced).abs().max()) > 1e-5          # the force is in
+    g = np.random.default_rng(6).standard_normal(f0.shape)
+    (gref,) = torch.autograd.grad(ref, ft, torch.tensor(g))
+    step.set_adjoint_pdfs(g)
+    step.run_backward(T)
+    assert np.abs(step.adjoint_pdf_array - gref.numpy()).max() <= 1e-12 * np.abs(gref.numpy()).max()
+
+
+def test_lbm_force_model_getter_shift():
+    """Guo forcing: the macroscopic getter reports the velocity shifted by F/2 (/ρ)."""
+    import torch
+    step, force = _forced('D2Q9', (6, 5), True, 'guo', 'cpu')
+    f0 = _init('D2Q9', (6, 5), True, seed=8)
+    rho, vel = step.create_macroscopic_getter_op().apply(torch.tensor(f0))
+    dirs, _ = OL.SETS['D2Q9']
+    r = f0.sum(-1)
+    for a in range(2):
+        m = sum(c[a] * f0[..., i] for i, c in enumerate(dirs))
+        assert np.abs(vel.numpy()[..., a] - (m + force[a] / 2) / r).max() < 1e-13
+    with pytest.raises(NotImplementedError):
+        lbm.create_lb_update_rule('D2Q9', force_model='luo', force=(0, 0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('stencil,shape,compressible,model', FORCE_CASES)
+def test_lbm_force_models_gpu_vs_oracle(stencil, shape, compressible, model):
+    """The forced rules on the HIP kernels (the rule's AutoDiffOp kernels, transposed-mode adjoint)."""
+    import torch
+    step, force = _forced(stencil, shape, compressible, model, 'gpu')
+    f0 = _init(stencil, shape, compressible, seed=5)
+    T = 3
+    step.set_pdfs(torch.tensor(f0, device='cuda'))
+    step.run(T, record=True)
+    ft = torch.tensor(f0, requires_grad=True)
+    ref = OL.run(ft, 1.4, T, stencil, compressible, xp=torch, force_model=model, force=force)
+    got = step.pdf_array.double().cpu().numpy()
+    assert np.abs(got - ref.detach().numpy()).max() <= 1e-12 * np.abs(f0).max()
+    g = np.random.default_rng(6).standard_normal(f0.shape)
+    (gref,) = torch.autograd.grad(ref, ft, torch.tensor(g))
+    step.set_adjoint_pdfs(torch.tensor(g, device='cuda'))
+    step.run_backward(T)
+    gg = step.adjoint_pdf_array.double().cpu().numpy()
+    assert np.abs(gg - gref.numpy()).max() <= 1e-11 * np.abs(gref.numpy()).max()
