@@ -25,9 +25,15 @@ the MI355X layer's scale-out for the 3-D configs (BASELINE configs 4 and 5):
 
 On the CPU (``gloo``) the same exchange runs and the C kernel evaluates a
 ghosted copy — used by the multi-process tests.
+
+fzyx (SoA) vector fields: every component is a C-contiguous spatial array of its own, and the GPU kernels
+bind each as a scalar field (``kernel_ir.split_soa``). A slab of such a field therefore exchanges one face
+pair PER COMPONENT (each face contiguous, in the same RCCL group) and hands the kernel one halo pair per
+component field (``u__c0``, ``u__c1``, …).
 """
 import ctypes
 import glob
+import itertools
 import os
 
 import torch
@@ -197,8 +203,6 @@ class ZSlabOp:
         for k in self.kernels.values():
             if k.ir.ndim != 3 and k.ir.ndim != 2:
                 raise ValueError('z-slab decomposition needs 2-D or 3-D fields')
-            if any(f.is_soa for f in k.ir.fields):
-                raise NotImplementedError('z-slab decomposition of fzyx (SoA) vector fields')
             if k.ir.periodic:
                 # a periodic lattice needs a wrap-around exchange between the first and last rank (and the
                 # kernels' own wrapped reads disabled along z): not built
@@ -239,6 +243,32 @@ class ZSlabOp:
         if self._halo is not None:
             self._halo.close()
             self._halo = None
+
+    @staticmethod
+    def _units(f, t):
+        """The exchange units of stencil field ``f``'s slab ``t`` as ``[(halo name, tensor)]``: the slab itself, or
+        for an fzyx (SoA) field one C-contiguous component array per component under the kernels' component field
+        names (``Field.component_field``, ``kernel_ir.split_soa``)."""
+        if not f.is_soa:
+            return [(f.name, t)]
+        sdim = t.dim() - f.index_dimensions
+        return [(f.component_field(idx).name, t[(Ellipsis,) + idx])
+                for idx in itertools.product(*[range(int(n)) for n in t.shape[sdim:]])]
+
+    @staticmethod
+    def _layout(f, t):
+        """``t`` in the memory order the kernels expect for field ``f``: C order, or fzyx (components-first) for
+        an SoA field — copied only if it is not already."""
+        if not f.is_soa:
+            return t.contiguous()
+        sdim = t.dim() - f.index_dimensions
+        from .backends._torch_native import _soa_empty
+        want = _soa_empty(tuple(t.shape), sdim, torch.empty, t.dtype, 'meta').stride()
+        if tuple(t.stride()) == tuple(want):
+            return t
+        out = _soa_empty(tuple(t.shape), sdim, torch.empty, t.dtype, t.device)
+        out.copy_(t)
+        return out
 
     def _radius(self, kernel, field):
         return max([abs(r.offsets[0]) for r in kernel.ir.reads if r.field.name == field.name] + [0])
@@ -322,12 +352,13 @@ class ZSlabOp:
             return
         pending, halos = [], {}
         for f in stencil:
-            t = kwargs[f.name]
-            key = (which, f.name, rz, t.dtype, tuple(t.shape[1:]), t.device)
-            works, lo, hi = exchange_halos(t, rz, self.group, self._bufs.get(key))
-            self._bufs[key] = (lo, hi)
-            pending += works
-            halos[f.name] = (lo, hi)
+            # the GPU kernels take one halo pair per fzyx component; the CPU path ghosts whole slabs
+            for name, t in (self._units(f, kwargs[f.name]) if self.use_cuda else [(f.name, kwargs[f.name])]):
+                key = (which, name, rz, t.dtype, tuple(t.shape[1:]), t.device)
+                works, lo, hi = exchange_halos(t, rz, self.group, self._bufs.get(key))
+                self._bufs[key] = (lo, hi)
+                pending += works
+                halos[name] = (lo, hi)
         # interior-only kernels always take the limits (their own bounds would skip the slab's end planes)
         kz = None if (ir.zeros or ir.ghost_layers == 0) else zlim
         if self.use_cuda:
@@ -433,7 +464,7 @@ class ZSlabOp:
             k = self.kernels.get(which)
             if k is None:
                 continue
-            named = [(f.name, slabs[f.name]) for f in k.ir.stencil_fields if f.name in slabs]
+            named = [u for f in k.ir.stencil_fields if f.name in slabs for u in self._units(f, slabs[f.name])]
             rz = max([self._radius(k, f) for f in k.ir.stencil_fields] + [0])
             if named and rz:
                 planes, _ = self._face_planes(halo, named, rz)
@@ -447,7 +478,7 @@ class ZSlabOp:
         cur = torch.cuda.current_stream(halo.device)
         halo.ev_faces.record(cur)
         halo.stream.wait_event(halo.ev_faces)         # the faces are final; the last sweep's reads are done
-        planes, halos = self._face_planes(halo, [(f.name, kwargs[f.name]) for f in stencil], rz)
+        planes, halos = self._face_planes(halo, [u for f in stencil for u in self._units(f, kwargs[f.name])], rz)
         halo.exchange(planes, peer_lo, peer_hi)
         compiled = k.compile()
         zl = kwargs[k.ir.fields_written[0].name].shape[0]
@@ -461,21 +492,30 @@ class ZSlabOp:
         self._launch_faces(compiled, halos, faces, kz, kwargs)
 
     def _alloc(self, kernel, name, like, dtype, read):
-        """An output / gradient slab: zeros when the kernel accumulates into it or (CPU) leaves a border;
-        under ``boundary_handling=None`` on the GPU uninitialised plus one zero fill of the planes, rows
-        and columns the kernel does not write (the reference's ``torch.zeros`` values)."""
+        """An output / gradient slab of field ``name`` (the spatial shape of ``like``, the field's components; fzyx
+        fields components-first): zeros when the kernel accumulates into it or (CPU) leaves a border; under
+        ``boundary_handling=None`` on the GPU uninitialised plus one zero fill of the planes, rows and columns the
+        kernel does not write (the reference's ``torch.zeros`` values)."""
+        from .backends._torch_native import _soa_components, _soa_empty
         ir = kernel.ir
-        if read or (not ir.zeros and ir.ghost_layers and not like.is_cuda):
-            return torch.zeros_like(like, dtype=dtype)
-        t = torch.empty_like(like, dtype=dtype)
-        if not ir.zeros and ir.ghost_layers:
+        sdim = ir.ndim
+        f = next((g for g in ir.fields if g.name == name), None)
+        comps = tuple(int(n) for n in f.index_shape) if f is not None and f.index_dimensions else ()
+        shape = tuple(like.shape[:sdim]) + comps
+        soa = f is not None and f.is_soa
+        zero = read or (not ir.zeros and ir.ghost_layers and not like.is_cuda)
+        factory = torch.zeros if zero else torch.empty
+        t = _soa_empty(shape, sdim, factory, dtype, like.device) if soa else \
+            factory(shape, dtype=dtype, device=like.device)
+        if not zero and not ir.zeros and ir.ghost_layers:
             from .backends.hip_kernel import zero_border
-            bounds = ir.iteration_bounds(tuple(like.shape[:ir.ndim]))
+            bounds = ir.iteration_bounds(tuple(like.shape[:sdim]))
             bounds[0] = self.z_limits(kernel, like.shape[0])
             ncomp = 1
-            for n in like.shape[ir.ndim:]:
-                ncomp *= int(n)
-            zero_border(t, bounds, ncomp)
+            for n in comps:
+                ncomp *= n
+            for p in (_soa_components(t, sdim) if soa else [t]):
+                zero_border(p, bounds, 1 if soa else ncomp)
         return t
 
     def autograd_function(self):
@@ -495,6 +535,7 @@ class ZSlabOp:
         bwd_outputs = [f.name for f in op.backward_output_fields]
         bwd_read = {r.field.name for r in bk.ir.reads}        # accumulated adjoints start from zeros
         adj = {f.name: op.adjoint_name(f) for f in fwd_inputs + fwd_outputs}
+        bwd_field = {f.name: f for f in bk.ir.fields}
 
         def tdtype(f):
             return getattr(torch, f.dtype.numpy_dtype.name)
@@ -504,7 +545,7 @@ class ZSlabOp:
 
             @staticmethod
             def forward(ctx, *slabs):
-                kw = {f.name: t.contiguous() for f, t in zip(fwd_inputs, slabs) if f.name in fwd_names}
+                kw = {f.name: zop._layout(f, t) for f, t in zip(fwd_inputs, slabs) if f.name in fwd_names}
                 kw.update({s.name: ZSlabFunction.class_kwargs[s.name] for s in fk.ir.scalars})
                 outs = [zop._alloc(fk, f.name, slabs[0], tdtype(f), f.name in fwd_read) for f in fwd_outputs]
                 kw.update({f.name: t for f, t in zip(fwd_outputs, outs)})
@@ -521,8 +562,10 @@ class ZSlabOp:
                 kw.update({s.name: ZSlabFunction.class_kwargs[s.name] for s in bk.ir.scalars})
                 like = next(g for g in grads if g is not None)
                 for f, g in zip(fwd_outputs, grads):
-                    if adj[f.name] in bwd_names:
-                        kw[adj[f.name]] = (g if g is not None else torch.zeros_like(like)).contiguous()
+                    a = adj[f.name]
+                    if a in bwd_names:
+                        kw[a] = zop._layout(bwd_field[a], g) if g is not None else \
+                            zop._alloc(bk, a, like, tdtype(f), True)
                 res = {}
                 for name in bwd_outputs:
                     res[name] = zop._alloc(bk, name, like, like.dtype, name in bwd_read)
@@ -607,6 +650,8 @@ class _NativeSlab:
         for k in (fk, bk):
             if not (k.ir.zeros or k.ir.ghost_layers == 0):
                 return None                 # interior-only kernels: border fills and global z limits
+            if any(f.is_soa for f in k.ir.fields):
+                return None                 # fzyx vector fields: per-component halos and strided slabs
         for a in args:
             if not a.is_cuda or not a.is_contiguous() or a.data_ptr() % 32 or a.device != args[0].device or \
                     str(a.dtype).replace('torch.', '') not in _SCALAR_TYPE or tuple(a.shape) != tuple(args[0].shape):
