@@ -119,6 +119,19 @@ def abs_terms(collection, inputs, boundary_handling='zeros'):
                        boundary_handling=boundary_handling)
 
 
+def assert_cells_linear(actual, ref, collection, inputs, boundary_handling, storage, what=''):
+    """``assert_cells`` for a linear ``collection`` (Σ|terms| from the inputs, its term count); a nonlinear one keeps
+    the caller's field-scaled check only. Returns whether the element-wise check ran."""
+    if abs_linear(collection) is None:
+        return False
+    absr = abs_terms(collection, inputs, boundary_handling)
+    for name, r in (ref.items() if isinstance(ref, dict) else [(None, ref)]):
+        a = actual[name] if isinstance(actual, dict) else actual
+        n = name if name is not None else next(iter(absr))
+        assert_cells(a, r, absr[n], n_terms(collection), storage, f'{what} {n}')
+    return True
+
+
 def n_terms(collection):
     """Most terms in one main assignment's linear expansion (the products the kernel sums per cell)."""
     ac = abs_linear(collection)

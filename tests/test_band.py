@@ -239,6 +239,8 @@ def test_band_zslab_launch_pattern_bitwise(bh):
     assert torch.equal(torch.cat(outs), full)
     ref = OE.evaluate(op.forward_assignments, {'u': u.double().cpu().numpy()}, boundary_handling=bh)['out']
     assert_close_rel(full.double().cpu().numpy(), ref, TOL16)
+    assert_cells(full.double().cpu().numpy(), ref, abs_terms(op.forward_assignments, {'u': u.double().cpu().numpy()},
+                                                              bh)['out'], 27, np.float16, 'slab launches')
 
 
 @pytest.mark.gpu
@@ -298,6 +300,8 @@ def test_band_misaligned_views_fall_back():
         assert (k.last_variant[1].BAND > 0) == band, k.last_variant
         ref = OE.evaluate(op.forward_assignments, {'u': u.double().cpu().numpy()}, boundary_handling='zeros')['out']
         assert_close_rel(out.double().cpu().numpy(), ref, TOL16, f'offset {off}')
+        assert_cells(out.double().cpu().numpy(), ref, abs_terms(op.forward_assignments, {'u': u.double().cpu().numpy()})[
+            'out'], 27, np.float16, f'offset {off}')
 
 
 @pytest.mark.gpu
@@ -315,8 +319,10 @@ def test_band_two_outputs():
     torch.cuda.synchronize()
     assert k.last_variant[1].BAND == 2, k.last_variant
     ref = OE.evaluate(ac, {'u': x.astype(np.float64)}, boundary_handling='zeros')
+    absr = abs_terms(ac, {'u': x.astype(np.float64)})
     for n in ('a', 'b'):
         assert_close_rel(outs[n].double().cpu().numpy(), ref[n], TOL16, n)
+        assert_cells(outs[n].double().cpu().numpy(), ref[n], absr[n], n_terms(ac), np.float16, n)
 
 
 @pytest.mark.gpu
@@ -339,9 +345,13 @@ def test_band_through_the_op(bh, monkeypatch, shape=(12, 24, 256)):
     assert op.forward_ast_gpu.compile().last_variant[1].BAND == 4
     ref = OE.evaluate(op.forward_assignments, {'u': u.astype(np.float64)}, boundary_handling=bh)['out']
     assert_close_rel(out.detach().double().cpu().numpy(), ref, TOL16, 'forward')
+    assert_cells(out.detach().double().cpu().numpy(), ref, abs_terms(op.forward_assignments, {'u': u}, bh)['out'], 27,
+                 np.float16, 'forward')
     refb = OE.evaluate(op.backward_assignments, {'diffout': d.astype(np.float64)}, boundary_handling=bh)
     (gname,) = refb.keys()
     assert_close_rel(ut.grad.double().cpu().numpy(), refb[gname], TOL16, 'adjoint')
+    assert_cells(ut.grad.double().cpu().numpy(), refb[gname], abs_terms(op.backward_assignments, {'diffout': d}, bh)[
+        gname], 27, np.float16, 'adjoint')
 
 
 @pytest.mark.gpu
@@ -361,8 +371,10 @@ def test_band_16_row_bands_1024(shape):
         torch.cuda.synchronize()
         cfg = k.last_variant[1]
         assert (cfg.BAND, cfg.BTY, cfg.D, cfg.BMASK) == (4, 16, 1, shape[1] % 16 != 0), cfg
+        absr = abs_terms(ac, ins)
         for n, t in outs.items():
             assert_close_rel(t.double().cpu().numpy(), ref[n], TOL16, f'{which} {n} {shape}')
+            assert_cells(t.double().cpu().numpy(), ref[n], absr[n], n_terms(ac), np.float16, f'{which} {n} {shape}')
 
 
 @pytest.mark.gpu
@@ -381,9 +393,10 @@ def test_band_scalar_coefficient():
     torch.cuda.synchronize()
     assert k.last_variant[1].BAND == 4
     xs = x.astype(np.float64)
-    ref = OE.evaluate(ps.AssignmentCollection({out.center: ac.main_assignments[0].rhs.subs(a, 0.15)}),
-                      {'u': xs}, boundary_handling='zeros')['out']
+    acv = ps.AssignmentCollection({out.center: ac.main_assignments[0].rhs.subs(a, 0.15)})
+    ref = OE.evaluate(acv, {'u': xs}, boundary_handling='zeros')['out']
     assert_close_rel(res.double().cpu().numpy(), ref, TOL16)
+    assert_cells(res.double().cpu().numpy(), ref, abs_terms(acv, {'u': xs})['out'], n_terms(acv), np.float16)
 
 
 @pytest.mark.gpu

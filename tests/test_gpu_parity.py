@@ -18,7 +18,7 @@ from oracle import evaluate as OE
 from oracle import stencils as S
 from pystencils_autodiff_amd import ps
 from pystencils_autodiff_amd import workloads as W
-from tests.conftest import abs_terms, assert_cells, assert_close_rel, golden, n_terms
+from tests.conftest import abs_terms, assert_cells, assert_cells_linear, assert_close_rel, golden, n_terms
 
 pytestmark = pytest.mark.gpu
 
@@ -318,6 +318,7 @@ def test_march_tunings_vs_oracle(params, builder):
         torch.cuda.synchronize()
         assert k.last_variant[0] == 'march'
         assert_close_rel(out.cpu().numpy(), ref, 1e-3 if is16 else 1e-6, f'{params} {which}')
+        assert_cells_linear(out.cpu().numpy(), ref, ac, ins, 'zeros', dt, f'{params} {which}')
 
 
 @pytest.mark.parametrize('params', [dict(VIEW2D='yx'), dict(VIEW2D='zy'), dict(VIEW2D='yx', CX=1, NR=3),
@@ -380,6 +381,7 @@ def test_zsum_schedule_vs_oracle(params, case, bh):
         assert k.last_variant[0] == 'march' and k.last_variant[1].ZSUM
         for n, t in outs.items():
             assert_close_rel(t.cpu().numpy(), ref[n], 1e-3 if is16 else 1e-6, f'{name} {which} {n}')
+        assert_cells_linear({n: t.cpu().numpy() for n, t in outs.items()}, ref, ac, ins, bh, dt, f'{name} {which}')
 
 
 @pytest.mark.parametrize('params', [dict(ZSUM=True, CX=1, NR=2, ZC=4), dict(ZSUM=True, CX=2, NR=2, PK=True),
@@ -411,6 +413,8 @@ def test_interior_tiles_vs_oracle(params, case):
         assert k.last_variant[0] == 'march'
         for n, t in outs.items():
             assert_close_rel(t.cpu().numpy(), ref[n], 1e-3 if is16 else 1e-6, f'{name} {which} {n} {params}')
+        assert_cells_linear({n: t.cpu().numpy() for n, t in outs.items()}, ref, ac, ins, 'zeros', dt,
+                            f'{name} {which} {params}')
 
 
 def test_zsum_halo_planes_equal_full_domain():
@@ -579,6 +583,9 @@ def test_ws_loader_schedule_vs_oracle(params, shape, case):
             assert ws_geometry(k.ir, cfg) is not None, cfg
         for n, t in outs.items():
             assert_close_rel(t.cpu().numpy(), ref[n], TOL[dt], f'{name} {which} {n} {params}')
+        if dt != np.float64:
+            assert_cells_linear({n: t.cpu().numpy() for n, t in outs.items()}, ref, ac, ins, 'zeros', dt,
+                                f'{name} {which} {params}')
 
 
 @pytest.mark.parametrize('case', [
@@ -624,6 +631,9 @@ def test_row_pitch_vector_width_vs_oracle(case):
             assert k.last_variant[0] == 'march' and k.last_variant[1].VE == expect, k.last_variant
         for n, t in outs.items():
             assert_close_rel(t.cpu().numpy(), ref[n], TOL[dt], f'{name} {which} {n} {shape}')
+        if dt != np.float64:
+            assert_cells_linear({n: t.cpu().numpy() for n, t in outs.items()}, ref, ac, ins, 'zeros', dt,
+                                f'{name} {which} {shape}')
 
 
 @pytest.mark.parametrize('case', [('27pt_f16', W.stencil_27pt, np.float16, (6, 20, 136)),
@@ -651,6 +661,7 @@ def test_one_kernel_alternating_pointer_alignment(case):
         k(u=tu, out=out)
         torch.cuda.synchronize()
         assert_close_rel(out.cpu().numpy(), ref, TOL[dt], f'{name} offset {off_bytes} B')
+        assert_cells_linear(out.cpu().numpy(), ref, op.forward_assignments, {'u': u}, 'zeros', dt, f'offset {off_bytes}')
 
 
 @pytest.mark.parametrize('shape', [(10, 70, 264), (33, 97, 520), (130, 64, 256)])
@@ -676,6 +687,8 @@ def test_ws_fp16_star_default_tiles_vs_oracle(builder, shape):
         assert kind == 'march' and cfg.WS and cfg.NR == 8 and cfg.CX == 4, cfg
         for n, t in outs.items():
             assert_close_rel(t.cpu().numpy(), ref[n], TOL[np.float16], f'{which} {n} {shape}')
+        assert_cells_linear({n: t.cpu().numpy() for n, t in outs.items()}, ref, ac, ins, 'zeros', np.float16,
+                            f'{which} {shape}')
 
 
 @pytest.mark.parametrize('params', [dict(), dict(ZSUM=True, WS=True, D=2, CX=1, NR=2, ZC=3),
@@ -794,6 +807,8 @@ def test_degenerate_and_empty_shapes(shape, case):
     tol = TOL[dt]
     assert_close_rel(out, ref, tol, f'{name} forward {shape}')
     assert_close_rel(du, refb, tol, f'{name} adjoint {shape}')
+    assert_cells_linear(out, ref, op.forward_assignments, {'u': u}, 'zeros', dt, f'{name} forward {shape}')
+    assert_cells_linear(du, refb, op.backward_assignments, {'diffout': d}, 'zeros', dt, f'{name} adjoint {shape}')
 
 
 def _curl_op(bh):
@@ -963,9 +978,12 @@ def test_interior_only_border_allocation_gpu(monkeypatch, bmin, builder, shape, 
     finally:
         m.set_debug_poison(False)
     tol = 1e-3 if dt == np.float16 else 1e-6
-    assert_close_rel(out, OE.evaluate(op.forward_assignments, {'u': u}, boundary_handling=None)['out'], tol, 'out')
-    assert_close_rel(du, OE.evaluate(op.backward_assignments, {'diffout': d}, boundary_handling=None)['diffu'],
-                     tol, 'diffu')
+    ref = OE.evaluate(op.forward_assignments, {'u': u}, boundary_handling=None)['out']
+    refb = OE.evaluate(op.backward_assignments, {'diffout': d}, boundary_handling=None)['diffu']
+    assert_close_rel(out, ref, tol, 'out')
+    assert_close_rel(du, refb, tol, 'diffu')
+    assert_cells_linear(out, ref, op.forward_assignments, {'u': u}, None, dt, 'out')
+    assert_cells_linear(du, refb, op.backward_assignments, {'diffout': d}, None, dt, 'diffu')
     if bmin == 0 and not native:
         v = op.forward_ast_gpu.compile().last_variant[1]
         assert v.XB or not v.ZSUM              # zsum launches store the x ends themselves
