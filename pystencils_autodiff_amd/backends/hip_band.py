@@ -95,12 +95,14 @@ def band_geometry(X, TY, R, D, es=2, pad=0, reg=0):
                 NS=NS, lds_bytes=(NS * SLOT + 64) * es)
 
 
-def _fits(X, TY, R, D, es=2, pad=0, reg=0):
+def _fits(X, TY, R, D, es=2, pad=0, reg=0, idle=False):
+    """Whether the geometry fits (compute lanes, the loader's vmcnt budget, 80 KB of LDS). Without ``idle`` every
+    compute lane owns a task (``ntask`` a multiple of 64); with it the last compute wave may hold idle lanes."""
     g = band_geometry(X, TY, R, D, es, pad, reg)
-    return g['ntask'] % 64 == 0 and g['NCT'] <= 960 and D * g['NI'] <= 63 and g['lds_bytes'] <= 80 * 1024
+    return (idle or g['ntask'] % 64 == 0) and g['NCT'] <= 960 and D * g['NI'] <= 63 and g['lds_bytes'] <= 80 * 1024
 
 
-def band_choice(X, nstore=1, es=2, pad=0, reg=0):
+def band_choice(X, nstore=1, es=2, pad=0, reg=0, idle=False):
     """(TY, R, D) for rows of X elements, or None. fp16, measured (scripts/probes/band_ab.py,
     profiles/r03_band_ab*.log): 8-row bands of 4 rows per lane with 2 planes in flight at X = 768 and 1024
     (27-point 1024³: 0.895 ms vs 0.921 for 4-row bands of 2 rows per lane, 3 planes in flight); three workgroups
@@ -115,6 +117,18 @@ def band_choice(X, nstore=1, es=2, pad=0, reg=0):
     for TY, R, D in cands:
         if R <= rmax and _fits(X, TY, R, D, es, pad, reg):
             return TY, R, D
+    if idle:
+        # rows whose chunk count leaves no band height of whole compute waves (X = 504 / 520 / 760 / 1000 halves: 63 /
+        # 65 / 95 / 125 chunks): the last compute wave holds idle lanes. Measured through the op against the zsum
+        # schedule these rows took before (profiles/r04_op_band_idle.log, fwd+bwd): 16-row bands of 2 rows per lane
+        # first — 27-point 512²×520 0.246 vs 0.320 ms, ×504 0.217 vs 0.272, ×760 0.313 vs 0.400; fp16 7-point ×520
+        # 0.194 vs 0.290, ×504 0.195 vs 0.249 — then 16-row bands of 4 rows per lane, one plane in flight (27-point
+        # ×1000 0.402 vs 0.538). fp32: 8-row bands of 2 rows per lane (7-point ×520 0.389 vs 0.632 ms)
+        order = [(16, 2, 2), (16, 4, 1), (8, 4, 2), (8, 2, 3)] if es == 2 else [(8, 2, 2), (8, 4, 2), (4, 4, 2)]
+        for TY, R, D in order:
+            g = band_geometry(X, TY, R, D, es, pad, reg)
+            if R <= rmax and g['NCT'] <= 960 and D * g['NI'] <= 63 and g['lds_bytes'] <= 160 * 1024:
+                return TY, R, D
     return None
 
 

@@ -60,6 +60,9 @@ BAND_PAD_BOX = 1
 # (profiles/r04_op_band_ab9.log): 7-point 511³ 0.210 vs 0.217 ms (DMA row pieces + v_perm realignment); even rows
 # (510³ 0.207 vs 0.201) and box stencils (27-point 510³ 0.259 vs 0.245, 511³ 0.259 vs 0.252) keep the DMA pieces
 BAND_REG_STAR_ODD = 1
+# fp32 star stencils on rows with no whole-wave band height (idle lanes, hip_band.band_choice): the band up to this
+# row length (7-point 512²×520 0.389 vs 0.632 ms on zsum, profiles/r04_op_band_idle.log)
+BAND_F32_IDLE_MAX_X = 1024
 
 # gpu_indexing_params keys of pystencils' own GPU indexing (``block_size``, ``maximum_block_size``, …, e.g.
 # ``gpu_indexing_params={'block_size': (8, 4, 2)}`` in the reference's tests/test_graph_datahandling.py:70): they
@@ -84,9 +87,13 @@ def _band_config(ir, ve, shape, over):
     X = int(shape[-1])
     es = band_esize(ir) if plans else 0
     ntaps = max(len(pl['w']) for pl in plans) if plans else 0
-    if plans and es == 4 and not (ntaps <= 12 and X <= BAND_F32_STAR_MAX_X) and 'BAND' not in over:
+    whole = band_choice(X, len(plans), es) if plans else None
+    if plans and es == 4 and 'BAND' not in over and \
+            not (ntaps <= 12 and X <= (BAND_F32_STAR_MAX_X if whole else BAND_F32_IDLE_MAX_X)):
         return None
-    choice = band_choice(X, len(plans), es) if plans else None
+    # rows with no band height of whole compute waves: a band whose last compute wave holds idle lanes
+    choice = whole or (band_choice(X, len(plans), es, idle=True) if plans else None)
+    idle_pick = whole is None
     if choice is None:
         return None
     TY, R, D = choice
@@ -118,7 +125,7 @@ def _band_config(ir, ve, shape, over):
         long_ok = X <= BAND_STAR_LONG_MAX_X and nty * -(-Z // BAND_ZC_STAR_LONG) >= BAND_STAR_LONG_MIN_WG
         zc = BAND_ZC_STAR_LONG if long_ok else BAND_ZC_STAR
         min_wg = BAND_STAR_LONG_MIN_WG if long_ok else BAND_MIN_WG
-    elif TY == 16:
+    elif TY == 16 and not idle_pick:
         zc = BAND_ZC_BOX16
     else:
         zc = next((c for c in BAND_ZC_BOX_LADDER if nty * -(-Z // c) >= BAND_ROUND_WG), BAND_ZC_BOX_LADDER[-1])

@@ -2,7 +2,7 @@
 settled A/B rounds: op A plans its kernels with PSAD_BAND=0 (zsum ring), op B with the band default.
 
 python scripts/probes/op_band_ab.py [workload:edge[:PSAD_MARCH variant ...] ...]
-  e.g. f7:512 s27:768 s27:1024:BTRIM=0,ZMIN=48,ZMAX=48:ZMIN=48,ZMAX=48
+  e.g. f7:512 s27:768 s27:1024:BTRIM=0,ZMIN=48,ZMAX=48:ZMIN=48,ZMAX=48 s27:96x768 (a slab) s27:512x510x512 (Z x Y x X)
 """
 import os
 import sys
@@ -30,7 +30,7 @@ def inputs(name, n):
         _INPUTS.clear()
         dt = WL[name][1]
         g = torch.Generator(device='cuda').manual_seed(0)
-        shape = (n[0], n[1], n[1]) if isinstance(n, tuple) else (n, n, n)
+        shape = (n if len(n) == 3 else (n[0], n[1], n[1])) if isinstance(n, tuple) else (n, n, n)
         u = torch.rand(shape, device='cuda', generator=g).to(dt).requires_grad_(True)
         d = (torch.rand(shape, device='cuda', generator=g) * 2 - 1).to(dt)
         _INPUTS[key] = (u, d)
@@ -54,6 +54,8 @@ def make(name, n, band, march=''):
     torch.cuda.synchronize()
     cfg = op.forward_ast_gpu.compile().last_variant[1]
     os.environ.pop('PSAD_BAND', None)
+    if cfg.BAND:
+        march = f'{march} BMASK={int(cfg.BMASK)} BPAD={cfg.BPAD} ZC={cfg.ZMIN}'.strip()
     os.environ.pop('PSAD_MARCH', None)
     return step, f'BAND={cfg.BAND} BTY={cfg.BTY} {march}'
 

@@ -100,6 +100,26 @@ def test_band_default_selection_fp32_star(shape, band):
         assert (cfg.BTY, cfg.BAND, cfg.D, cfg.ZMIN) == (8, 4, 2, 16), cfg
 
 
+@pytest.mark.parametrize('builder,ve,shape,expect', [
+    (W.stencil_27pt, 8, (512, 512, 520), (16, 2, 2)), (W.stencil_27pt, 8, (512, 512, 760), (16, 2, 2)),
+    (W.stencil_27pt, 8, (512, 512, 1000), (16, 4, 1)), (lambda: W.diffusion_7pt(dtype='float16'), 8, (512, 512, 504),
+                                                        (16, 2, 2)),
+    (W.diffusion_7pt, 4, (512, 512, 520), (8, 2, 2)), (W.diffusion_7pt, 4, (512, 512, 1000), (4, 4, 2))])
+def test_band_default_selection_idle_lanes(builder, ve, shape, expect):
+    """Rows with no band height of whole compute waves take a band whose last compute wave holds idle lanes (not the
+    zsum schedule), chunk lengths from the ladder (>= 768 workgroups), not the 16-row rule's 32 planes."""
+    from pystencils_autodiff_amd.backends.hip_band import band_choice
+    op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
+    ir = HipStencilKernel(_kernel(op.forward_assignments)).ir
+    es = 16 // ve
+    assert band_choice(shape[-1], 1, es) is None and band_choice(shape[-1], 1, es, idle=True) == expect
+    cfg = default_march_config(ir, ve, shape)
+    assert (cfg.BTY, cfg.BAND, cfg.D) == expect, cfg
+    g = band_geometry(shape[-1], cfg.BTY, cfg.BAND, cfg.D, es, cfg.BPAD, cfg.BREG)
+    assert g['ntask'] % 64 != 0 and g['NCT'] <= 960, g
+    assert -(-shape[1] // cfg.BTY) * -(-shape[0] // cfg.ZMIN) >= 512, cfg
+
+
 def test_band_sources_compile():
     from pystencils_autodiff_amd.backends import hip_runtime as rt
     from pystencils_autodiff_amd.backends.hip_emitter import MarchConfig
@@ -155,7 +175,7 @@ def _band_vs_oracle(case, shape, bh, **extra):
     for which, ac in (('f', op.forward_assignments), ('b', op.backward_assignments)):
         k0 = _kernel(ac, bh, f'band_{which}')
         dt = np.dtype(k0.ir.fields[0].dtype.numpy_dtype)
-        choice = band_choice(shape[-1], 1, dt.itemsize)
+        choice = band_choice(shape[-1], 1, dt.itemsize) or band_choice(shape[-1], 1, dt.itemsize, idle=True)
         if choice is None:
             pytest.skip(f'no band geometry for rows of {shape[-1]} {dt}')
         k = _kernel(ac, bh, f'band_{which}', BAND=choice[1], **extra).compile()
@@ -175,6 +195,21 @@ def _band_vs_oracle(case, shape, bh, **extra):
             assert_close_rel(t.double().cpu().numpy(), ref[n], TOL16 if dt.itemsize == 2 else 1e-6,
                              f'{case[0]} {which} {n} {shape} {bh}')
             assert_cells(t.double().cpu().numpy(), ref[n], absr[n], n_terms(ac), dt, f'{case[0]} {which} {n} {shape} {bh}')
+
+
+# rows whose chunk count has no band height of whole compute waves: the last compute wave holds idle lanes
+IDLE = [('27pt', (9, 32, 520)), ('27pt', (7, 21, 504)), ('7pt_f16', (6, 16, 520)), ('asym_f16', (5, 19, 1000)),
+        ('asym_f32', (6, 16, 520)), ('27pt_f32', (5, 11, 504)), ('27pt', (5, 16, 760))]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case_shape', IDLE, ids=lambda c: f'{c[0]}-{c[1][2]}')
+@pytest.mark.parametrize('bh', ['zeros', None])
+def test_band_idle_lanes_vs_oracle(case_shape, bh):
+    """Band geometries whose last compute wave holds idle lanes (rows of 63 / 65 / 95 / 125 chunks), forward and
+    adjoint vs the oracle, whole and masked stores."""
+    name, shape = case_shape
+    test_band_vs_oracle(next(c for c in CASES if c[0] == name), shape, bh)
 
 
 UNALIGNED = [('27pt', (7, 16, 766)), ('7pt_f16', (6, 13, 510)), ('27pt', (5, 9, 762)), ('asym_f16', (4, 8, 254)),
