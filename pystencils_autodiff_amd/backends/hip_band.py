@@ -533,6 +533,29 @@ def emit_band(ir, name, cfg):
                 # every row of every band inside [ylo, yhi), x range = whole rows (checked at plan time)
                 B.append(f'{ind}  {{ const {vt} ov = {{{vals}}}; {st} }}')
                 continue
+            nb_t = (X % VE) * es if partial else 0           # bytes of a row's partial last chunk
+            ndw_t, nh_t = nb_t // 4, (nb_t % 4) // 2       # whole dwords, then one half (X odd)
+            if cfg.BXW and not cfg.BMBR:
+                # whole rows: no branches. A row outside [ylo, yhi) (or an idle lane's) stores at an offset past the
+                # buffer's range, which the range check drops; a partial last chunk stores its whole dwords (and
+                # half) at the row offset while its 16-byte store is dropped, every other lane the reverse
+                ro = f'((rowok & {1 << o}u) ? sofs + {o * X * es}u : 0x7ffffff0u)'
+                B.append(f'{ind}  {{ const {vt} ov = {{{vals}}}; const unsigned ro = {ro};')
+                if partial:
+                    c = 'xyzw'
+                    B.append(f'{ind}    const u32x4 ow = __builtin_bit_cast(u32x4, ov);')
+                    B.append(f'{ind}    __builtin_amdgcn_raw_buffer_store_b128(ow, ors, xtail ? 0x7ffffff0u : ro, 0, 2);')
+                    B.append(f'{ind}    const unsigned rt = xtail ? ro : 0x7ffffff0u;')
+                    if ndw_t:
+                        ty = {1: 'unsigned', 2: 'u32x2', 3: 'u32x3'}[ndw_t]
+                        B.append(f'{ind}    __builtin_amdgcn_raw_buffer_store_b{32 * ndw_t}(({ty})ow.{c[:ndw_t]}, ors, rt, 0, 2);')
+                    if nh_t:
+                        B.append(f'{ind}    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)ow.{c[ndw_t]}, ors, '
+                                 f'rt + {4 * ndw_t}u, 0, 2);')
+                else:
+                    B.append(f'{ind}    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ov), ors, ro, 0, 2);')
+                B.append(f'{ind}  }}')
+                continue
             B.append(f'{ind}  if (rowok & {1 << o}u) {{')
             B.append(f'{ind}    const {vt} ov = {{{vals}}};')
             B.append(f'{ind}    if (xfull) {{')
@@ -540,8 +563,6 @@ def emit_band(ir, name, cfg):
             B.append(f'{ind}    }} else {{')
             # not a whole in-range chunk. 'bu' rows: the partial last chunk holds X % VE cells of the row (the rest is
             # the next row's), stored as whole dwords (X·es is a multiple of 4)
-            nb_t = (X % VE) * es if partial else 0           # bytes of a row's partial last chunk
-            ndw_t, nh_t = nb_t // 4, (nb_t % 4) // 2       # whole dwords, then one half (X odd)
 
             def tail_store(vec):
                 """The partial last chunk of vector ``vec``: whole dwords, then the odd element's half."""
