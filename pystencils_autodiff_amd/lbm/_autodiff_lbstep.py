@@ -140,8 +140,10 @@ class AutoDiffLatticeBoltzmannStep:
         backward = None
         # (a force term that depends on the pdfs — Guo's, through u — is not in that structure: the generic
         # transposed derivation then; the 'simple' term is a constant and changes no derivative)
+        from ._method import force_is_field
         if getattr(update_rule, 'stencil', None) is not None and not time_constant_fields and \
-                getattr(update_rule, 'force_model', None) in (None, 'simple'):
+                getattr(update_rule, 'force_model', None) in (None, 'simple') and \
+                not force_is_field(getattr(update_rule, 'force', None)):
             from ._method import create_lb_adjoint_rule
             backward = create_lb_adjoint_rule(update_rule)
         self._autodiff = AutoDiffOp(update_rule, 'LBM', boundary_handling='periodic', diff_mode='transposed',
@@ -428,21 +430,30 @@ class AutoDiffLatticeBoltzmannStep:
         ``torch_native`` backend ignores the loops and differentiates one kernel launch)."""
         if str(backend).lower() not in ('torch_native', 'torch'):
             raise NotImplementedError(f"backend '{backend}': only the torch backends are built")
-        extra_inputs = [f for f in (input_field_to_tensor_dict or {}) if f not in (self.pdf_field, self.pdf_field.name)]
-        if extra_inputs or self._additional_fields:
-            # the kernels would need those fields bound per step (and their adjoints accumulated): not built
-            raise NotImplementedError('timestep op over update rules with additional input fields '
-                                      f'({[getattr(f, "name", f) for f in extra_inputs or self._additional_fields]})')
+        extras = list(self._additional_fields)
+        known = {self.pdf_field.name} | {f.name for f in extras}
+        unknown = [getattr(f, 'name', f) for f in (input_field_to_tensor_dict or {}) if getattr(f, 'name', f) not in known]
+        if unknown:
+            raise ValueError(f'input fields {unknown} are not read by the update rule (inputs: {sorted(known)})')
         torch = _torch()
         step = self
         T = int(num_time_steps)
+        adj = {f.name: self._autodiff.adjoint_name(f) for f in extras}
 
         class LbmTimesteps(torch.autograd.Function):
             @staticmethod
-            def forward(ctx, pdfs):
+            def forward(ctx, pdfs, *xs):
+                if len(xs) != len(extras):
+                    raise TypeError(f'{LbmTimesteps.__name__}.apply(pdfs, {", ".join(f.name for f in extras)}): '
+                                    f'{1 + len(xs)} tensors given')
+                # additional input fields (a per-cell force): constant over the steps, bound to every launch
+                ex = {f.name: step._field_layout(f, x.detach()) for f, x in zip(extras, xs)}
+                ctx.extras = ex
                 if not step._gpu:
+                    ex = {n: x.cpu().numpy() for n, x in ex.items()}
+                    ctx.extras = ex
                     step.set_pdfs(pdfs.detach().cpu().numpy())
-                    step.run(T, record=True)
+                    step.run(T, record=True, extra=ex)
                     ctx.records = step._records
                     step._records = None
                     return torch.from_numpy(step.pdf_array.copy())
@@ -460,7 +471,7 @@ class AutoDiffLatticeBoltzmannStep:
                     states = [x0]
                     for t in range(T):
                         out = step._alloc(zero=False)
-                        step._fwd(states[-1], out, {})
+                        step._fwd(states[-1], out, ex)
                         states.append(out)
                 # state 0 may be the caller's tensor: keep it through save_for_backward, so that an in-place
                 # change between forward and backward raises (version counter) instead of skewing the adjoint
@@ -471,12 +482,22 @@ class AutoDiffLatticeBoltzmannStep:
 
             @staticmethod
             def backward(ctx, grad):
+                ex = ctx.extras
+                ctx.extras = None
                 if not step._gpu:
                     step._records = ctx.records
                     step.set_adjoint_pdfs(grad.detach().cpu().numpy())
-                    step.run_backward(T)
+                    acc = {n: np.zeros_like(x) for n, x in ex.items()}
+                    for t in range(T):
+                        # each step's adjoint of the additional fields into a zeroed array, summed over the steps
+                        tmp = {adj[n]: np.zeros_like(x) for n, x in ex.items()}
+                        step.backward_time_step(step._records[-1 - t], ex, tmp)
+                        for n in acc:
+                            acc[n] += tmp[adj[n]]
+                    step._records = step._records[:len(step._records) - T]
                     ctx.records = None
-                    return torch.from_numpy(step.adjoint_pdf_array.copy())
+                    return (torch.from_numpy(step.adjoint_pdf_array.copy()),
+                            *[torch.from_numpy(acc[f.name]) for f in extras])
                 lattice = step._lattice is not None
                 g = grad if lattice and step._lattice_input_ok(grad) else step._as_layout(grad)
                 x0 = ctx.saved_tensors[0].detach() if ctx.input_is_state0 else None
@@ -496,15 +517,28 @@ class AutoDiffLatticeBoltzmannStep:
                     _lattice_sweeps(step, 'adj', launches)
                     return out
                 cur = g
+                acc = {n: torch.zeros_like(x) for n, x in ex.items()}
                 for t in reversed(range(T)):
                     nxt = step._alloc(zero=False)
-                    step._bwd(records[t], cur, nxt, {}, {})
+                    tmp = {adj[n]: torch.zeros_like(x) for n, x in ex.items()}
+                    step._bwd(records[t], cur, nxt, ex, tmp)
+                    for n in acc:
+                        acc[n] += tmp[adj[n]]
                     cur = nxt
-                return cur
+                return (cur, *[acc[f.name] for f in extras]) if extras else cur
 
         LbmTimesteps.num_time_steps = T
         LbmTimesteps.lb_step = self
         return LbmTimesteps
+
+    def _field_layout(self, f, t):
+        """An additional input tensor in field ``f``'s memory layout (fzyx: components-first) on the step's side."""
+        if not self._gpu:
+            return t
+        if f.index_dimensions and f.is_soa:
+            from ..zslab import ZSlabOp
+            return ZSlabOp._layout(f, t)
+        return t.contiguous()
 
     def _pdf_io_field(self):
         """The pdf field of the macroscopic ops, in the step's pdf layout (fzyx pdfs enter without a copy)."""
@@ -520,11 +554,19 @@ class AutoDiffLatticeBoltzmannStep:
         autograd records the chain). Returns ``SimulationResultsTensors``."""
         if str(backend).lower() not in ('torch_native', 'torch'):
             raise NotImplementedError(f"backend '{backend}': only the torch backends are built")
+        from ._method import force_is_field
+        given = {getattr(f, 'name', f): t for f, t in dict(additional_fields_to_tensor_map or {}).items()}
+        force = getattr(self._update_rule, 'force', None)
         if force_input_tensor is not None:
-            raise NotImplementedError('a per-cell force field is not built (constant body forces: the update '
-                                      "rule's force_model / force)")
-        if additional_fields_to_tensor_map:
-            raise NotImplementedError('additional fields of the update rule are not built')
+            if not force_is_field(force):
+                raise ValueError('force_input_tensor given, but the update rule has no force field')
+            (ff,) = {a.field for v in force for a in sp.sympify(v).atoms(ps.Field.Access)}
+            given[ff.name] = force_input_tensor
+        missing = [f.name for f in self._additional_fields if f.name not in given]
+        if missing:
+            raise ValueError(f'tensors for the update rule\'s additional input fields {missing} are needed '
+                             '(additional_fields_to_tensor_map / force_input_tensor)')
+        xs = [given[f.name] for f in self._additional_fields]
         setter = self._e2e_ops.get('setter') if hasattr(self, '_e2e_ops') else None
         if setter is None:
             self._e2e_ops = {'setter': self.create_macroscopic_setter_op(backend, **kernel_compilation_kwargs),
@@ -535,8 +577,8 @@ class AutoDiffLatticeBoltzmannStep:
         (input_pdf,) = ops['setter'].apply(density_input_tensor, velocity_input_tensor)
         out = input_pdf
         for _ in range(int(num_time_steps) // group):
-            out = step_op.apply(out)
-        rho, vel = ops['getter'].apply(out)
+            out = step_op.apply(out, *xs)
+        rho, vel = self._apply_getter(ops['getter'], out, given)
         return SimulationResultsTensors(input_pdf, out, rho, vel)
 
     def _macroscopic_fields(self):
@@ -544,9 +586,16 @@ class AutoDiffLatticeBoltzmannStep:
         D = len(self.domain_size)
         return ps.fields(f"rho, vel({D}): {np.dtype(dt).name}[{D}D]")
 
+    def _apply_getter(self, getter, pdfs, given):
+        """The getter on ``pdfs`` (and, with a per-cell Guo force, the force tensor: its inputs in the op's order)."""
+        names = [f.name for f in getter.autodiff_op.forward_input_fields]
+        pdf = self._pdf_io_field().name
+        return getter.apply(*[pdfs if n == pdf else given[n] for n in names])
+
     def create_macroscopic_getter_op(self, backend='torch_native', **kernel_compilation_kwargs):
         """ρ and u from pdfs as a differentiable op (``_autodiff_lbstep.py:249-280``): ``Op.apply(pdfs)`` →
-        ``(rho, vel)``."""
+        ``(rho, vel)`` (a per-cell Guo force: its field is an input too, in the op's ``forward_input_fields``
+        order)."""
         from ._method import macroscopic_getter
         rho, vel = self._macroscopic_fields()
         pdf = self._pdf_io_field()

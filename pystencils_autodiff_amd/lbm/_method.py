@@ -86,6 +86,21 @@ def _moments(stencil, f, compressible, shift=None):
 FORCE_MODELS = ('simple', 'guo')
 
 
+def force_components(force, D):
+    """The body force per axis as sympy expressions: numbers / symbols, or a force FIELD (a vector field of ``D``
+    components, or a sequence of accesses) — a per-cell force, an additional input of the update rule."""
+    if isinstance(force, ps.Field):
+        if force.index_dimensions != 1 or int(force.index_shape[0]) != D:
+            raise ValueError(f"force field '{force.name}' needs {D} components (one index dimension)")
+        return [force.center(a) for a in range(D)]
+    return [sp.sympify(v) for v in force]
+
+
+def force_is_field(force):
+    """Whether the (stored) force reads a field: a per-cell force."""
+    return force is not None and any(sp.sympify(v).atoms(ps.Field.Access) for v in force)
+
+
 def _force(force_model, force, stencil):
     """(velocity shift or None, per-direction force term builder) of a constant body force."""
     if force_model is None:
@@ -95,7 +110,7 @@ def _force(force_model, force, stencil):
     fm = str(force_model).lower()
     if fm not in FORCE_MODELS:
         raise NotImplementedError(f"force_model '{force_model}': one of {FORCE_MODELS}")
-    F = [sp.sympify(v) for v in force]
+    F = force_components(force, stencil.D)
     if len(F) != stencil.D:
         raise ValueError(f'force needs {stencil.D} components')
 
@@ -128,8 +143,9 @@ def create_lb_update_rule(stencil='D2Q9', relaxation_rate=None, compressible=Fal
     relaxation_rate=…, compressible=…, kernel_type='stream_pull_collide')`` [ext]). ``relaxation_rate`` =
     ω: a number, or a sympy symbol left as a kernel parameter (default: the symbol ``omega``). Fields:
     ``src(q)``/``dst(q)`` vector fields in ``layout`` (``'fzyx'``: components slowest, lbmpy's default)
-    unless given. ``force_model`` ('simple' or 'guo') with ``force``: a constant body force (numbers or symbols per
-    axis) — such rules run on the rule's own AutoDiffOp kernels, not the lattice schedule."""
+    unless given. ``force_model`` ('simple' or 'guo') with ``force``: a body force — constant (numbers or symbols per
+    axis) or per cell (a vector field of D components: an additional input of the rule, its adjoint accumulated over
+    the steps) — such rules run on the rule's own AutoDiffOp kernels, not the lattice schedule."""
     if kernel_type != 'stream_pull_collide':
         raise NotImplementedError("only kernel_type='stream_pull_collide' is restated")
     st = stencil if isinstance(stencil, LBStencil) else LBStencil(stencil)
@@ -147,7 +163,7 @@ def create_lb_update_rule(stencil='D2Q9', relaxation_rate=None, compressible=Fal
     ac.compressible = compressible
     ac.relaxation_rate = omega
     ac.force_model = None if force_model is None else str(force_model).lower()
-    ac.force = None if force is None else tuple(sp.sympify(v) for v in force)
+    ac.force = None if force is None else tuple(force_components(force, st.D))
     return ac
 
 

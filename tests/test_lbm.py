@@ -614,3 +614,88 @@ def test_lbm_force_models_gpu_vs_oracle(stencil, shape, compressible, model):
     step.run_backward(T)
     gg = step.adjoint_pdf_array.double().cpu().numpy()
     assert np.abs(gg - gref.numpy()).max() <= 1e-11 * np.abs(gref.numpy()).max()
+
+
+# a per-cell body force: a force FIELD (D components) in the update rule — an additional input of the step, its adjoint
+# summed over the steps (the reference's additional / time-constant fields, _autodiff_lbstep.py:113-128, :284-306)
+FIELD_FORCE_CASES = [('D2Q9', (9, 7), True, 'guo', 'numpy'), ('D2Q9', (8, 6), False, 'simple', 'fzyx'),
+                     ('D2Q9', (7, 9), False, 'guo', 'fzyx'), ('D3Q19', (5, 4, 6), True, 'guo', 'numpy')]
+
+
+def _force_field_case(stencil, shape, compressible, model, layout, target, T=3):
+    import torch
+    D = len(shape)
+    F = ps.fields(f"F({D}): float64[{D}D]", layout=layout)
+    rule = lbm.create_lb_update_rule(stencil, compressible=compressible, force_model=model, force=F)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.4, target=target)
+    assert [f.name for f in step._additional_fields] == ['F'] and step._lattice is None
+    op = step.create_timestep_op(T)
+    rng = np.random.default_rng(sum(shape))
+    f0 = _init(stencil, shape, compressible, seed=9)
+    Fv = 1e-3 * rng.standard_normal(shape + (D,))
+    dev = 'cuda' if target == 'gpu' else 'cpu'
+    x = torch.tensor(f0, device=dev, requires_grad=True)
+    Ft = torch.tensor(Fv, device=dev, requires_grad=True)
+    out = op.apply(x, Ft)
+    ft, Fr = torch.tensor(f0, requires_grad=True), torch.tensor(Fv, requires_grad=True)
+    ref = OL.run(ft, 1.4, T, stencil, compressible, xp=torch, force_model=model,
+                 force=tuple(Fr[..., a] for a in range(D)))
+    g = torch.tensor(rng.standard_normal(f0.shape))
+    out.backward(g.to(dev))
+    gx, gF = torch.autograd.grad(ref, (ft, Fr), g)
+    return out.detach().cpu(), ref.detach(), x.grad.cpu(), gx, Ft.grad.cpu(), gF
+
+
+@pytest.mark.parametrize('stencil,shape,compressible,model,layout', FIELD_FORCE_CASES)
+def test_lbm_force_field_cpu_vs_oracle(stencil, shape, compressible, model, layout):
+    """A per-cell force field through the timestep op on the C kernels: pdfs after T steps, the pdf adjoint and the
+    force adjoint (summed over the steps) vs the oracle's forced collision with per-cell forces and torch's reverse
+    mode (parity unpinned vs lbmpy, which is absent)."""
+    out, ref, gx, gxr, gF, gFr = _force_field_case(stencil, shape, compressible, model, layout, 'cpu')
+    assert float((out - ref).abs().max()) <= 1e-13 * float(ref.abs().max())
+    assert float((gx - gxr).abs().max()) <= 1e-12 * float(gxr.abs().max())
+    assert float((gF - gFr).abs().max()) <= 1e-12 * float(gFr.abs().max())
+
+
+def test_lbm_force_field_end_to_end_and_errors():
+    """create_end_to_end_op(force_input_tensor=…): setter → steps (force bound to every step) → getter (Guo's shifted
+    velocity reads the force too); dloss/dF against central finite differences; a rule with a force field needs
+    its tensor, a rule without one refuses it."""
+    import torch
+    F = ps.fields("F(2): float64[2D]")
+    rule = lbm.create_lb_update_rule('D2Q9', compressible=True, force_model='guo', force=F)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=(9, 7), relaxation_rate=1.4, target='cpu')
+    rng = np.random.default_rng(1)
+    rho = torch.tensor(1 + 0.01 * rng.standard_normal((9, 7)))
+    vel = torch.tensor(0.01 * rng.standard_normal((9, 7, 2)))
+    Ft = torch.tensor(1e-3 * rng.standard_normal((9, 7, 2)), requires_grad=True)
+
+    def loss(Fv):
+        r = step.create_end_to_end_op(4, vel, rho, force_input_tensor=Fv, num_times_steps_without_save=1)
+        return (r.output_velocity_tensor ** 2).sum() + r.output_density_tensor.sum()
+    loss(Ft).backward()
+    e = 1e-6
+    for idx in ((3, 2, 1), (0, 6, 0), (8, 0, 1)):
+        Fp, Fm = Ft.detach().clone(), Ft.detach().clone()
+        Fp[idx] += e
+        Fm[idx] -= e
+        fd = (float(loss(Fp)) - float(loss(Fm))) / (2 * e)
+        assert abs(fd - float(Ft.grad[idx])) <= 1e-6 * abs(fd) + 1e-9, (idx, fd, float(Ft.grad[idx]))
+    with pytest.raises(ValueError):
+        step.create_end_to_end_op(4, vel, rho)
+    plain = lbm.AutoDiffLatticeBoltzmannStep(lbm.create_lb_update_rule('D2Q9'), domain_size=(9, 7),
+                                             relaxation_rate=1.4, target='cpu')
+    with pytest.raises(ValueError):
+        plain.create_end_to_end_op(4, vel, rho, force_input_tensor=Ft)
+    with pytest.raises(ValueError):
+        lbm.create_lb_update_rule('D2Q9', force_model='guo', force=ps.fields("G(3): float64[2D]"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('stencil,shape,compressible,model,layout', FIELD_FORCE_CASES)
+def test_lbm_force_field_gpu_vs_oracle(stencil, shape, compressible, model, layout):
+    """The per-cell force field on the HIP kernels (the rule's AutoDiffOp kernels, transposed-mode adjoint)."""
+    out, ref, gx, gxr, gF, gFr = _force_field_case(stencil, shape, compressible, model, layout, 'gpu')
+    assert float((out.double() - ref).abs().max()) <= 1e-12 * float(ref.abs().max())
+    assert float((gx.double() - gxr).abs().max()) <= 1e-11 * float(gxr.abs().max())
+    assert float((gF.double() - gFr).abs().max()) <= 1e-11 * float(gFr.abs().max())
