@@ -168,8 +168,12 @@ class AutoDiffLatticeBoltzmannStep:
         self._omega_of = (lambda: float(self.kernel_params[rr.name])) if isinstance(rr, sp.Symbol) else \
             ((lambda v=rr: float(v)) if rr is not None else None)
         # (PSAD_LBM_LATTICE=0: the AutoDiffOp kernels instead — tests of that path, A/B probes)
+        force = getattr(update_rule, 'force', None)
+        self._lattice_force = (getattr(update_rule, 'force_model', None),
+                               None if force is None else tuple(float(v) for v in force)) \
+            if force is None or all(sp.sympify(v).is_number for v in force) else None
         self._lattice = {} if (getattr(update_rule, 'stencil', None) is not None and not time_constant_fields
-                               and getattr(update_rule, 'force_model', None) is None
+                               and self._lattice_force is not None
                                and os.environ.get('PSAD_LBM_LATTICE', '1') != '0'
                                and not self._additional_fields and self._omega_of is not None
                                and np.dtype(src.dtype.numpy_dtype) in (np.float32, np.float64)) else None
@@ -352,7 +356,7 @@ class AutoDiffLatticeBoltzmannStep:
         if k is None:
             k = self._lattice[(walls, links)] = LatticeKernels(
                 self.method, getattr(self._update_rule, 'compressible', False), self.pdf_field.dtype.numpy_dtype,
-                walls, self._target, links)
+                walls, self._target, links, *self._lattice_force)
         return k
 
     # -- kernels -----------------------------------------------------------------------------------

@@ -44,7 +44,7 @@ def _c(v):
 SELF_BIT = 30      # bit of a cell's neighbour mask: the cell itself is an obstacle (bits 0..Q-1: x − c_i is one)
 
 
-def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=None):
+def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=None, force_model=None, force=None):
     """Source of the forward (``lbm_fwd``) and adjoint (``lbm_adj``) kernels.
 
     ``addr='buf'`` (HIP): every pdf array is one buffer resource (its bytes below 2³²); a component's plane
@@ -54,10 +54,18 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     mask per cell (bit i: ``x − c_i`` is an obstacle; bit ``SELF_BIT``: ``x`` is one), one load per cell.
     ``links``: None (every wall a plain bounce-back), or per wall id (the flag array's values) the boundary's link
     coefficients per direction (``boundaries.link_coefficients``): a bounced component then becomes
-    ``α·src_ī(x) + β`` (id of the wall cell ``x − c_i`` from the flag array) and its adjoint is scaled by γ."""
+    ``α·src_ī(x) + β`` (id of the wall cell ``x − c_i`` from the flag array) and its adjoint is scaled by γ.
+    ``force_model`` 'simple' / 'guo' with a constant body force ``force`` (D numbers, ``_method._force``): 'simple'
+    adds the constant 3 w_i (c_i·F) to every fluid cell's post-collision value (its adjoint is unchanged); 'guo'
+    shifts the velocity by F/2 (/ρ) and adds w_i (1 − ω/2)(3 (c_i − u)·F + 9 (c_i·u)(c_i·F)), whose derivative through
+    u joins the adjoint's velocity sensitivities: B_a += C_a / ω with
+    C_a = (1 − ω/2) Σ_i g_i w_i (9 c_ia (c_i·F) − 3 F_a)."""
     D, Q = stencil.D, stencil.Q
     dirs = [tuple(d) for d in stencil.directions]
     w = [float(x) for x in stencil.weights]
+    fm = None if force_model is None else str(force_model).lower()
+    F = [float(v) for v in force] if fm else None
+    cF = [sum(c * f for c, f in zip(d, F)) for d in dirs] if fm else None
     inv = [stencil.inverse_direction_index(i) for i in range(Q)]
     axes = ['z', 'y', 'x'][3 - D:]          # spatial axes, axis 0 slowest; x fastest
     ct = ctype
@@ -183,8 +191,12 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         if compressible:
             L.append(f'  const {ct} irho = ({ct})1 / rho;')
         for a in range(D):
-            L.append(f'  const {ct} u{a} = m{a}' + (' * irho;' if compressible else ';'))
+            m = f'(m{a} + {c_(F[a] / 2)})' if fm == 'guo' else f'm{a}'      # Guo: velocity shifted by F/2
+            L.append(f'  const {ct} u{a} = {m}' + (' * irho;' if compressible else ';'))
         L.append(f'  const {ct} usq = ' + ' + '.join(f'u{a} * u{a}' for a in range(D)) + ';')
+        if fm == 'guo':
+            L.append(f'  const {ct} uF = ' + ' + '.join(f'u{a} * {c_(F[a])}' for a in range(D)) + ';')
+            L.append(f'  const {ct} kg = ({ct})1 - ({ct})0.5 * omega;')
 
     def cu_expr(i):
         t = [('+ ' if dirs[i][a] > 0 else '- ') + f'u{a}' for a in range(D) if dirs[i][a]]
@@ -229,7 +241,13 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         L.append(f'  {{ const {ct} cu = {cu_expr(i)};')
         L.append(f'    const {ct} poly = cu * (({ct})3 + ({ct})4.5 * cu) - ({ct})1.5 * usq;')
         feq = f'{c_(w[i])} * rho * (({ct})1 + poly)' if compressible else f'{c_(w[i])} * (rho + poly)'
-        L.append('    ' + store('d', 'dst', i, dcoff, f'f{i} + omega * ({feq} - f{i})') + ' }')
+        term = ''
+        if fm == 'simple' and cF[i]:
+            term = f' + {c_(3 * w[i] * cF[i])}'
+        elif fm == 'guo':
+            term = (f' + {c_(w[i])} * kg * (({ct})3 * ({c_(cF[i])} - uF)'
+                    + (f' + {c_(9 * cF[i])} * cu' if cF[i] else '') + ')')
+        L.append('    ' + store('d', 'dst', i, dcoff, f'f{i} + omega * ({feq} - f{i}){term}') + ' }')
     L.append('}')
 
     # ---- adjoint (scatter to where the forward pulled from)
@@ -258,6 +276,8 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     L.append(f'  {ct} S = 0, A = 0;')
     for a in range(D):
         L.append(f'  {ct} B{a} = 0;')
+        if fm == 'guo':
+            L.append(f'  {ct} E{a} = 0;')           # Σ_i g_i w_i c_ia (c_i·F)
     for i in range(Q):
         L.append(f'  {{ const {ct} cu = {cu_expr(i)};')
         L.append(f'    const {ct} gw = g{i} * {c_(w[i])};')
@@ -269,6 +289,11 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             for a in range(D):
                 if dirs[i][a]:
                     L.append(f'    B{a} {"+" if dirs[i][a] > 0 else "-"}= t;')
+            if fm == 'guo' and cF[i]:
+                L.append(f'    const {ct} tf = gw * {c_(cF[i])};')
+                for a in range(D):
+                    if dirs[i][a]:
+                        L.append(f'    E{a} {"+" if dirs[i][a] > 0 else "-"}= tf;')
         L.append('  }')
     if not compressible:
         L.append('  A = S;')
@@ -276,6 +301,9 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         L.append(f'  B{a} -= ({ct})3 * u{a} * S;')
         if compressible:
             L.append(f'  B{a} *= rho;')
+        if fm == 'guo':
+            # the force term's derivative through u, scaled into B (v = … + ω (A + Σ B_a ∂u_a/∂f_j))
+            L.append(f'  B{a} += kg * (({ct})9 * E{a} - ({ct})3 * {c_(F[a])} * S) / omega;')
     if compressible:
         L.append(f'  const {ct} Bu = ' + ' + '.join(f'B{a} * u{a}' for a in range(D)) + ';')
     for j in range(Q):
@@ -390,8 +418,10 @@ class LatticeKernels:
     cells' wall ids (the ``uint8`` flag array, C order) when ``links`` is given (walls other than plain
     bounce-back)."""
 
-    def __init__(self, stencil, compressible, dtype, walls, target, links=None):
+    def __init__(self, stencil, compressible, dtype, walls, target, links=None, force_model=None, force=None):
         self.stencil = stencil
+        self.force_model = force_model
+        self.force = None if force_model is None else tuple(float(v) for v in force)
         self.compressible = bool(compressible)
         self.dtype = np.dtype(dtype)
         if self.dtype not in (np.float32, np.float64):
@@ -405,8 +435,10 @@ class LatticeKernels:
 
     def source(self, idx='int', addr='buf'):
         if self.target != 'gpu':
-            return _emit(self.stencil, self.compressible, self.ct, self.walls, 'c', 'i64', 'ptr', self.links)
-        return _emit(self.stencil, self.compressible, self.ct, self.walls, 'hip', idx, addr, self.links)
+            return _emit(self.stencil, self.compressible, self.ct, self.walls, 'c', 'i64', 'ptr', self.links,
+                         self.force_model, self.force)
+        return _emit(self.stencil, self.compressible, self.ct, self.walls, 'hip', idx, addr, self.links,
+                     self.force_model, self.force)
 
     # -- GPU ---------------------------------------------------------------------------------------
     def _gpu_fn(self, which, idx, addr, device):

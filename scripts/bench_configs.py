@@ -180,7 +180,7 @@ def run_slab(name, builder, shape, dtype, full_cells, steps=20, warmup=3):
     sys.stdout.flush()
 
 
-def run_lbm(name, stencil, shape, dtype, T=10, reps=5, compressible=False, walls=False):
+def run_lbm(name, stencil, shape, dtype, T=10, reps=5, compressible=False, walls=False, force_model=None):
     """Lattice Boltzmann time-step op (lbm.AutoDiffLatticeBoltzmannStep.create_timestep_op): T forward steps
     and the T adjoint steps, HIP events around Op.apply and backward (back-to-back applies). MLUPS = cells · T / time; algorithmic
     bytes per cell and step: forward 2q·s (read src, write dst), adjoint 3q·s (read diffdst and the recorded
@@ -188,7 +188,9 @@ def run_lbm(name, stencil, shape, dtype, T=10, reps=5, compressible=False, walls
     import torch
 
     from pystencils_autodiff_amd import lbm
-    rule = lbm.create_lb_update_rule(stencil, compressible=compressible, data_type=str(dtype).replace('torch.', ''))
+    D = len(shape)
+    rule = lbm.create_lb_update_rule(stencil, compressible=compressible, data_type=str(dtype).replace('torch.', ''),
+                                     force_model=force_model, force=(1e-5, -2e-5, 5e-6)[:D] if force_model else None)
     step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.5, target='gpu')
     if walls:
         # a channel: no-slip walls on the first and last rows of axis 1

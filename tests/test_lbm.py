@@ -548,21 +548,33 @@ FORCE_CASES = [('D2Q9', (10, 7), False, 'guo'), ('D2Q9', (9, 12), True, 'guo'), 
                ('D3Q19', (6, 5, 4), False, 'guo')]
 
 
-def _forced(stencil, shape, compressible, model, target, dtype='float64'):
+def _forced(stencil, shape, compressible, model, target, dtype='float64', schedule='lattice'):
+    """A constant body force: the lattice kernels (force terms compiled in) or, with PSAD_LBM_LATTICE=0, the rule's
+    own AutoDiffOp kernels (Guo: the transposed derivation)."""
+    import os
     force = (1e-3, -2e-3, 5e-4)[:len(shape)]
     rule = lbm.create_lb_update_rule(stencil, compressible=compressible, force_model=model, force=force,
                                      data_type=dtype)
-    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.4, target=target)
-    assert step._lattice is None                     # forced rules: the rule's own AutoDiffOp kernels
+    old = os.environ.get('PSAD_LBM_LATTICE')
+    os.environ['PSAD_LBM_LATTICE'] = '1' if schedule == 'lattice' else '0'
+    try:
+        step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.4, target=target)
+    finally:
+        if old is None:
+            os.environ.pop('PSAD_LBM_LATTICE')
+        else:
+            os.environ['PSAD_LBM_LATTICE'] = old
+    assert (step._lattice is not None) == (schedule == 'lattice')
     return step, force
 
 
+@pytest.mark.parametrize('schedule', ['lattice', 'autodiffop'])
 @pytest.mark.parametrize('stencil,shape,compressible,model', FORCE_CASES)
-def test_lbm_force_models_cpu_vs_oracle(stencil, shape, compressible, model):
+def test_lbm_force_models_cpu_vs_oracle(stencil, shape, compressible, model, schedule):
     """A constant body force (lbmpy's 'simple' / 'guo' force models restated; parity unpinned vs lbmpy): T steps
     and the adjoint of T steps on the C kernels vs the oracle's forced collision and torch's reverse mode."""
     import torch
-    step, force = _forced(stencil, shape, compressible, model, 'cpu')
+    step, force = _forced(stencil, shape, compressible, model, 'cpu', schedule=schedule)
     f0 = _init(stencil, shape, compressible, seed=5)
     T = 3
     step.set_pdfs(f0)
@@ -595,11 +607,13 @@ def test_lbm_force_model_getter_shift():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('schedule', ['lattice', 'autodiffop'])
 @pytest.mark.parametrize('stencil,shape,compressible,model', FORCE_CASES)
-def test_lbm_force_models_gpu_vs_oracle(stencil, shape, compressible, model):
-    """The forced rules on the HIP kernels (the rule's AutoDiffOp kernels, transposed-mode adjoint)."""
+def test_lbm_force_models_gpu_vs_oracle(stencil, shape, compressible, model, schedule):
+    """The forced rules on the HIP kernels: the lattice kernels with the force terms compiled in, and the rule's
+    AutoDiffOp kernels (transposed-mode adjoint)."""
     import torch
-    step, force = _forced(stencil, shape, compressible, model, 'gpu')
+    step, force = _forced(stencil, shape, compressible, model, 'gpu', schedule=schedule)
     f0 = _init(stencil, shape, compressible, seed=5)
     T = 3
     step.set_pdfs(torch.tensor(f0, device='cuda'))
