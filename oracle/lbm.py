@@ -127,18 +127,19 @@ def stream_walls(f, stencil, wall, xp):
     return xp.stack(comps, -1) if xp.__name__ != 'torch' else xp.stack(comps, dim=-1)
 
 
-def step_walls(f, omega, wall, stencil='D2Q9', compressible=False, xp=None):
-    """One stream-pull-collide step with no-slip obstacles; obstacle cells keep their state."""
+def step_walls(f, omega, wall, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None):
+    """One stream-pull-collide step with no-slip obstacles (and optionally a body force on the fluid cells, as
+    ``collide``); obstacle cells keep their state."""
     if xp is None:
         import numpy as xp
-    new = collide(stream_walls(f, stencil, wall, xp), omega, stencil, compressible, xp)
+    new = collide(stream_walls(f, stencil, wall, xp), omega, stencil, compressible, xp, force_model, force)
     keep = wall[..., None] if xp.__name__ != 'torch' else wall.unsqueeze(-1)
     return xp.where(keep, f, new)
 
 
-def run_walls(f, omega, wall, steps, stencil='D2Q9', compressible=False, xp=None):
+def run_walls(f, omega, wall, steps, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None):
     for _ in range(steps):
-        f = step_walls(f, omega, wall, stencil, compressible, xp)
+        f = step_walls(f, omega, wall, stencil, compressible, xp, force_model, force)
     return f
 
 

@@ -713,3 +713,51 @@ def test_lbm_force_field_gpu_vs_oracle(stencil, shape, compressible, model, layo
     assert float((out.double() - ref).abs().max()) <= 1e-12 * float(ref.abs().max())
     assert float((gx.double() - gxr).abs().max()) <= 1e-11 * float(gxr.abs().max())
     assert float((gF.double() - gFr).abs().max()) <= 1e-11 * float(gFr.abs().max())
+
+
+@pytest.mark.parametrize('target', ['cpu', pytest.param('gpu', marks=pytest.mark.gpu)])
+@pytest.mark.parametrize('model,compressible', [('guo', True), ('simple', False)])
+def test_lbm_force_driven_channel(target, model, compressible):
+    """A body force along a no-slip channel on the lattice kernels (walls and force terms in one kernel): T steps and
+    the adjoint vs the oracle's wall step with the forced collision; after many steps the profile across the channel
+    is Poiseuille's parabola (Guo: the velocity with the F/2 shift against F (y − y0)(y1 − y) / (2ν) within a few %).
+    """
+    import torch
+    shape, T = (12, 9), 4
+    F = (0.0, 1e-5)                                   # along axis 1 (the channel's walls are the first / last axis-0 rows)
+    rule = lbm.create_lb_update_rule('D2Q9', compressible=compressible, force_model=model, force=F)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.2, target=target)
+    step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[0, :])
+    step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[-1, :])
+    assert step._lattice is not None
+    wall = np.zeros(shape, bool)
+    wall[0, :] = wall[-1, :] = True
+    f0 = _init('D2Q9', shape, compressible, seed=13)
+    dev = 'cuda' if target == 'gpu' else 'cpu'
+    step.set_pdfs(torch.tensor(f0, device=dev) if target == 'gpu' else f0)
+    step.run(T, record=True)
+    ft = torch.tensor(f0, requires_grad=True)
+    ref = OL.run_walls(ft, 1.2, torch.tensor(wall), T, 'D2Q9', compressible, xp=torch, force_model=model, force=F)
+    got = step.pdf_array.double().cpu().numpy() if target == 'gpu' else step.pdf_array
+    assert np.abs(got - ref.detach().numpy()).max() <= 1e-12 * np.abs(f0).max()
+    g = np.random.default_rng(14).standard_normal(f0.shape)
+    (gref,) = torch.autograd.grad(ref, ft, torch.tensor(g))
+    step.set_adjoint_pdfs(torch.tensor(g, device=dev) if target == 'gpu' else g)
+    step.run_backward(T)
+    ga = step.adjoint_pdf_array.double().cpu().numpy() if target == 'gpu' else step.adjoint_pdf_array
+    assert np.abs(ga - gref.numpy()).max() <= 1e-11 * np.abs(gref.numpy()).max()
+    if model == 'guo':
+        # steady state from rest: Poiseuille across axis 0 (walls half-way between rows 0/1 and 10/11)
+        rest = np.broadcast_to(np.asarray([float(w) for w in OL.SETS['D2Q9'][1]]), shape + (9,)).copy()
+        step.set_pdfs(torch.tensor(rest, device=dev) if target == 'gpu' else rest)
+        step.run(4000)
+        f = step.pdf_array.double().cpu().numpy() if target == 'gpu' else step.pdf_array
+        dirs = OL.SETS['D2Q9'][0]
+        rho = f.sum(-1)
+        u1 = (sum(c[1] * f[..., i] for i, c in enumerate(dirs)) + F[1] / 2) / rho
+        nu = (1 / 1.2 - 0.5) / 3
+        y = np.arange(shape[0]) - 0.5                 # distance from the lower wall (half-way bounce-back)
+        H = shape[0] - 2
+        prof = F[1] * y * (H - y) / (2 * nu)
+        inner = slice(1, shape[0] - 1)
+        assert np.abs(u1[inner].mean(1) - prof[inner]).max() <= 0.03 * prof[inner].max()
