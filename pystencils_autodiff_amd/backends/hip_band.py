@@ -634,6 +634,9 @@ def emit_band(ir, name, cfg):
             B.append(f'{ind}    }}')
             B.append(f'{ind}  }}')
         B.append(f'{ind}}}')
+        if cfg.BNT != 2:
+            # store cache policy probe (2 = non-temporal, the default)
+            B = [ln.replace(', 0, 2);', f', 0, {cfg.BNT});') if 'raw_buffer_store' in ln else ln for ln in B]
         return B
 
     def step(k, ind, part='full', guard='jj < nplanes', store='jj >= 2'):
