@@ -131,7 +131,10 @@ def test_band_sources_compile():
                   MarchConfig(**{**cfg.__dict__, 'BMASK': True, 'XB': True}),
                   MarchConfig(**{**cfg.__dict__, 'BTRIM': 1}), MarchConfig(**{**cfg.__dict__, 'BTRIM': 2}),
                   MarchConfig(**{**cfg.__dict__, 'BTRIM': 3, 'ZMIN': 16, 'ZMAX': 16}),
-                  MarchConfig(**{**cfg.__dict__, 'BPAD': 1}), MarchConfig(**{**cfg.__dict__, 'BPAD': 1, 'BMASK': True})):
+                  MarchConfig(**{**cfg.__dict__, 'BPAD': 1}), MarchConfig(**{**cfg.__dict__, 'BPAD': 1, 'BMASK': True}),
+                  # round 3's branched masked stores, the store cache-policy probe
+                  MarchConfig(**{**cfg.__dict__, 'BMASK': True, 'BXW': True, 'BMBR': 1}),
+                  MarchConfig(**{**cfg.__dict__, 'BMASK': True, 'BXW': True, 'BNT': 0})):
             src, kname = hk.source(('march', c))
             assert kname.endswith('_band') and 'band schedule' in src
             assert len(rt.compile_hip(src)) > 0
@@ -231,12 +234,13 @@ def test_band_unaligned_vs_oracle(case_shape, bh):
 @pytest.mark.gpu
 @pytest.mark.parametrize('case_shape', UNALIGNED, ids=lambda c: f'{c[0]}-{c[1][2]}')
 @pytest.mark.parametrize('bh', ['zeros', None])
-@pytest.mark.parametrize('knob', [{'BZF': 0}, {'BREG': 1}], ids=['BZF0', 'BREG1'])
+@pytest.mark.parametrize('knob', [{'BZF': 0}, {'BREG': 1}, {'BMBR': 1}], ids=['BZF0', 'BREG1', 'BMBR1'])
 def test_band_unaligned_variants_vs_oracle(case_shape, bh, knob):
     """Unaligned rows, forward and adjoint vs the oracle: ``BZF=0`` (no loader zero fill past each row end; the
     compute lanes of a row's last chunk zero its first element past X in registers) and ``BREG=1`` (a padded image
     filled through registers: row pieces read at the dword at or below them, realigned by v_alignbyte, cells past X
-    zeroed, written with ds_write_b128)."""
+    zeroed, written with ds_write_b128) and ``BMBR=1`` (round 3's masked stores behind per-row branches instead of
+    range-check drops)."""
     name, shape = case_shape
     _band_vs_oracle(next(c for c in CASES if c[0] == name), shape, bh, **knob)
 
