@@ -108,6 +108,9 @@ def _band_config(ir, ve, shape, over):
         # band instead of 10/8; 72 KB LDS): 27-point 1024³ fwd+bwd 1.712-1.719 vs 1.764-1.766 ms with 8-row bands
         # (profiles/r03_op_band_ab5.log, _ab6.log); the 7-point star stencil loses (1.65 vs 1.42), 768-wide rows too
         TY, D = 16, 1
+        rule16 = True
+    else:
+        rule16 = False
     if 'BAND' in over:
         R = int(over['BAND'])
     TY = int(over.get('BTY', TY if TY % R == 0 else R * max(1, TY // R)))
@@ -125,8 +128,8 @@ def _band_config(ir, ve, shape, over):
         long_ok = X <= BAND_STAR_LONG_MAX_X and nty * -(-Z // BAND_ZC_STAR_LONG) >= BAND_STAR_LONG_MIN_WG
         zc = BAND_ZC_STAR_LONG if long_ok else BAND_ZC_STAR
         min_wg = BAND_STAR_LONG_MIN_WG if long_ok else BAND_MIN_WG
-    elif TY == 16 and not idle_pick:
-        zc = BAND_ZC_BOX16
+    elif TY == 16 and rule16:
+        zc = BAND_ZC_BOX16              # (16-row bands of other rows — 2 rows per lane, idle lanes — take the ladder)
     else:
         zc = next((c for c in BAND_ZC_BOX_LADDER if nty * -(-Z // c) >= BAND_ROUND_WG), BAND_ZC_BOX_LADDER[-1])
     zc = int(over.get('ZMIN', zc))

@@ -120,6 +120,19 @@ def test_band_default_selection_idle_lanes(builder, ve, shape, expect):
     assert -(-shape[1] // cfg.BTY) * -(-shape[0] // cfg.ZMIN) >= 512, cfg
 
 
+@pytest.mark.parametrize('builder,shape,expect', [
+    (W.stencil_27pt, (512, 512, 576), (16, 2, 2, 16)), (W.stencil_27pt, (512, 512, 640), (16, 2, 2, 16)),
+    (W.stencil_27pt, (512, 512, 320), (16, 2, 2, 16)), (W.stencil_27pt, (512, 512, 896), (8, 2, 3, 32)),
+    (W.stencil_27pt, (1024, 1024, 1024), (16, 4, 1, 32)),
+    (lambda: W.diffusion_7pt(dtype='float16'), (512, 512, 640), (16, 2, 2, 8))])
+def test_band_default_selection_16_row_bands(builder, shape, expect):
+    """fp16 rows whose whole-wave choices are 16-row bands of 2 rows per lane (ahead of 3 planes in flight), with
+    ladder chunks — the 32-plane chunks stay with the 1024-wide box rule (16 rows, 4 per lane, one plane in flight)."""
+    op = pa.AutoDiffOp(builder(), boundary_handling='zeros')
+    cfg = default_march_config(HipStencilKernel(_kernel(op.forward_assignments)).ir, 8, shape)
+    assert (cfg.BTY, cfg.BAND, cfg.D, cfg.ZMIN) == expect, cfg
+
+
 def test_band_sources_compile():
     from pystencils_autodiff_amd.backends import hip_runtime as rt
     from pystencils_autodiff_amd.backends.hip_emitter import MarchConfig
