@@ -27,7 +27,7 @@ extern "C" {
 
 #define PSAD_HIPRTC_ERROR_BASE 10000
 
-/* ABI version of this header; bumped on any signature change. */
+/* ABI version of this header; bumped on any signature change (3: psad_source_hash added). */
 int psad_abi_version(void);
 
 /* The sources the library was built from: 16 hex digits of sha256 over csrc/psad_hip.cpp, csrc/psad_halo.cpp and

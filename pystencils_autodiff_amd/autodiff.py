@@ -457,6 +457,15 @@ class AutoDiffOp:
                       for g in ghost_layers]
             if len(gl) != ndim:
                 raise ValueError(f'ghost_layers {ghost_layers}: one entry per spatial axis ({ndim})')
+            if len(set(gl)) == 1 and gl[0][0] == gl[0][1]:
+                # the same k layers on every side, at least the stencil's own (pystencils' required ghost layers):
+                # the interior-only kernel of boundary_handling=None with k layers — the tuned schedules, not the
+                # one-thread-per-cell slice kernel (ghost_layers=1 on a radius-1 stencil is the default's cells)
+                k = StencilKernel(ac, boundary_handling=None, function_name=f"{self.op_name}_{which}_{target}_custom",
+                                  target=target, data_type=data_type, **{**self._kwargs, **kwargs})
+                if gl[0][0] >= k.ir.ghost_layers:
+                    k.ir.ghost_layers = gl[0][0]
+                    return k.compile()
             iteration_slice = tuple(slice(lo, -hi if hi else None) for lo, hi in gl)
         bh = 'zeros' if ghost_layers == 0 else None
         return StencilKernel(ac, boundary_handling=bh, function_name=f"{self.op_name}_{which}_{target}_custom",

@@ -215,7 +215,10 @@ def native_module():
                 # no GPU here: nothing launches, ops are only built (hiprtc) — the Python Function will do
                 _psad_torch = False
             if _psad_torch:
-                from .hip_runtime import _check_stamp
+                from .hip_runtime import HipError, _check_stamp
+                if not hasattr(_psad_torch, 'source_hash'):
+                    raise HipError(f'{_psad_torch.__file__} predates the source stamp (a stale build): rebuild with '
+                                   '`python -m pystencils_autodiff_amd.build`')
                 _check_stamp(_psad_torch.source_hash(), 'torch', _psad_torch.__file__)
             _native = _psad_torch
     return _native or None

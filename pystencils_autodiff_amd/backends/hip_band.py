@@ -134,6 +134,52 @@ def band_choice(X, nstore=1, es=2, pad=0, reg=0, idle=False):
     return None
 
 
+def band_dpp_edges_ok(CPR):
+    """Edge dwords by DPP ``row_shr/row_shl:1`` (``BPE=3``) need every row-group boundary (and the last task) on a
+    16-lane row boundary of the wave: rows of a multiple of 16 chunks."""
+    return CPR % 16 == 0
+
+
+def band_edge_table(g, R, es):
+    """Per compute task (``ctid``): the element offset from the lane's chunk of the one LDS dword it reads per image
+    row under ``BPE=3``. Lanes 0 / 15 of each 16-lane row (DPP ``row_shr:1`` / ``row_shl:1`` has no source for them)
+    read their true left / right dword (a zero pad at a row end); the other lanes read a dword chosen so that each
+    32-lane half's addresses spread over the 32 banks of ``ds_read_b32`` ((a/4) mod 32, MI355X_MICROARCH.md §LDS).
+    Banks are computed relative to the wave's slot row base, which every lane shares (row and slot offsets are
+    uniform), so the table holds for every image row and slot. Returns (offsets, worst bank multiplicity)."""
+    VE, CPR, XP, NCT, ntask = g['VE'], g['CPR'], g['XP'], g['NCT'], g['ntask']
+    dw = 4 // es                                    # elements per dword
+    c0 = VE                                         # padded image: a row's first element sits after its zero piece
+    offs, worst = [0] * NCT, 1
+    for w in range(NCT // 64):
+        for h in range(2):
+            lanes = range(64 * w + 32 * h, 64 * w + 32 * h + 32)
+            pos = {}
+            for t in lanes:
+                tt = min(t, ntask - 1)
+                grp, col = divmod(tt, CPR)
+                pos[t] = (grp * R * XP + c0 + col * VE) // dw        # the chunk's first dword
+            used = {}
+            for t in lanes:
+                L = t % 16
+                if L == 0:
+                    offs[t] = -dw
+                elif L == 15:
+                    offs[t] = VE
+                else:
+                    continue
+                b = (pos[t] + offs[t] // dw) % 32
+                used[b] = used.get(b, 0) + 1
+            for t in lanes:
+                if t % 16 in (0, 15):
+                    continue
+                b = min(range(32), key=lambda k: (used.get(k, 0), k))
+                used[b] = used.get(b, 0) + 1
+                offs[t] = ((b - pos[t]) % 32) * dw
+            worst = max(worst, max(used.values()))
+    return offs, worst
+
+
 def emit_band(ir, name, cfg):
     """HIP source of the band kernel (signature identical to the march / zsum kernels: fields, 2 halo pointers
     per stencil field, Z Y X zlo zhi ylo yhi xlo xhi zc zstep ntx nty, scalars)."""
@@ -162,6 +208,7 @@ def emit_band(ir, name, cfg):
     bo = not breg and (X * es) % 4 != 0             # rows on half dwords (fp16, X odd): realigned in registers
     assert not partial or cfg.BMASK, 'rows of a partial last chunk need the masked stores'
     czf = bu and not cfg.BZF                        # BZF=0: the first element past a row zeroed in registers
+    dpp_edges = padded and not breg and cfg.BPE == 3 and band_dpp_edges_ok(CPR)
     pr = KernelExprPrinter('float', dict(ir.symbol_names))
     W = []
     for pl in plans:
@@ -193,6 +240,11 @@ def emit_band(ir, name, cfg):
     L.append(f'// band schedule: {TY}-row bands of full {X}-element rows, {R} rows x {VE} cells per lane, {NCT // 64} '
              f'compute waves + LDS-DMA loader wave, {NS}-slot {et} plane ring ({D} planes in flight), z partial sums '
              f'in 3 rotating register sets, LDS {g["lds_bytes"]} B')
+    if dpp_edges:
+        etab, eworst = band_edge_table(g, R, es)
+        L.append(f'// x-edge dwords: DPP row_shr/row_shl:1, one ds_read_b32 per row for the 16-lane rows\' end lanes '
+                 f'(worst bank multiplicity {eworst})')
+        L.append(f'__constant__ short {name}_eoff[{NCT}] = {{{", ".join(str(v) for v in etab)}}};')
     wpe = f' __attribute__((amdgpu_waves_per_eu({int(cfg.BWPE)}, {int(cfg.BWPE)})))' if cfg.BWPE else ''
     L.append(f'extern "C" __global__ void __launch_bounds__({NT}){wpe} {name}({", ".join(params)})\n{{')
     L.append(f'  __shared__ __attribute__((aligned(1024))) {et} lds[{NS * SLOT + 64}];')
@@ -220,6 +272,8 @@ def emit_band(ir, name, cfg):
     else:
         L.append(f'  const int ldw = {NCT // 64};')
     L.append('  if (wave == ldw) {')
+    if cfg.BPRIO:
+        L.append(f'    __builtin_amdgcn_s_setprio({int(cfg.BPRIO)});')
     if not breg:
         L.append(f'    int vo[{NI}];')
         if bo:
@@ -419,7 +473,9 @@ def emit_band(ir, name, cfg):
     L.append("  // column 0 (x boundary, masked) reads its own first dword instead of the one before the slot.")
     dw = 4 // es                                          # elements per dword
     # dword targets relative to the wave's block (64 chunks of 4 dwords): -1, 0 .. 30 | 33 .. 63, 256
-    if padded:
+    if dpp_edges:
+        L.append(f'  const int eoff = {name}_eoff[ctid < {NCT} ? ctid : 0];')
+    elif padded:
         pass                                              # x neighbours read from the image (zero pads at row ends)
     elif cfg.BEDGE:
         L.append(f'  const int eoff = {dw} * (lane == 0 ? (col == 0 ? 0 : -1) : (lane == 63 ? 256 : (lane < 32 ? lane - 1 '
@@ -460,19 +516,30 @@ def emit_band(ir, name, cfg):
                   f'{ind}    const f32x2 P3 = {{(float)w1[1], (float)w3[1]}}, P4 = {{(float)w2[0], (float)w4[0]}}, '
                   'P5 = {(float)w2[1], (float)rr};']
             return B
-        if padded:
+        if dpp_edges:
+            # the dwords left and right of the lane's chunk from the neighbour lanes (DPP within 16-lane rows); the rows'
+            # end lanes take the one LDS dword they read (their true edge, a zero pad at a row end), the other lanes'
+            # reads are spread over the banks (band_edge_table)
+            vt = 'f16x8' if half else 'f32x4'
+            B += [f'{ind}    const {vt} v = *(const {vt}*)rp;',
+                  f'{ind}    const unsigned e = *(const unsigned*)(rp + eoff);',
+                  f'{ind}    const u32x4 d = __builtin_bit_cast(u32x4, v);',
+                  f'{ind}    const unsigned el = __builtin_amdgcn_update_dpp(e, d.w, 0x111, 0xf, 0xf, false);   // row_shr:1',
+                  f'{ind}    const unsigned er = __builtin_amdgcn_update_dpp(e, d.x, 0x101, 0xf, 0xf, false);   // row_shl:1']
+        elif padded:
             # the dwords left and right of the lane's chunk straight from the image (a row's end chunks meet the zero
             # pads): no DPP, no boundary selects (one ds_read2_b32 per row)
             B += [f'{ind}    const unsigned el = *(const unsigned*)(rp - {dw}), er = *(const unsigned*)(rp + {VE});']
+        if padded:
             if half:
-                B += [f'{ind}    const f16x8 v = *(const f16x8*)rp;',
+                B += [f'{ind}    const f16x8 v = *(const f16x8*)rp;'] * (not dpp_edges) + [
                       f'{ind}    const _Float16 l = __builtin_bit_cast(f16x2, el)[1], rr = __builtin_bit_cast(f16x2, er)[0];',
                       f'{ind}    const f32x2 P0 = {{(float)l, (float)v[3]}}, P1 = {{(float)v[0], (float)v[4]}}, '
                       'P2 = {(float)v[1], (float)v[5]};',
                       f'{ind}    const f32x2 P3 = {{(float)v[2], (float)v[6]}}, P4 = {{(float)v[3], (float)v[7]}}, '
                       'P5 = {(float)v[4], (float)rr};']
             else:
-                B += [f'{ind}    const f32x4 v = *(const f32x4*)rp;',
+                B += [f'{ind}    const f32x4 v = *(const f32x4*)rp;'] * (not dpp_edges) + [
                       f'{ind}    const float H0 = __builtin_bit_cast(float, el), H5 = __builtin_bit_cast(float, er);',
                       f'{ind}    const float H1 = v.x, H2 = v.y, H3 = v.z, H4 = v.w;']
             return B
@@ -523,12 +590,12 @@ def emit_band(ir, name, cfg):
                                 B.append(f'{ind}{acc} = {acc} + {term};')
         return B
 
-    def stores(ind, si, sp, fld):
+    def stores(ind, si, sp, fld, rows=None):
         B = [f'{ind}{{',
              f'{ind}  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc('
              f'(void*)(f_{fld.name} + (i64)(zb - 2 + jj) * YX), (short)0, (int)(YX * {es}), 0x00020000);']
         vt = 'f16x8' if half else 'f32x4'
-        for o in range(R):
+        for o in (range(R) if rows is None else rows):
             vals = ', '.join(cell(si, sp, o, q) for q in range(VE))
             st = f'__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ov), ors, sofs + {o * X * es}u, 0, 2);'
             if not cfg.BMASK:
@@ -668,6 +735,10 @@ def emit_band(ir, name, cfg):
                 for o in range(R):
                     B.append(f'{ind}  ' + ' '.join(f'{A(si, s_, o, a)} = {azero};' for a in range(4)))
         first = set()
+        # idle lanes (band tasks not a multiple of 64) compute on a clamped task with wrong x neighbours: no stores
+        act = 'active' if g['ntask'] != NCT else ''
+        cond = ' && '.join(c for c in (store, act) if c) if store is not None else None
+        interleave = cfg.BSI and store is not None
         for r in range(R + 2):
             B.append(f'{ind}  {{')
             B += row_prologue(ind, r)
@@ -675,6 +746,12 @@ def emit_band(ir, name, cfg):
             # FMAs between two dependent ones)
             B += taps(f'{ind}    ', r, sets, first)
             B.append(f'{ind}  }}')
+            if interleave and r >= 2:
+                # output row r-2 of plane q-1 took its last taps (input row r, dy = +1): store it now
+                B.append(f'{ind}  if ({cond}) {{' if cond else f'{ind}  {{')
+                for si, fld in enumerate(store_field):
+                    B += stores(f'{ind}    ', si, sp, fld, [r - 2])
+                B.append(f'{ind}  }}')
         # outputs of q+1 that received no tap this plane (no dz = -1 taps) start from zero
         if any(dz == -1 for _, dz in sets):
             for si in range(NP):
@@ -682,10 +759,7 @@ def emit_band(ir, name, cfg):
                     for a in range(4):
                         if (si, o, a) not in first:
                             B.append(f'{ind}  {A(si, sn, o, a)} = {azero};')
-        # idle lanes (band tasks not a multiple of 64) compute on a clamped task with wrong x neighbours: no stores
-        act = 'active' if g['ntask'] != NCT else ''
-        cond = ' && '.join(c for c in (store, act) if c)
-        if store is not None:
+        if store is not None and not interleave:
             B.append(f'{ind}  if ({cond}) {{' if cond else f'{ind}  {{')
             for si, fld in enumerate(store_field):
                 B += stores(f'{ind}    ', si, sp, fld)

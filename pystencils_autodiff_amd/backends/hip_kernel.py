@@ -69,7 +69,8 @@ BAND_F32_IDLE_MAX_X = 1024
 # describe a one-thread-per-cell launch these schedules do not have, so they are accepted and ignored. Upper-case
 # keys are this layer's tile parameters; an unknown one is a typo and raises.
 TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
-             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE', 'BLDR', 'BLAUX', 'BPAD', 'BZF', 'BREG', 'BMBR', 'BNT')
+             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE', 'BLDR', 'BLAUX', 'BPAD', 'BZF', 'BREG', 'BMBR', 'BNT', 'BPE', 'BSI',
+             'BPRIO')
 
 
 def _band_config(ir, ve, shape, over):
@@ -93,14 +94,17 @@ def _band_config(ir, ve, shape, over):
         return None
     # rows with no band height of whole compute waves: a band whose last compute wave holds idle lanes
     choice = whole or (band_choice(X, len(plans), es, idle=True) if plans else None)
-    idle_pick = whole is None
     if choice is None:
         return None
     TY, R, D = choice
-    g8 = band_geometry(X, 8, 4, 2, 4) if es == 4 else None
+    pad = int(over.get('BPAD', BAND_PAD_BOX if ntaps > 12 else 0))
+    reg = int(over.get('BREG', BAND_REG_STAR_ODD if ntaps <= 12 and es == 2 and X % 2 else 0))
+    # fp32 star stencils: 8-row bands of 4 rows per lane (see BAND_F32_STAR_MAX_X) — one output only (band_choice's
+    # rule: at most 2 rows per lane when a kernel stores two fields)
+    g8 = band_geometry(X, 8, 4, 2, 4, pad, reg) if es == 4 and len(plans) == 1 else None
     if g8 and ntaps <= 12 and 'BAND' not in over and g8['ntask'] % 64 == 0 and g8['NCT'] <= 960 and \
             2 * g8['NI'] <= 63 and g8['lds_bytes'] <= 160 * 1024:
-        TY, R, D = 8, 4, 2              # fp32 star stencils: 8-row bands (see BAND_F32_STAR_MAX_X)
+        TY, R, D = 8, 4, 2
     zc0 = int(over.get('ZMIN', BAND_ZC_BOX if ntaps > 12 else BAND_ZC_STAR))
     if ntaps > 12 and es == 2 and (X // 8) % 128 == 0 and R == 4 and \
             -(-int(shape[-2]) // 16) * -(-int(shape[0]) // zc0) >= BAND_MIN_WG:
@@ -115,8 +119,6 @@ def _band_config(ir, ve, shape, over):
         R = int(over['BAND'])
     TY = int(over.get('BTY', TY if TY % R == 0 else R * max(1, TY // R)))
     D = int(over.get('D', D))
-    pad = int(over.get('BPAD', BAND_PAD_BOX if ntaps > 12 else 0))
-    reg = int(over.get('BREG', BAND_REG_STAR_ODD if ntaps <= 12 and es == 2 and X % 2 else 0))
     g = band_geometry(X, TY, R, D, es, pad, reg)
     if TY % R or g['NCT'] > 960 or D * g['NI'] > 63 or g['lds_bytes'] > 160 * 1024:
         raise ValueError(f'band schedule: BTY={TY} BAND={R} D={D} do not fit rows of {X} elements')
@@ -146,7 +148,8 @@ def _band_config(ir, ve, shape, over):
                        BTRIM=btrim, BEDGE=int(over.get('BEDGE', 1)),
                        BSTAG=int(over.get('BSTAG', 0)), BWPE=int(over.get('BWPE', 0)), BLDR=int(over.get('BLDR', 0)),
                        BLAUX=int(over.get('BLAUX', 0)), BPAD=pad, BZF=int(over.get('BZF', 1)), BREG=reg,
-                       BMBR=int(over.get('BMBR', 0)), BNT=int(over.get('BNT', 2)))
+                       BMBR=int(over.get('BMBR', 0)), BNT=int(over.get('BNT', 2)), BPE=int(over.get('BPE', 0)),
+                       BSI=int(over.get('BSI', 0)), BPRIO=int(over.get('BPRIO', 0)))
 
 
 def default_march_config(ir, ve, shape=None, tuning=None, band=True):

@@ -102,8 +102,9 @@ def lib():
         L.psad_halo_exchange.restype = c_int
         L.psad_rccl_error_string.argtypes = [c_int]
         L.psad_rccl_error_string.restype = cp
-        if L.psad_abi_version() != 2:
-            raise HipError('libpsad_hip.so ABI mismatch: rebuild the extension')
+        if L.psad_abi_version() != 3:
+            raise HipError(f'{library_path}: ABI version {L.psad_abi_version()}, this tree needs 3 (a stale build): '
+                           'rebuild with `python -m pystencils_autodiff_amd.build`')
         L.psad_source_hash.restype = cp
         _check_stamp(L.psad_source_hash().decode(), 'lib', library_path)
         _lib = L

@@ -29,7 +29,7 @@ void copy_log(hiprtcProgram prog, char* log, size_t log_size) {
 
 extern "C" {
 
-int psad_abi_version(void) { return 2; }
+int psad_abi_version(void) { return 3; }   // 3: psad_source_hash
 
 #ifndef PSAD_SOURCE_HASH
 #define PSAD_SOURCE_HASH "0000000000000000"

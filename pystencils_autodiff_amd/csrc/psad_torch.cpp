@@ -188,8 +188,16 @@ struct Exchange {
     // one HSA signal per ordering (signal memory is allocated 8 bytes at a time)
     uint32_t* sig = nullptr;              // faces final (compute -> halo stream)
     uint32_t* sig_halo = nullptr;         // halos landed (halo -> compute)
+    // under g_sweep_mutex: the sweep counter, and the one compute stream whose sweeps order through the signals. A
+    // wait for "sig >= seq" is a point in THAT stream only while every write to sig comes from it, in counter order;
+    // a sweep enqueued on another compute stream (torch.cuda.stream(s2), a second Python thread) would let the halo
+    // stream pass early, so such sweeps take the event record + wait path instead
     mutable uint32_t seq = 0;
+    mutable hipStream_t sig_stream = nullptr;
 };
+
+std::mutex g_sweep_mutex;               // serialises the enqueue of exchanging sweeps (counter order = stream order)
+std::atomic<int64_t> g_event_sweeps{0};  // exchanging sweeps ordered by events (tests)
 
 struct Sweep {
     Exchange ex;
@@ -227,12 +235,20 @@ void run_sweep(const Sweep& w, const std::vector<at::Tensor>& table, const std::
     hipStream_t cur = c10::hip::getCurrentHIPStream(device).stream();
     const Exchange& ex = w.ex;
     const size_t n = ex.slot.size();
-    if (n && ex.sig) ++ex.seq;
-    if (n && ex.sig) {
-        hip_ok(hipStreamWriteValue32(cur, ex.sig, ex.seq, 0), "hipStreamWriteValue32");
-        hip_ok(hipStreamWaitValue32(ex.stream, ex.sig, ex.seq, hipStreamWaitValueGte, 0xffffffffu),
+    std::unique_lock<std::mutex> lock(g_sweep_mutex, std::defer_lock);
+    if (n) lock.lock();
+    const bool sig = n && ex.sig && (ex.sig_stream == nullptr || ex.sig_stream == cur);
+    uint32_t seq = 0;
+    if (sig) {
+        ex.sig_stream = cur;
+        seq = ++ex.seq;
+    }
+    if (sig) {
+        hip_ok(hipStreamWriteValue32(cur, ex.sig, seq, 0), "hipStreamWriteValue32");
+        hip_ok(hipStreamWaitValue32(ex.stream, ex.sig, seq, hipStreamWaitValueGte, 0xffffffffu),
                "hipStreamWaitValue32");
     } else if (n) {
+        g_event_sweeps.fetch_add(1);
         hip_ok(hipEventRecord(ex.ev_faces, cur), "hipEventRecord");           // the faces are final
         hip_ok(hipStreamWaitEvent(ex.stream, ex.ev_faces, 0), "hipStreamWaitEvent");
     }
@@ -253,9 +269,9 @@ void run_sweep(const Sweep& w, const std::vector<at::Tensor>& table, const std::
     if (n && w.faces_on_halo)                                                // faces beside the interior
         for (const auto& f : w.faces) launch_on(f, table, scalars, ex.stream);
     if (w.has_inner) launch(w.inner, table, scalars, device);                // interior overlaps the exchange
-    if (n && ex.sig) {
-        hip_ok(hipStreamWriteValue32(ex.stream, ex.sig_halo, ex.seq, 0), "hipStreamWriteValue32");
-        hip_ok(hipStreamWaitValue32(cur, ex.sig_halo, ex.seq, hipStreamWaitValueGte, 0xffffffffu),
+    if (sig) {
+        hip_ok(hipStreamWriteValue32(ex.stream, ex.sig_halo, seq, 0), "hipStreamWriteValue32");
+        hip_ok(hipStreamWaitValue32(cur, ex.sig_halo, seq, hipStreamWaitValueGte, 0xffffffffu),
                "hipStreamWaitValue32");
     } else if (n) {
         hip_ok(hipEventRecord(ex.ev_halos, ex.stream), "hipEventRecord");
@@ -516,6 +532,8 @@ PYBIND11_MODULE(_psad_torch, m) {
         std::lock_guard<std::mutex> lock(g_mutex);
         return static_cast<int64_t>(g_slab_plans.size());
     });
+    m.def("num_event_sweeps", []() { return g_event_sweeps.load(); },
+          "exchanging slab sweeps ordered by event record + wait (PSAD_SLAB_SYNC=event, or another compute stream)");
     m.def("set_debug_poison", [](bool on) { g_poison.store(on); },
           "fill the outputs allocated uninitialised with NaN (tests: a kernel that leaves cells unwritten shows)");
     m.def("num_plans", []() {

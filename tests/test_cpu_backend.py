@@ -300,13 +300,19 @@ def test_create_kernel_iteration_slice(target, islice):
         op.create_forward_kernel(target, iteration_slice=(slice(0, None, 2),))
 
 
-@pytest.mark.parametrize('gl', [2, [(1, 2), 3, (2, 1)]])
+@pytest.mark.parametrize('gl', [1, 2, [(1, 2), 3, (2, 1)], [1, 1, (1, 1)]])
 def test_create_kernel_explicit_ghost_layers(gl):
     """create_forward_kernel(ghost_layers=k | per-axis (lower, upper)) like pystencils: the kernel writes
-    [lower, N - upper) per axis and leaves the rest."""
+    [lower, N - upper) per axis and leaves the rest. The same k >= the stencil radius on every side is the
+    interior-only kernel (no iteration slice: on the GPU the tuned schedules); other layers take the
+    iteration-slice kernel."""
     op = pa.AutoDiffOp(W.asym_7pt(), boundary_handling='zeros')
     u = np.random.default_rng(4).uniform(-1, 1, (7, 8, 9)).astype(np.float32)
     k = op.create_forward_kernel('cpu', ghost_layers=gl)
+    uniform = isinstance(gl, int) or gl == [1, 1, (1, 1)]
+    assert (k.ir.islice is None) == uniform, k.ir.islice
+    kg = op.create_forward_kernel('gpu', ghost_layers=gl)
+    assert (kg.ir.islice is None) == uniform and (not uniform or kg.ir.ghost_layers == (gl if isinstance(gl, int) else 1))
     out = np.full_like(u, 5.0)
     k(u=u, out=out)
     gls = [(gl, gl)] * 3 if isinstance(gl, int) else [(g, g) if isinstance(g, int) else g for g in gl]

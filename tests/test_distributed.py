@@ -524,6 +524,56 @@ def test_zslab_full_size_eight_ranks_emulated(builder_name, edge, tmp_path):
 
 
 @pytest.mark.gpu
+def test_zslab_native_plan_on_two_streams(monkeypatch):
+    """One native slab plan applied from two compute streams: the signal-memory ordering
+    (``hipStreamWriteValue32`` of a sweep counter, the halo stream waiting for ``>=``) holds only while one stream
+    writes the counter, so the plan keeps it for the stream it first ran on and a sweep enqueued on another stream
+    orders through event record + wait. Results bitwise equal on both streams, the second stream's two sweeps on the
+    event path, the first stream back on the signals afterwards."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import pystencils_autodiff_amd as pa
+    from pystencils_autodiff_amd import _psad_torch
+    from pystencils_autodiff_amd import workloads as W
+    from pystencils_autodiff_amd.zslab import RcclHalo, ZSlabOp
+    monkeypatch.delenv('PSAD_SLAB_SYNC', raising=False)
+    monkeypatch.setenv('PSAD_NATIVE_SLAB', '1')
+    op = pa.AutoDiffOp(W.diffusion_7pt(), boundary_handling='zeros')
+    g = torch.Generator().manual_seed(9)
+    tu = torch.rand((16, 40, 128), generator=g).cuda()
+    td = (torch.rand((16, 40, 128), generator=g) * 2 - 1).cuda()
+    z = ZSlabOp(op, use_cuda=True)
+    z._halo = RcclHalo(loopback=True)
+    try:
+        z.warm_exchange(u=tu, diffout=td)
+        fn = z.autograd_function()
+
+        def step():
+            uu = tu.clone().requires_grad_(True)
+            (o,) = fn.apply(uu)
+            assert 'CppNode' in o.grad_fn.name(), o.grad_fn.name()
+            o.backward(td)
+            return o.detach().clone(), uu.grad.clone()
+        ref = step()
+        torch.cuda.synchronize()
+        n0 = _psad_torch.num_event_sweeps()
+        s2 = torch.cuda.Stream()
+        s2.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s2):
+            other = step()
+        torch.cuda.current_stream().wait_stream(s2)
+        n1 = _psad_torch.num_event_sweeps()
+        again = step()
+        torch.cuda.synchronize()
+        assert n1 - n0 == 2, (n0, n1)
+        assert _psad_torch.num_event_sweeps() == n1
+        for a, b in ((ref, other), (ref, again)):
+            assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    finally:
+        z.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('builder_name,shape', [('asym_7pt', (12, 40, 70)), ('diffusion_7pt', (2, 9, 64)),
                                                 ('stencil_27pt', (9, 24, 80)), ('stencil_27pt', (96, 64, 256))])
 def test_zslab_native_node_loopback(builder_name, shape, monkeypatch):

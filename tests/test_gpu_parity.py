@@ -588,6 +588,50 @@ def test_ws_loader_schedule_vs_oracle(params, shape, case):
                                 f'{name} {which} {params}')
 
 
+def test_ws_tilings_bitwise_same_process():
+    """The warp-specialised zsum ring (LDS-DMA loader wave, consumer plane barrier ``WS_CONSUMER_BARRIER``): ring
+    depths and chunk lengths change which slot holds a plane and when the loader refills it, not the FMA chain of a
+    cell — so every such variant, each launched three times in one process, gives bitwise the same 7-point fp32
+    forward and adjoint. A consumer read sunk below the next plane barrier (the band kernel's round-4 race) would
+    show here as run-to-run or variant-to-variant differences. Another tile shape is other code (the compiler
+    contracts the taps differently: 67 025 of 3.4 M cells differ in the last bit, deterministically,
+    gpurun_out r05_tests1.log): it is repeated for determinism and checked element-wise against the oracle, as is
+    the first variant."""
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    op = pa.AutoDiffOp(W.diffusion_7pt(), boundary_handling='zeros')
+    shape = (70, 96, 512)
+    g = torch.Generator().manual_seed(5)
+    u = (torch.rand(shape, generator=g) * 2 - 1).cuda()
+    variants = (dict(), dict(ZSUM=True, WS=True, D=2), dict(ZSUM=True, WS=True, D=3, ZMIN=8, ZMAX=8),
+                dict(ZSUM=True, WS=True, D=4, ZMIN=33, ZMAX=33), dict(ZSUM=True, WS=True, D=1, ZMIN=16, ZMAX=16))
+    other_tile = dict(ZSUM=True, WS=True, CX=4, NR=8, D=2)
+    for which, ac in (('f', op.forward_assignments), ('b', op.backward_assignments)):
+        res = []
+        for params in variants + (other_tile,):
+            k = StencilKernel(ac, boundary_handling='zeros', function_name=f'wsb_{which}', target='gpu',
+                              gpu_indexing_params=params).compile()
+            for rep in range(3):
+                out = torch.full(shape, float('nan'), device='cuda')
+                (fin,) = k.ir.fields_read
+                k(**{fin.name: u}, **{f.name: out for f in k.ir.fields_written})
+                cfg = k.last_variant[1]
+                assert cfg.WS and cfg.ZSUM and not cfg.BAND, cfg
+                res.append((params, rep, out))
+        torch.cuda.synchronize()
+        ins = {fin.name: u.cpu().numpy()}
+        ref = OE.evaluate(ac, ins, boundary_handling='zeros')
+        (name, r64), = ref.items()
+        for first in (res[0], res[-3]):
+            assert_close_rel(first[2].cpu().numpy(), r64, TOL[np.float32], f'ws {which} {first[0]}')
+            assert assert_cells_linear({name: first[2].cpu().numpy()}, ref, ac, ins, 'zeros', np.float32,
+                                       f'ws {which} {first[0]}')
+        bad = [f'{p} run {rep}: {int((o != res[0][2]).sum())} cells differ' for p, rep, o in res[1:-3]
+               if not torch.equal(o, res[0][2])]
+        bad += [f'{p} run {rep} vs run 0: {int((o != res[-3][2]).sum())} cells differ' for p, rep, o in res[-2:]
+                if not torch.equal(o, res[-3][2])]
+        assert not bad, f'{which}: ' + '; '.join(bad)
+
+
 @pytest.mark.parametrize('case', [
     ('7pt_f32', W.diffusion_7pt, np.float32, (9, 37, 262), 'xm'), ('7pt_f32', W.diffusion_7pt, np.float32, (6, 20, 261), 'xm'),
     ('7pt_f32', W.diffusion_7pt, np.float32, (13, 45, 255), 'xm'), ('asym_f32', W.asym_7pt, np.float32, (11, 29, 134), 'xm'),

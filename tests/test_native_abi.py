@@ -33,7 +33,7 @@ def test_library_exports_header_symbols():
     lib = rt.lib()
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.psad_abi_version() == 2
+    assert lib.psad_abi_version() == 3
     assert lib.psad_rtc_version() > 0
     assert lib.psad_error_string(1)
 
