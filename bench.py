@@ -132,15 +132,26 @@ def cpu_baseline(budget_s, workload='diffusion7_f32', edge=1024):
 
 def load_traffic(workload, kernel):
     """HBM bytes per launch of ``kernel`` from the committed PMC summary (profiles/traffic.json):
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled (gfx950 wide-read correction)."""
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled (gfx950 wide-read correction). Returns
+    (bytes, the entry: its source, the git commit it was collected at, the sha of the kernels it measured)."""
     path = os.path.join(ROOT, 'profiles', 'traffic.json')
     try:
         with open(path) as fh:
             entry = json.load(fh).get(workload) or {}
     except (OSError, ValueError):
-        return None, None
+        return None, {}
     k = entry.get('kernels', {}).get(kernel)
-    return (k['total'] if k else None), entry.get('source')
+    return (k['total'] if k else None), entry
+
+
+def kernel_sha(*kernels):
+    """16 hex digits of sha256 over the HIP sources of the launches that ran (the emitted kernels, the exact code
+    the PMC passes of profiles/traffic.json measured when its ``kernel_sha16`` is the same)."""
+    import hashlib
+    h = hashlib.sha256()
+    for k in kernels:
+        h.update(k.source(k.last_variant)[0].encode() if k.last_variant else b'?')
+    return h.hexdigest()[:16]
 
 
 def _sig(x, n=4):
@@ -157,9 +168,13 @@ def roofline(name, r, world):
     wl = WORKLOADS[name]
     n, zl = r['n'], r['zl']
     key = f'{name}_{n}^3' if world == 1 else f'{name}_{zl}x{n}^2_slab'
-    tf, src = load_traffic(key, r['kname'])
+    tf, entry = load_traffic(key, r['kname'])
     tb, _ = load_traffic(key, r['kname'].replace('_forward_', '_backward_'))
     traffic = tf + tb if tf is not None and tb is not None else None      # per step, like ``achieved``
+    src = entry.get('source')
+    if src and entry.get('git_head'):
+        src = f'{src}; collected at commit {entry["git_head"]}'
+    match = entry.get('kernel_sha16') == r['ksha'] if entry.get('kernel_sha16') else None
     return {'bound': 'hbm', 'achieved': round(r['achieved'], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': _sig(r['achieved'] / HBM_PEAK_GBS),
             'frac_fwd': _sig(r['achieved_fwd'] / HBM_PEAK_GBS),
@@ -167,6 +182,8 @@ def roofline(name, r, world):
             'achieved_fwd': round(r['achieved_fwd'], 1), 'achieved_bwd': round(r['achieved_bwd'], 1),
             'traffic': traffic, 'traffic_fwd_launch': tf,
             'traffic_source': src or f'no PMC entry for the launch shape {key}',
+            'kernel_sha16': r['ksha'], 'traffic_kernel_sha16': entry.get('kernel_sha16'),
+            'traffic_measured_these_kernels': match,
             'kernel': f'{r["kname"]} + its adjoint (step: both sweeps, {2 * wl["bytes"]} B per cell)',
             'bytes_per_launch': r['bytes_fwd'], 'bytes_per_step': 2 * wl['bytes'] * r['cells']}
 
@@ -221,7 +238,7 @@ def run_workload(name, edge, args, world, rank, distributed, extras, warmup=None
     bwd_k.prepare(diffout=d, diffu=scratch[1])
     del scratch
     # and a first backward with an explicit gradient (its lazy imports in autograd._make_grads cost ~40 ms)
-    # run on a 1-element tensor (scripts/probes/first_step.py)
+    # run on a 1-element tensor (measured by a round-2 probe)
     probe = torch.zeros(1, device=u.device, requires_grad=True)
     (probe * 2).backward(torch.ones_like(probe))
     del probe
@@ -305,6 +322,7 @@ def run_workload(name, edge, args, world, rank, distributed, extras, warmup=None
     zop_keep = zop if distributed else None
     kname = fwd_k.source(fwd_k.last_variant)[1] if fwd_k.last_variant else fwd_k.name
     out = dict(n=n, zl=zl, value=value, ms_per_step=ms_per_step, fwd_ms=fwd_ms, bwd_ms=bwd_ms, achieved=achieved,
+               ksha=kernel_sha(fwd_k, bwd_k),
                achieved_fwd=achieved_fwd, achieved_bwd=achieved_bwd, bytes_fwd=bytes_fwd, kname=kname,
                cells=cells_total, extra=result_extra, zop=zop_keep)
     del uu, u, d, fn, op

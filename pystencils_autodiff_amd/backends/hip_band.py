@@ -316,6 +316,8 @@ def emit_band(ir, name, cfg):
             L.append(f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? pb : '
                      f'f_{S.name}), (short)0, pb ? (int)(YX * {es}) : 0, 0x00020000);')
         L.append(f'      {et}* dst = lds + slot * {SLOT};')
+        if cfg.BABL == 3:
+            L.append('      if (Z < 0)   // ablation probe: no plane loads')
         L.append('      #pragma unroll')
         L.append(f'      for (int i = 0; i < {NI}; ++i)')
         L.append(f'        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + i * '
@@ -572,6 +574,18 @@ def emit_band(ir, name, cfg):
     def taps(ind, r, sets, first):
         """FMA statements of input row r into the given (set, dz) accumulators, dx outer."""
         B = []
+        if cfg.BABL == 1:
+            # ablation probe: one add per row and set (the row's loads and one convert stay live)
+            for st, dz in sets:
+                for si in range(NP):
+                    o = min(max(r - 1, 0), R - 1)
+                    acc = A(si, st, o, 0)
+                    if dz == -1 and (si, o, 0) not in first:
+                        first.add((si, o, 0))
+                        B.append(f'{ind}{acc} = {operand(0, 0)};')
+                    else:
+                        B.append(f'{ind}{acc} = {acc} + {operand(0, 0)};')
+            return B
         for dx in (-1, 0, 1):
             for st, dz in sets:
                 for si in range(NP):
@@ -759,6 +773,8 @@ def emit_band(ir, name, cfg):
                     for a in range(4):
                         if (si, o, a) not in first:
                             B.append(f'{ind}  {A(si, sn, o, a)} = {azero};')
+        if cfg.BABL == 2 and cond is not None:
+            cond = f'({cond}) && Z < 0' if cond else 'Z < 0'          # ablation probe: no output stores
         if store is not None and not interleave:
             B.append(f'{ind}  if ({cond}) {{' if cond else f'{ind}  {{')
             for si, fld in enumerate(store_field):

@@ -70,7 +70,7 @@ BAND_F32_IDLE_MAX_X = 1024
 # keys are this layer's tile parameters; an unknown one is a typo and raises.
 TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
              'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE', 'BLDR', 'BLAUX', 'BPAD', 'BZF', 'BREG', 'BMBR', 'BNT', 'BPE', 'BSI',
-             'BPRIO')
+             'BPRIO', 'BABL')
 
 
 def _band_config(ir, ve, shape, over):
@@ -149,7 +149,7 @@ def _band_config(ir, ve, shape, over):
                        BSTAG=int(over.get('BSTAG', 0)), BWPE=int(over.get('BWPE', 0)), BLDR=int(over.get('BLDR', 0)),
                        BLAUX=int(over.get('BLAUX', 0)), BPAD=pad, BZF=int(over.get('BZF', 1)), BREG=reg,
                        BMBR=int(over.get('BMBR', 0)), BNT=int(over.get('BNT', 2)), BPE=int(over.get('BPE', 0)),
-                       BSI=int(over.get('BSI', 0)), BPRIO=int(over.get('BPRIO', 0)))
+                       BSI=int(over.get('BSI', 0)), BPRIO=int(over.get('BPRIO', 0)), BABL=int(over.get('BABL', 0)))
 
 
 def default_march_config(ir, ve, shape=None, tuning=None, band=True):

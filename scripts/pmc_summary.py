@@ -27,6 +27,8 @@ def main():
     p.add_argument('--json')
     p.add_argument('--source', default='')
     p.add_argument('--select', default='autodiffop', help='substring of the kernel names of the workload')
+    p.add_argument('--git-head', default='', help='the commit the passes ran at')
+    p.add_argument('--kernel-sha', default='', help="bench.py's roofline.kernel_sha16 of the measured launches")
     a = p.parse_args()
     f = per_kernel(a.fetch, 'FETCH_SIZE')
     w = per_kernel(a.write, 'WRITE_SIZE')
@@ -39,6 +41,7 @@ def main():
     if a.json and a.workload:
         sel = {k: v for k, v in out.items() if a.select in k}
         entry = {'kernels': sel, 'algorithmic_bytes_per_launch': a.bytes, 'source': a.source,
+                 'git_head': a.git_head, 'kernel_sha16': a.kernel_sha,
                  'note': 'FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KB->bytes, mean per launch'}
         fwd = [v['total'] for k, v in sel.items() if 'forward' in k]
         entry['bytes_per_launch'] = fwd[0] if fwd else None
