@@ -58,23 +58,46 @@ class SimulationResultsTensors:
         self.output_velocity_tensor = output_velocity_tensor
 
 
-def _lattice_sweeps(step, which, launches):
+def _lattice_sweeps(step, which, launches, force=None, dforce=None):
     """The lattice kernels over ``launches`` (tensor tuples of ``LatticeKernels.forward`` / ``adjoint``) on the
     current stream: one launch plan per distinct (shapes, strides) — the first, middle and last steps — and only
-    the pointers packed per launch."""
+    the pointers packed per launch. ``force`` (a per-cell force field): bound to every launch; ``dforce``: the
+    adjoint launches add their force adjoints into it."""
     K = step._lattice_kernels()
     mask = step._flag_arg()
     ids = step._ids_arg()
     om = step._omega_of()
     mptr = (mask.data_ptr() if mask is not None else 0, ids.data_ptr() if ids is not None else 0)
+    if force is not None:
+        mptr += (force.data_ptr(),) + ((dforce.data_ptr(),) if which == 'adj' else ())
     stream = _torch()._C._cuda_getCurrentRawStream(launches[0][0].device.index)
     plans = {}
     for ts in launches:
         sig = tuple(t.stride() for t in ts)
         plan = plans.get(sig)
         if plan is None:
-            plan = plans[sig] = K.plan(which, list(ts), mask, om, ids)
+            plan = plans[sig] = K.plan(which, list(ts), mask, om, ids, force, dforce if which == 'adj' else None)
         plan(tuple(t.data_ptr() for t in ts) + mptr, stream, om)
+
+
+def _plain_force_field(force, D):
+    """The force FIELD when the rule's force is exactly ``F(x)[a]`` per axis a (one field of D components read at
+    the cell itself), else None."""
+    if force is None:
+        return None
+    comps = [sp.sympify(v) for v in force]
+    if len(comps) != D or not all(isinstance(c, ps.Field.Access) for c in comps):
+        return None
+    fields = {c.field for c in comps}
+    if len(fields) != 1:
+        return None
+    (F,) = fields
+    if F.index_dimensions != 1 or int(F.index_shape[0]) != D:
+        return None
+    for a, c in enumerate(comps):
+        if tuple(int(o) for o in c.offsets) != (0,) * D or tuple(int(i) for i in c.index) != (a,):
+            return None
+    return F
 
 
 def _guess_src_dst_field_from_update_rule(update_rule, src_hint, dst_hint):
@@ -146,10 +169,17 @@ class AutoDiffLatticeBoltzmannStep:
                 not force_is_field(getattr(update_rule, 'force', None)):
             from ._method import create_lb_adjoint_rule
             backward = create_lb_adjoint_rule(update_rule)
-        self._autodiff = AutoDiffOp(update_rule, 'LBM', boundary_handling='periodic', diff_mode='transposed',
-                                    time_constant_fields=list(time_constant_fields) or None,
-                                    constant_fields=list(constant_fields), backward_assignments=backward)
-        self._additional_fields = [f for f in self._autodiff.forward_input_fields if f not in (src, tmp)]
+        # the rule's AutoDiffOp (its kernels are the schedule for rules the lattice kernels do not take, and its
+        # transposed derivation — tens of seconds of sympy for a D3Q19 force-field rule — is only needed then):
+        # built on first use
+        self._autodiff_op = None
+        self._autodiff_args = dict(forward_assignments=update_rule, op_name='LBM', boundary_handling='periodic',
+                                   diff_mode='transposed', time_constant_fields=list(time_constant_fields) or None,
+                                   constant_fields=list(constant_fields), backward_assignments=backward)
+        self._diff_prefix = 'diff'
+        # the op's forward input fields (the fields the rule reads, sorted by name — transposed_backward's order)
+        read = {a.field for asg in update_rule.all_assignments for a in sp.sympify(asg.rhs).atoms(ps.Field.Access)}
+        self._additional_fields = [f for f in sorted(read, key=str) if f not in (src, tmp)]
         scalars = sorted({s for a in update_rule.all_assignments for s in a.rhs.free_symbols
                           if isinstance(s, sp.Symbol) and not isinstance(s, ps.Field.Access)}
                          - {a.lhs for a in update_rule.subexpressions}, key=str)
@@ -169,18 +199,42 @@ class AutoDiffLatticeBoltzmannStep:
             ((lambda v=rr: float(v)) if rr is not None else None)
         # (PSAD_LBM_LATTICE=0: the AutoDiffOp kernels instead — tests of that path, A/B probes)
         force = getattr(update_rule, 'force', None)
-        self._lattice_force = (getattr(update_rule, 'force_model', None),
-                               None if force is None else tuple(float(v) for v in force)) \
-            if force is None or all(sp.sympify(v).is_number for v in force) else None
+        # a per-cell force read as F(x)[a] (the field's centre, component a, for every axis): the lattice kernels
+        # take the field as an array and accumulate its adjoint; any other force expression runs on the AutoDiffOp
+        # kernels
+        self._force_field = _plain_force_field(force, src.spatial_dimensions)
+        if self._force_field is not None:
+            self._lattice_force = (getattr(update_rule, 'force_model', None), None)
+        else:
+            self._lattice_force = (getattr(update_rule, 'force_model', None),
+                                   None if force is None else tuple(float(v) for v in force)) \
+                if force is None or all(sp.sympify(v).is_number for v in force) else None
+        extras_ok = not self._additional_fields or (self._force_field is not None and
+                                                    self._additional_fields == [self._force_field])
         self._lattice = {} if (getattr(update_rule, 'stencil', None) is not None and not time_constant_fields
                                and self._lattice_force is not None
                                and os.environ.get('PSAD_LBM_LATTICE', '1') != '0'
-                               and not self._additional_fields and self._omega_of is not None
-                               and np.dtype(src.dtype.numpy_dtype) in (np.float32, np.float64)) else None
+                               and extras_ok and self._omega_of is not None
+                               and np.dtype(src.dtype.numpy_dtype) in (np.float32, np.float64)
+                               and (self._force_field is None or
+                                    self._force_field.dtype.numpy_dtype == src.dtype.numpy_dtype)) else None
         self._boundary = BoundaryHandling(self.domain_size, on_change=self._flags_changed)
         self._adjoint_boundary_conditions = {}
         self._flag_dev = None
         self._ids_dev = None
+
+    @property
+    def _autodiff(self):
+        if self._autodiff_op is None:
+            self._autodiff_op = AutoDiffOp(**self._autodiff_args)
+        return self._autodiff_op
+
+    def _adjoint_name(self, field):
+        """The adjoint array name of an additional input field (the op's field map once it exists; the AdjointField
+        naming ``diff<name>`` before, which is what that map holds)."""
+        if self._autodiff_op is not None:
+            return self._autodiff_op.adjoint_name(field)
+        return self._diff_prefix + field.name
 
     # -- reference-named properties ----------------------------------------------------------------
     @property
@@ -356,7 +410,7 @@ class AutoDiffLatticeBoltzmannStep:
         if k is None:
             k = self._lattice[(walls, links)] = LatticeKernels(
                 self.method, getattr(self._update_rule, 'compressible', False), self.pdf_field.dtype.numpy_dtype,
-                walls, self._target, links, *self._lattice_force)
+                walls, self._target, links, *self._lattice_force, force_field=self._force_field is not None)
         return k
 
     # -- kernels -----------------------------------------------------------------------------------
@@ -368,14 +422,31 @@ class AutoDiffLatticeBoltzmannStep:
 
     def _fwd(self, src, dst, extra):
         if self._lattice is not None:
-            return self._lattice_kernels().forward(src, dst, self._omega_of(), self._flag_arg(), ids=self._ids_arg())
+            return self._lattice_kernels().forward(src, dst, self._omega_of(), self._flag_arg(), ids=self._ids_arg(),
+                                                   force=self._force_arg(extra))
         kf, _ = self._kernels()
         kf(**{self._pdf_arr_name: src, self._tmp_arr_name: dst}, **extra, **self.kernel_params)
 
+    def _force_arg(self, extra):
+        """The per-cell force array of the lattice kernels (None without a force field)."""
+        if self._force_field is None:
+            return None
+        try:
+            return extra[self._force_field.name]
+        except (KeyError, TypeError):
+            raise ValueError(f"the update rule reads the force field '{self._force_field.name}': pass its array "
+                             "(extra={name: array})") from None
+
     def _bwd(self, src, diffdst, diffsrc, extra, extra_adj):
         if self._lattice is not None:
+            dforce = None
+            if self._force_field is not None:
+                name = self._adjoint_name(self._force_field)
+                if name not in (extra_adj or {}):
+                    raise ValueError(f"the force field's adjoint '{name}' needs an array (extra_adj), accumulated into")
+                dforce = extra_adj[name]
             return self._lattice_kernels().adjoint(src, diffdst, diffsrc, self._omega_of(), self._flag_arg(),
-                                                   ids=self._ids_arg())
+                                                   ids=self._ids_arg(), force=self._force_arg(extra), dforce=dforce)
         _, kb = self._kernels()
         kb(**{self._pdf_arr_name: src, 'diff' + self._tmp_arr_name: diffdst, 'diff' + self._pdf_arr_name: diffsrc},
            **extra, **extra_adj, **self.kernel_params)
@@ -442,7 +513,7 @@ class AutoDiffLatticeBoltzmannStep:
         torch = _torch()
         step = self
         T = int(num_time_steps)
-        adj = {f.name: self._autodiff.adjoint_name(f) for f in extras}
+        adj = {f.name: self._adjoint_name(f) for f in extras}
 
         class LbmTimesteps(torch.autograd.Function):
             @staticmethod
@@ -470,7 +541,8 @@ class AutoDiffLatticeBoltzmannStep:
                 x0 = x0 if lattice and step._lattice_input_ok(x0) else step._as_layout(x0)
                 if lattice:
                     states = [x0] + step._internal_states(T - 1) + [step._alloc(zero=False)]
-                    _lattice_sweeps(step, 'fwd', [(states[t], states[t + 1]) for t in range(T)])
+                    _lattice_sweeps(step, 'fwd', [(states[t], states[t + 1]) for t in range(T)],
+                                    step._force_arg(ex))
                 else:
                     states = [x0]
                     for t in range(T):
@@ -518,8 +590,14 @@ class AutoDiffLatticeBoltzmannStep:
                         nxt = out if t == 0 else ping[(T - 1 - t) % 2]
                         launches.append((records[t], cur, nxt))
                         cur = nxt
-                    _lattice_sweeps(step, 'adj', launches)
-                    return out
+                    if step._force_field is None:
+                        _lattice_sweeps(step, 'adj', launches)
+                        return out
+                    # the force adjoint: every step's adjoint launch adds its share into one zeroed array
+                    F = step._force_arg(ex)
+                    dF = torch.zeros_like(F)
+                    _lattice_sweeps(step, 'adj', launches, F, dF)
+                    return out, dF
                 cur = g
                 acc = {n: torch.zeros_like(x) for n, x in ex.items()}
                 for t in reversed(range(T)):

@@ -44,7 +44,8 @@ def _c(v):
 SELF_BIT = 30      # bit of a cell's neighbour mask: the cell itself is an obstacle (bits 0..Q-1: x − c_i is one)
 
 
-def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=None, force_model=None, force=None):
+def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=None, force_model=None, force=None,
+          force_field=False):
     """Source of the forward (``lbm_fwd``) and adjoint (``lbm_adj``) kernels.
 
     ``addr='buf'`` (HIP): every pdf array is one buffer resource (its bytes below 2³²); a component's plane
@@ -59,13 +60,20 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     adds the constant 3 w_i (c_i·F) to every fluid cell's post-collision value (its adjoint is unchanged); 'guo'
     shifts the velocity by F/2 (/ρ) and adds w_i (1 − ω/2)(3 (c_i − u)·F + 9 (c_i·u)(c_i·F)), whose derivative through
     u joins the adjoint's velocity sensitivities: B_a += C_a / ω with
-    C_a = (1 − ω/2) Σ_i g_i w_i (9 c_ia (c_i·F) − 3 F_a)."""
+    C_a = (1 − ω/2) Σ_i g_i w_i (9 c_ia (c_i·F) − 3 F_a).
+    ``force_field``: the force is a per-cell vector field instead (``force`` unused): the kernels read ``F(x)`` from a
+    ``[*domain, D]`` array by strides (an additional input of the rule, ``_autodiff_lbstep.py:113-128``) and the
+    adjoint ACCUMULATES the force adjoint into ``dforce`` (same strides; every cell by one thread, so the T steps of
+    the time-step op sum into one zeroed array): 'simple' ``dF_a = 3 Σ_i g_i w_i c_ia``; 'guo' — through the explicit
+    term and the velocity shift ``∂u_a/∂F_a = 1/2 (/ρ)`` — ``dF_a = (1 − ω/2) Bf_a + ω B_a / 2 (/ρ)`` with ``Bf_a`` the
+    equilibrium part of the velocity sensitivity (before the ρ scaling) and ``B_a`` the full one."""
     D, Q = stencil.D, stencil.Q
     dirs = [tuple(d) for d in stencil.directions]
     w = [float(x) for x in stencil.weights]
     fm = None if force_model is None else str(force_model).lower()
-    F = [float(v) for v in force] if fm else None
-    cF = [sum(c * f for c, f in zip(d, F)) for d in dirs] if fm else None
+    ff = bool(fm) and bool(force_field)
+    F = [float(v) for v in force] if fm and not ff else None
+    cF = [sum(c * f for c, f in zip(d, F)) for d in dirs] if fm and not ff else None
     inv = [stencil.inverse_direction_index(i) for i in range(Q)]
     axes = ['z', 'y', 'x'][3 - D:]          # spatial axes, axis 0 slowest; x fastest
     ct = ctype
@@ -90,6 +98,32 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
 
     def c_(v):
         return f'({ct}){_c(v)}'
+
+    def Fa(a):
+        """Force component a: a constant, or the cell's value (``force_field``)."""
+        return f'F{a}' if ff else c_(F[a])
+
+    def cFi(i, scale=1):
+        """scale · (c_i · F) (None where it is the constant 0)."""
+        if ff:
+            if not any(dirs[i]):
+                return None
+            return f'cF{i}' if scale == 1 else f'({c_(scale)} * cF{i})'
+        return c_(scale * cF[i]) if cF[i] else None
+
+    def force_loads(L):
+        """The cell's force vector and its projections c_i · F (``force_field``)."""
+        if not ff:
+            return
+        fcell = ' + '.join(f'(IDX){a} * f_{a}' for a in axes)
+        L.append(f'  const IDX fc = {fcell};')
+        for a in range(D):
+            L.append(f'  const {ct} F{a} = ({ct})force[(IDX){a} * f_c + fc];')
+        for i in range(Q):
+            t = [('+ ' if dirs[i][a] > 0 else '- ') + f'F{a}' for a in range(D) if dirs[i][a]]
+            if t:
+                e = ' '.join(t)
+                L.append(f'  const {ct} cF{i} = {e[2:] if e.startswith("+ ") else "(" + e + ")"};')
 
     def key(d):
         return '_'.join({0: '0', 1: 'm', -1: 'p'}[c] for c in d)      # pull: x − c → m(inus) / p(lus)
@@ -191,11 +225,12 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         if compressible:
             L.append(f'  const {ct} irho = ({ct})1 / rho;')
         for a in range(D):
-            m = f'(m{a} + {c_(F[a] / 2)})' if fm == 'guo' else f'm{a}'      # Guo: velocity shifted by F/2
+            half = f'({ct})0.5 * F{a}' if ff else c_(F[a] / 2) if fm == 'guo' else None
+            m = f'(m{a} + {half})' if fm == 'guo' else f'm{a}'      # Guo: velocity shifted by F/2
             L.append(f'  const {ct} u{a} = {m}' + (' * irho;' if compressible else ';'))
         L.append(f'  const {ct} usq = ' + ' + '.join(f'u{a} * u{a}' for a in range(D)) + ';')
         if fm == 'guo':
-            L.append(f'  const {ct} uF = ' + ' + '.join(f'u{a} * {c_(F[a])}' for a in range(D)) + ';')
+            L.append(f'  const {ct} uF = ' + ' + '.join(f'u{a} * {Fa(a)}' for a in range(D)) + ';')
             L.append(f'  const {ct} kg = ({ct})1 - ({ct})0.5 * omega;')
 
     def cu_expr(i):
@@ -206,21 +241,28 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         return s_[2:] if s_.startswith('+ ') else '(' + s_ + ')'
 
     mask_param = 'const unsigned* __restrict__ nbmask, const unsigned char* __restrict__ wallid'
-    sig_fwd = (f'const T* __restrict__ src, T* __restrict__ dst, {mask_param}, const int Z, const int Y, const int X, '
-               'const IDX s_q, const IDX s_z, const IDX s_y, const IDX s_x, '
-               'const IDX d_q, const IDX d_z, const IDX d_y, const IDX d_x, '
+    fptr_f = ', const T* __restrict__ force' if ff else ''
+    fptr_a = ', const T* __restrict__ force, T* __restrict__ dforce' if ff else ''
+    fstr = 'const IDX f_c, const IDX f_z, const IDX f_y, const IDX f_x, ' if ff else ''
+    sig_fwd = (f'const T* __restrict__ src, T* __restrict__ dst, {mask_param}{fptr_f}, const int Z, const int Y, '
+               'const int X, const IDX s_q, const IDX s_z, const IDX s_y, const IDX s_x, '
+               f'const IDX d_q, const IDX d_z, const IDX d_y, const IDX d_x, {fstr}'
                f'const long long s_bytes, const long long d_bytes, const {ct} omega')
-    sig_adj = (f'const T* __restrict__ src, const T* __restrict__ g, T* __restrict__ out, {mask_param}, '
+    sig_adj = (f'const T* __restrict__ src, const T* __restrict__ g, T* __restrict__ out, {mask_param}{fptr_a}, '
                'const int Z, const int Y, const int X, '
                'const IDX s_q, const IDX s_z, const IDX s_y, const IDX s_x, '
                'const IDX g_q, const IDX g_z, const IDX g_y, const IDX g_x, '
-               'const IDX o_q, const IDX o_z, const IDX o_y, const IDX o_x, '
+               f'const IDX o_q, const IDX o_z, const IDX o_y, const IDX o_x, {fstr}'
                f'const long long s_bytes, const long long g_bytes, const long long o_bytes, const {ct} omega')
+    if ff and D == 2:
+        fstr_unused = '(void)f_z; '
+    else:
+        fstr_unused = ''
     cell = '((IDX)z * Y + y) * X + x' if D == 3 else '(IDX)y * X + x'
 
     # ---- forward
     L.append(f'{fn} void lbm_fwd_cell({sig_fwd}, const int z, const int y, const int x)\n{{')
-    L.append('  (void)Z; (void)s_bytes; (void)d_bytes; (void)wallid;')
+    L.append(f'  (void)Z; (void)s_bytes; (void)d_bytes; (void)wallid; {fstr_unused}')
     rsrc(L, 's', 'src')
     rsrc(L, 'd', 'dst')
     wrap_lines(L)
@@ -235,6 +277,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         for i in range(Q):
             L.append('    ' + store('d', 'dst', i, dcoff, load('s', 'src', i, f'so_{centre}')))
         L.append('    return;\n  }')
+    force_loads(L)
     pull_loads(L, 's', 'src')
     moments(L)
     for i in range(Q):
@@ -242,17 +285,17 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         L.append(f'    const {ct} poly = cu * (({ct})3 + ({ct})4.5 * cu) - ({ct})1.5 * usq;')
         feq = f'{c_(w[i])} * rho * (({ct})1 + poly)' if compressible else f'{c_(w[i])} * (rho + poly)'
         term = ''
-        if fm == 'simple' and cF[i]:
-            term = f' + {c_(3 * w[i] * cF[i])}'
+        if fm == 'simple' and cFi(i):
+            term = f' + {c_(3 * w[i])} * {cFi(i)}' if ff else f' + {c_(3 * w[i] * cF[i])}'
         elif fm == 'guo':
-            term = (f' + {c_(w[i])} * kg * (({ct})3 * ({c_(cF[i])} - uF)'
-                    + (f' + {c_(9 * cF[i])} * cu' if cF[i] else '') + ')')
+            term = (f' + {c_(w[i])} * kg * (({ct})3 * ({cFi(i) or c_(0)} - uF)'
+                    + (f' + {cFi(i, 9)} * cu' if cFi(i) else '') + ')')
         L.append('    ' + store('d', 'dst', i, dcoff, f'f{i} + omega * ({feq} - f{i}){term}') + ' }')
     L.append('}')
 
     # ---- adjoint (scatter to where the forward pulled from)
     L.append(f'{fn} void lbm_adj_cell({sig_adj}, const int z, const int y, const int x)\n{{')
-    L.append('  (void)Z; (void)s_bytes; (void)g_bytes; (void)o_bytes; (void)wallid;')
+    L.append(f'  (void)Z; (void)s_bytes; (void)g_bytes; (void)o_bytes; (void)wallid; {fstr_unused}')
     rsrc(L, 's', 'src')
     rsrc(L, 'g', 'g')
     rsrc(L, 'o', 'out')
@@ -271,6 +314,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         L.append('    return;\n  }')
     for i in range(Q):
         L.append(f'  const {ct} g{i} = {load("g", "g", i, gcoff)};')
+    force_loads(L)
     pull_loads(L, 's', 'src')
     moments(L)
     L.append(f'  {ct} S = 0, A = 0;')
@@ -278,6 +322,8 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         L.append(f'  {ct} B{a} = 0;')
         if fm == 'guo':
             L.append(f'  {ct} E{a} = 0;')           # Σ_i g_i w_i c_ia (c_i·F)
+        if ff and fm == 'simple':
+            L.append(f'  {ct} M{a} = 0;')           # Σ_i g_i w_i c_ia (the 'simple' force adjoint / 3)
     for i in range(Q):
         L.append(f'  {{ const {ct} cu = {cu_expr(i)};')
         L.append(f'    const {ct} gw = g{i} * {c_(w[i])};')
@@ -289,21 +335,35 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             for a in range(D):
                 if dirs[i][a]:
                     L.append(f'    B{a} {"+" if dirs[i][a] > 0 else "-"}= t;')
-            if fm == 'guo' and cF[i]:
-                L.append(f'    const {ct} tf = gw * {c_(cF[i])};')
+            if fm == 'guo' and cFi(i):
+                L.append(f'    const {ct} tf = gw * {cFi(i)};')
                 for a in range(D):
                     if dirs[i][a]:
                         L.append(f'    E{a} {"+" if dirs[i][a] > 0 else "-"}= tf;')
+            if ff and fm == 'simple':
+                for a in range(D):
+                    if dirs[i][a]:
+                        L.append(f'    M{a} {"+" if dirs[i][a] > 0 else "-"}= gw;')
         L.append('  }')
     if not compressible:
         L.append('  A = S;')
     for a in range(D):
         L.append(f'  B{a} -= ({ct})3 * u{a} * S;')
+        if ff and fm == 'guo':
+            L.append(f'  const {ct} Bf{a} = B{a};')
         if compressible:
             L.append(f'  B{a} *= rho;')
         if fm == 'guo':
             # the force term's derivative through u, scaled into B (v = … + ω (A + Σ B_a ∂u_a/∂f_j))
-            L.append(f'  B{a} += kg * (({ct})9 * E{a} - ({ct})3 * {c_(F[a])} * S) / omega;')
+            L.append(f'  B{a} += kg * (({ct})9 * E{a} - ({ct})3 * {Fa(a)} * S) / omega;')
+    if ff:
+        # the force adjoint of this cell, accumulated over the op's steps
+        for a in range(D):
+            if fm == 'simple':
+                val = f'({ct})3 * M{a}'
+            else:
+                val = f'kg * Bf{a} + ({ct})0.5 * omega * B{a}' + (' * irho' if compressible else '')
+            L.append(f'  dforce[(IDX){a} * f_c + fc] += {val};')
     if compressible:
         L.append(f'  const {ct} Bu = ' + ' + '.join(f'B{a} * u{a}' for a in range(D)) + ';')
     for j in range(Q):
@@ -329,9 +389,11 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     L.append('}')
 
     # ---- entry points
-    args_f = 'src, dst, nbmask, wallid, Z, Y, X, s_q, s_z, s_y, s_x, d_q, d_z, d_y, d_x, s_bytes, d_bytes, omega'
-    args_a = ('src, g, out, nbmask, wallid, Z, Y, X, s_q, s_z, s_y, s_x, g_q, g_z, g_y, g_x, o_q, o_z, o_y, o_x, '
-              's_bytes, g_bytes, o_bytes, omega')
+    fa_f, fa_a, fs = (', force', ', force, dforce', 'f_c, f_z, f_y, f_x, ') if ff else ('', '', '')
+    args_f = (f'src, dst, nbmask, wallid{fa_f}, Z, Y, X, s_q, s_z, s_y, s_x, d_q, d_z, d_y, d_x, {fs}s_bytes, d_bytes, '
+              'omega')
+    args_a = (f'src, g, out, nbmask, wallid{fa_a}, Z, Y, X, s_q, s_z, s_y, s_x, g_q, g_z, g_y, g_x, o_q, o_z, o_y, o_x, '
+              f'{fs}s_bytes, g_bytes, o_bytes, omega')
     if hip:
         # a block = 256 consecutive cells of the lattice in C order (rows of x), and consecutive blocks on one XCD
         # (bijective remap of the round-robin dispatch): a lattice row's x-shifted loads and the adjoint's
@@ -359,6 +421,9 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                          '(const unsigned*)P[2]; const unsigned char* wallid = (const unsigned char*)P[3];')
                 L.append('  const IDX s_q = S[0], s_z = S[1], s_y = S[2], s_x = S[3], d_q = S[4], d_z = S[5], '
                          'd_y = S[6], d_x = S[7];')
+                if ff:
+                    L.append('  const T* force = (const T*)P[4];')
+                    L.append('  const IDX f_c = S[8], f_z = S[9], f_y = S[10], f_x = S[11];')
                 L.append('  const long long s_bytes = 0, d_bytes = 0;')
                 call = f'lbm_fwd_cell({args_f}, z, y, x);'
             else:
@@ -367,6 +432,9 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                          'const unsigned char* wallid = (const unsigned char*)P[4];')
                 L.append('  const IDX s_q = S[0], s_z = S[1], s_y = S[2], s_x = S[3], g_q = S[4], g_z = S[5], '
                          'g_y = S[6], g_x = S[7], o_q = S[8], o_z = S[9], o_y = S[10], o_x = S[11];')
+                if ff:
+                    L.append('  const T* force = (const T*)P[5]; T* dforce = (T*)P[6];')
+                    L.append('  const IDX f_c = S[12], f_z = S[13], f_y = S[14], f_x = S[15];')
                 L.append('  const long long s_bytes = 0, g_bytes = 0, o_bytes = 0;')
                 call = f'lbm_adj_cell({args_a}, z, y, x);'
             L.append('  #pragma omp parallel for collapse(2) schedule(static)')
@@ -418,10 +486,12 @@ class LatticeKernels:
     cells' wall ids (the ``uint8`` flag array, C order) when ``links`` is given (walls other than plain
     bounce-back)."""
 
-    def __init__(self, stencil, compressible, dtype, walls, target, links=None, force_model=None, force=None):
+    def __init__(self, stencil, compressible, dtype, walls, target, links=None, force_model=None, force=None,
+                 force_field=False):
         self.stencil = stencil
         self.force_model = force_model
-        self.force = None if force_model is None else tuple(float(v) for v in force)
+        self.force_field = bool(force_model) and bool(force_field)
+        self.force = None if force_model is None or self.force_field else tuple(float(v) for v in force)
         self.compressible = bool(compressible)
         self.dtype = np.dtype(dtype)
         if self.dtype not in (np.float32, np.float64):
@@ -436,9 +506,9 @@ class LatticeKernels:
     def source(self, idx='int', addr='buf'):
         if self.target != 'gpu':
             return _emit(self.stencil, self.compressible, self.ct, self.walls, 'c', 'i64', 'ptr', self.links,
-                         self.force_model, self.force)
+                         self.force_model, self.force, self.force_field)
         return _emit(self.stencil, self.compressible, self.ct, self.walls, 'hip', idx, addr, self.links,
-                     self.force_model, self.force)
+                     self.force_model, self.force, self.force_field)
 
     # -- GPU ---------------------------------------------------------------------------------------
     def _gpu_fn(self, which, idx, addr, device):
@@ -499,17 +569,44 @@ class LatticeKernels:
             fn_args += list(lattice_strides(t, self.stencil.D))
         return idx, addr, fn_args
 
-    def plan(self, which, tensors, mask, omega, ids=None):
+    def _force_check(self, shape, force, dforce, which, xp_tensor=True):
+        """The per-cell force (and, for the adjoint, its accumulated adjoint): ``[*domain, D]`` of the pdf dtype,
+        ``dforce`` with the strides of ``force``; none without a force field."""
+        D = self.stencil.D
+        need = [force] + ([dforce] if which == 'adj' else [])
+        if not self.force_field:
+            if force is not None or dforce is not None:
+                raise ValueError('these lattice kernels take no force field')
+            return
+        if any(t is None for t in need):
+            raise ValueError(f'the force-field lattice kernels need the force{" and its adjoint" if which == "adj" else ""}')
+        for t in need:
+            if tuple(t.shape) != tuple(shape[:D]) + (D,):
+                raise ValueError(f'force field of shape {tuple(t.shape)}: expected {tuple(shape[:D]) + (D,)}')
+            if (t.dtype != self.dtype) if not xp_tensor else (str(t.dtype).split('.')[-1] != self.dtype.name):
+                raise ValueError(f'force field dtype {t.dtype}: expected {self.dtype}')
+        if which == 'adj' and tuple(dforce.stride() if xp_tensor else dforce.strides) != \
+                tuple(force.stride() if xp_tensor else force.strides):
+            raise ValueError('the force adjoint must have the strides of the force')
+
+    def plan(self, which, tensors, mask, omega, ids=None, force=None, dforce=None):
         """The launch of ``which`` ('fwd' / 'adj') on tensors of these shapes, strides, dtype and device (with or
         without walls): a ``LaunchPlan`` whose pointer slots and relaxation rate are patched per launch — the
         time-step op launches T of them per apply. ω is not part of the key (a trained or scheduled rate reuses the
         plan); the plan is built with the first ω it sees."""
         key = (which, mask is not None) + tuple((tuple(t.shape), tuple(t.stride()), t.dtype, t.device)
-                                                for t in tensors)
+                                                for t in tensors) + \
+            ((tuple(force.shape), tuple(force.stride())) if force is not None else ())
         plan = self._plans.get(key)
         if plan is not None:
             return plan
+        self._force_check(tuple(tensors[0].shape), force, dforce, which)
         idx, addr, strides = self._common(tensors, mask, ids)
+        if force is not None:
+            # the force is read (and its adjoint accumulated) through plain pointers with IDX offsets
+            if max(self._reach(force), self._reach(dforce) if dforce is not None else 0) >= 2 ** 31 - 1:
+                idx = 'long long'
+            strides += list(lattice_strides(force, self.stencil.D))
         dev = tensors[0].device.index
         fn = self._gpu_fn(which, idx, addr, dev)
         Z, Y, X = self._extent(tensors[0])
@@ -518,27 +615,33 @@ class LatticeKernels:
         reach = [self._reach(t) * t.element_size() for t in tensors]
         ptrs = [t.data_ptr() for t in tensors] + [mask.data_ptr() if mask is not None else 0,
                                                   ids.data_ptr() if ids is not None else 0]
-        fmt = 'Q' * len(ptrs) + 'iii' + code * (4 * len(tensors)) + 'q' * len(tensors) + \
+        if force is not None:
+            ptrs += [force.data_ptr()] + ([dforce.data_ptr()] if which == 'adj' else [])
+        fmt = 'Q' * len(ptrs) + 'iii' + code * len(strides) + 'q' * len(tensors) + \
             ('d' if self.ct == 'double' else 'f')
         args = _pack(fmt, *ptrs, Z, Y, X, *strides, *reach, float(omega))
         plan = self._plans[key] = LaunchPlan(fn, nblocks, args, len(ptrs), dev, _offset(fmt, len(fmt) - 1), fmt[-1])
         return plan
 
-    def forward(self, src, dst, omega, mask=None, stream=None, ids=None):
-        """``dst = stream-pull-collide(src)`` (torch tensors ``[*domain, q]``, any strides)."""
+    def forward(self, src, dst, omega, mask=None, stream=None, ids=None, force=None):
+        """``dst = stream-pull-collide(src)`` (torch tensors ``[*domain, q]``, any strides; ``force``: the per-cell
+        force ``[*domain, D]`` of force-field kernels)."""
         if self.target != 'gpu':
-            return self._cpu('fwd', [src, dst], omega, mask, ids)
-        self.plan('fwd', [src, dst], mask, omega, ids)(
+            return self._cpu('fwd', [src, dst], omega, mask, ids, force)
+        self.plan('fwd', [src, dst], mask, omega, ids, force)(
             (src.data_ptr(), dst.data_ptr(), mask.data_ptr() if mask is not None else 0,
-             ids.data_ptr() if ids is not None else 0), _stream(stream, src), omega)
+             ids.data_ptr() if ids is not None else 0) + ((force.data_ptr(),) if force is not None else ()),
+            _stream(stream, src), omega)
 
-    def adjoint(self, src, g, out, omega, mask=None, stream=None, ids=None):
-        """``out = (∂ step / ∂ src)ᵀ g`` at the state ``src``."""
+    def adjoint(self, src, g, out, omega, mask=None, stream=None, ids=None, force=None, dforce=None):
+        """``out = (∂ step / ∂ src)ᵀ g`` at the state ``src``; force-field kernels also ADD ``(∂ step / ∂ F)ᵀ g`` to
+        ``dforce``."""
         if self.target != 'gpu':
-            return self._cpu('adj', [src, g, out], omega, mask, ids)
-        self.plan('adj', [src, g, out], mask, omega, ids)(
+            return self._cpu('adj', [src, g, out], omega, mask, ids, force, dforce)
+        self.plan('adj', [src, g, out], mask, omega, ids, force, dforce)(
             (src.data_ptr(), g.data_ptr(), out.data_ptr(), mask.data_ptr() if mask is not None else 0,
-             ids.data_ptr() if ids is not None else 0), _stream(stream, src), omega)
+             ids.data_ptr() if ids is not None else 0) +
+            ((force.data_ptr(), dforce.data_ptr()) if force is not None else ()), _stream(stream, src), omega)
 
     def _extent(self, t):
         shape = [int(n) for n in t.shape[:self.stencil.D]]
@@ -559,7 +662,7 @@ class LatticeKernels:
             fn = self._fns[which] = compile_c(self.source(), f'lbm_{which}', openmp=True)
         return fn
 
-    def _cpu(self, which, arrays, omega, mask, ids=None):
+    def _cpu(self, which, arrays, omega, mask, ids=None, force=None, dforce=None):
         arrays = [np.asarray(a) for a in arrays]
         for a in arrays:
             if a.dtype != self.dtype:
@@ -583,12 +686,16 @@ class LatticeKernels:
             idv = np.ascontiguousarray(ids, dtype=np.uint8)
             if idv.shape != shape[:D]:
                 raise ValueError('wall ids do not match the domain')
+        self._force_check(shape, force, dforce, which, xp_tensor=False)
         fn = self._cpu_fn(which)
         ptrs = [a.ctypes.data for a in arrays] + [m.ctypes.data if m is not None else 0,
                                                   idv.ctypes.data if idv is not None else 0]
         strides = []
         for a in arrays:
             strides += list(lattice_strides(a, D))
+        if force is not None:
+            ptrs += [force.ctypes.data] + ([dforce.ctypes.data] if which == 'adj' else [])
+            strides += list(lattice_strides(force, D))
         ext = list(shape[:D]) if D == 3 else [1] + list(shape[:D])
         P = (ctypes.c_void_p * len(ptrs))(*ptrs)
         N = (ctypes.c_longlong * 3)(*ext)

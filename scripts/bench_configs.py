@@ -180,17 +180,25 @@ def run_slab(name, builder, shape, dtype, full_cells, steps=20, warmup=3):
     sys.stdout.flush()
 
 
-def run_lbm(name, stencil, shape, dtype, T=10, reps=5, compressible=False, walls=False, force_model=None):
+def run_lbm(name, stencil, shape, dtype, T=10, reps=5, compressible=False, walls=False, force_model=None,
+            force_field=False):
     """Lattice Boltzmann time-step op (lbm.AutoDiffLatticeBoltzmannStep.create_timestep_op): T forward steps
     and the T adjoint steps, HIP events around Op.apply and backward (back-to-back applies). MLUPS = cells · T / time; algorithmic
     bytes per cell and step: forward 2q·s (read src, write dst), adjoint 3q·s (read diffdst and the recorded
-    src, write diffsrc), s = element size; the ghost sync, state records and adjoint border fills are extra."""
+    src, write diffsrc), s = element size; the ghost sync, state records and adjoint border fills are extra.
+    ``force_field``: a per-cell force (a D-component fzyx field, an input of the op): + D·s per cell and step forward
+    (the force read), + 3·D·s adjoint (the force read, its accumulated adjoint read and written)."""
     import torch
 
     from pystencils_autodiff_amd import lbm
+    from pystencils_autodiff_amd import ps
     D = len(shape)
-    rule = lbm.create_lb_update_rule(stencil, compressible=compressible, data_type=str(dtype).replace('torch.', ''),
-                                     force_model=force_model, force=(1e-5, -2e-5, 5e-6)[:D] if force_model else None)
+    dts = str(dtype).replace('torch.', '')
+    force = (1e-5, -2e-5, 5e-6)[:D] if force_model else None
+    if force_model and force_field:
+        force = ps.fields(f"F({D}): {dts}[{D}D]", layout='fzyx')
+    rule = lbm.create_lb_update_rule(stencil, compressible=compressible, data_type=dts, force_model=force_model,
+                                     force=force)
     step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.5, target='gpu')
     if walls:
         # a channel: no-slip walls on the first and last rows of axis 1
@@ -208,9 +216,14 @@ def run_lbm(name, stencil, shape, dtype, T=10, reps=5, compressible=False, walls
     gr = step.empty_pdfs()
     gr.copy_(torch.rand(tuple(shape) + (q,), generator=g, device='cuda', dtype=dtype))
     fw, bw = [], []
+    extra = ()
+    if force_field:
+        Fv = torch.empty([D] + list(shape), device='cuda', dtype=dtype).permute(*range(1, D + 1), 0)
+        Fv.copy_(1e-5 * (torch.rand(tuple(shape) + (D,), generator=g, device='cuda', dtype=dtype) - 0.5))
+        extra = (Fv.requires_grad_(True),)
 
     def one():
-        Op.apply(x).backward(gr)
+        Op.apply(x, *extra).backward(gr)
         x.grad = None
     settle(one)
     # back-to-back applies as run() times the stencil configs (the queue stays ahead of the GPU: event times are
@@ -219,7 +232,7 @@ def run_lbm(name, stencil, shape, dtype, T=10, reps=5, compressible=False, walls
     for i in range(reps + 2):
         e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
         e0.record()
-        out = Op.apply(x)
+        out = Op.apply(x, *extra)
         e1.record()
         out.backward(gr)
         e2.record()
@@ -239,8 +252,9 @@ def run_lbm(name, stencil, shape, dtype, T=10, reps=5, compressible=False, walls
            'schedule': 'lattice' if step._lattice is not None else 'autodiffop', 'walls': bool(walls),
            'fwd_mlups': round(cells * T / (f_ms * 1e-3) / 1e6, 1), 'bwd_mlups': round(cells * T / (b_ms * 1e-3) / 1e6, 1),
            'fwd_ms': round(f_ms, 4), 'bwd_ms': round(b_ms, 4),
-           'fwd_GBps': round(2 * q * es * cells * T / (f_ms * 1e-3) / 1e9, 1),
-           'bwd_GBps': round(3 * q * es * cells * T / (b_ms * 1e-3) / 1e9, 1)}
+           'fwd_GBps': round((2 * q + (D if force_field else 0)) * es * cells * T / (f_ms * 1e-3) / 1e9, 1),
+           'bwd_GBps': round((3 * q + (3 * D if force_field else 0)) * es * cells * T / (b_ms * 1e-3) / 1e9, 1),
+           'force': (f'{force_model}, per-cell field' if force_field else force_model) if force_model else None}
     res['fwd_frac'] = round(res['fwd_GBps'] / PEAK, 4)
     res['bwd_frac'] = round(res['bwd_GBps'] / PEAK, 4)
     print(json.dumps(res))

@@ -634,15 +634,31 @@ def test_lbm_force_models_gpu_vs_oracle(stencil, shape, compressible, model, sch
 # summed over the steps (the reference's additional / time-constant fields, _autodiff_lbstep.py:113-128, :284-306)
 FIELD_FORCE_CASES = [('D2Q9', (9, 7), True, 'guo', 'numpy'), ('D2Q9', (8, 6), False, 'simple', 'fzyx'),
                      ('D2Q9', (7, 9), False, 'guo', 'fzyx'), ('D3Q19', (5, 4, 6), True, 'guo', 'numpy')]
+# the remaining (model, compressible, layout) combinations, lattice kernels only (the AutoDiffOp derivation of a D3Q19
+# rule takes ~1 min of sympy on the CPU)
+FIELD_FORCE_CASES_LATTICE = [('D3Q19', (4, 6, 5), False, 'simple', 'numpy'), ('D3Q19', (4, 5, 4), True, 'simple', 'fzyx'),
+                             ('D2Q9', (6, 8), True, 'simple', 'numpy'), ('D3Q19', (5, 5, 4), False, 'guo', 'fzyx')]
+FIELD_FORCE_ALL = [c + ('lattice',) for c in FIELD_FORCE_CASES + FIELD_FORCE_CASES_LATTICE] + \
+    [c + ('autodiffop',) for c in FIELD_FORCE_CASES]
 
 
-def _force_field_case(stencil, shape, compressible, model, layout, target, T=3):
+def _force_field_case(stencil, shape, compressible, model, layout, target, T=3, schedule='lattice'):
+    import os
     import torch
     D = len(shape)
     F = ps.fields(f"F({D}): float64[{D}D]", layout=layout)
     rule = lbm.create_lb_update_rule(stencil, compressible=compressible, force_model=model, force=F)
-    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.4, target=target)
-    assert [f.name for f in step._additional_fields] == ['F'] and step._lattice is None
+    old = os.environ.get('PSAD_LBM_LATTICE')
+    os.environ['PSAD_LBM_LATTICE'] = '1' if schedule == 'lattice' else '0'
+    try:
+        step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.4, target=target)
+    finally:
+        if old is None:
+            os.environ.pop('PSAD_LBM_LATTICE')
+        else:
+            os.environ['PSAD_LBM_LATTICE'] = old
+    assert [f.name for f in step._additional_fields] == ['F']
+    assert (step._lattice is not None) == (schedule == 'lattice')
     op = step.create_timestep_op(T)
     rng = np.random.default_rng(sum(shape))
     f0 = _init(stencil, shape, compressible, seed=9)
@@ -660,12 +676,14 @@ def _force_field_case(stencil, shape, compressible, model, layout, target, T=3):
     return out.detach().cpu(), ref.detach(), x.grad.cpu(), gx, Ft.grad.cpu(), gF
 
 
-@pytest.mark.parametrize('stencil,shape,compressible,model,layout', FIELD_FORCE_CASES)
-def test_lbm_force_field_cpu_vs_oracle(stencil, shape, compressible, model, layout):
-    """A per-cell force field through the timestep op on the C kernels: pdfs after T steps, the pdf adjoint and the
-    force adjoint (summed over the steps) vs the oracle's forced collision with per-cell forces and torch's reverse
-    mode (parity unpinned vs lbmpy, which is absent)."""
-    out, ref, gx, gxr, gF, gFr = _force_field_case(stencil, shape, compressible, model, layout, 'cpu')
+@pytest.mark.parametrize('stencil,shape,compressible,model,layout,schedule', FIELD_FORCE_ALL)
+def test_lbm_force_field_cpu_vs_oracle(stencil, shape, compressible, model, layout, schedule):
+    """A per-cell force field through the timestep op on the C kernels — the lattice kernels (the force read per
+    cell, its adjoint accumulated over the steps in the adjoint kernel) and the rule's AutoDiffOp kernels: pdfs after
+    T steps, the pdf adjoint and the force adjoint (summed over the steps) vs the oracle's forced collision with
+    per-cell forces and torch's reverse mode (parity unpinned vs lbmpy, which is absent)."""
+    out, ref, gx, gxr, gF, gFr = _force_field_case(stencil, shape, compressible, model, layout, 'cpu',
+                                                   schedule=schedule)
     assert float((out - ref).abs().max()) <= 1e-13 * float(ref.abs().max())
     assert float((gx - gxr).abs().max()) <= 1e-12 * float(gxr.abs().max())
     assert float((gF - gFr).abs().max()) <= 1e-12 * float(gFr.abs().max())
@@ -706,10 +724,12 @@ def test_lbm_force_field_end_to_end_and_errors():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('stencil,shape,compressible,model,layout', FIELD_FORCE_CASES)
-def test_lbm_force_field_gpu_vs_oracle(stencil, shape, compressible, model, layout):
-    """The per-cell force field on the HIP kernels (the rule's AutoDiffOp kernels, transposed-mode adjoint)."""
-    out, ref, gx, gxr, gF, gFr = _force_field_case(stencil, shape, compressible, model, layout, 'gpu')
+@pytest.mark.parametrize('stencil,shape,compressible,model,layout,schedule', FIELD_FORCE_ALL)
+def test_lbm_force_field_gpu_vs_oracle(stencil, shape, compressible, model, layout, schedule):
+    """The per-cell force field on the HIP kernels: the lattice kernels (force array read per cell, force adjoint
+    accumulated by the adjoint launches) and the rule's AutoDiffOp kernels (transposed-mode adjoint)."""
+    out, ref, gx, gxr, gF, gFr = _force_field_case(stencil, shape, compressible, model, layout, 'gpu',
+                                                   schedule=schedule)
     assert float((out.double() - ref).abs().max()) <= 1e-12 * float(ref.abs().max())
     assert float((gx.double() - gxr).abs().max()) <= 1e-11 * float(gxr.abs().max())
     assert float((gF.double() - gFr).abs().max()) <= 1e-11 * float(gFr.abs().max())
