@@ -1076,15 +1076,21 @@ def test_full_size_properties(builder, n, tol):
 
 
 def test_full_size_2d_and_readme_op():
-    """BASELINE config 2 at full size (4096² 5-point, every cell vs the oracle) and the README op at
-    16384² (sampled rows vs the closed-form forward / adjoint)."""
+    """BASELINE config 2 at full size (4096² 5-point, every cell vs the oracle, field-scaled AND element-wise) and
+    the README op at 16384² (sampled rows vs the closed-form forward / adjoint, field-scaled and per cell: the fp32
+    evaluation of ``x·log(x·y)`` and its adjoint bounded by a few ulps of each cell's own terms)."""
     op, fn = _op(W.laplace_5pt())
     g = np.random.default_rng(3)
     u = g.uniform(0, 1, (4096, 4096)).astype(np.float32)
     d = g.uniform(-1, 1, (4096, 4096)).astype(np.float32)
     (out,), (du,) = _run(fn, [u], [d])
-    assert_close_rel(out, S.linear_stencil(u, S.taps_laplace_5pt()), 1e-6, 'laplace 4096² out')
-    assert_close_rel(du, S.linear_stencil(d, S.flip(S.taps_laplace_5pt())), 1e-6, 'laplace 4096² diffu')
+    ref_o, ref_d = S.linear_stencil(u, S.taps_laplace_5pt()), S.linear_stencil(d, S.flip(S.taps_laplace_5pt()))
+    assert_close_rel(out, ref_o, 1e-6, 'laplace 4096² out')
+    assert_close_rel(du, ref_d, 1e-6, 'laplace 4096² diffu')
+    absu = S.linear_stencil(np.abs(u), {o: abs(w) for o, w in S.taps_laplace_5pt().items()})
+    absd = S.linear_stencil(np.abs(d), {o: abs(w) for o, w in S.flip(S.taps_laplace_5pt()).items()})
+    assert_cells(out, ref_o, absu, 5, np.float32, 'laplace 4096² out')
+    assert_cells(du, ref_d, absd, 5, np.float32, 'laplace 4096² diffu')
     op, fn = _op(W.readme_op(shape=None), None)
     n = 16384
     gt = torch.Generator(device='cuda').manual_seed(5)
@@ -1095,7 +1101,15 @@ def test_full_size_2d_and_readme_op():
     z.backward(dz)
     for r in (0, 1, n // 2, n - 1):
         xr, yr, dr = (t.detach()[r].cpu().numpy() for t in (x, y, dz))
-        assert_close_rel(z.detach()[r].cpu().numpy(), S.readme_forward(xr, yr), 1e-6, f'z row {r}')
+        z_ref = S.readme_forward(xr, yr)
+        assert_close_rel(z.detach()[r].cpu().numpy(), z_ref, 1e-6, f'z row {r}')
         dx_ref, dy_ref = S.readme_backward(xr, yr, dr)
         assert_close_rel(x.grad[r].cpu().numpy(), dx_ref, 1e-6, f'diffx row {r}')
         assert_close_rel(y.grad[r].cpu().numpy(), dy_ref, 1e-6, f'diffy row {r}')
+        # per cell: the rounding of x·y, log and the products, each a few ulps of the cell's own magnitudes
+        x64, y64, d64 = (np.asarray(a, np.float64) for a in (xr, yr, dr))
+        lg = np.abs(np.log(x64 * y64))
+        assert_cells(z.detach()[r].cpu().numpy(), z_ref, np.abs(x64) * (lg + 1) + np.abs(z_ref), 2, np.float32,
+                     f'z row {r}')
+        assert_cells(x.grad[r].cpu().numpy(), dx_ref, np.abs(d64) * (lg + 2), 2, np.float32, f'diffx row {r}')
+        assert_cells(y.grad[r].cpu().numpy(), dy_ref, 3 * np.abs(dy_ref), 2, np.float32, f'diffy row {r}')
