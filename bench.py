@@ -280,6 +280,19 @@ def run_workload(name, edge, args, world, rank, distributed, extras, warmup=None
 
     fwd_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / len(ev)
     bwd_ms = sum(b.elapsed_time(c) for _, b, c in ev) / len(ev)
+    if os.environ.get('PSAD_BENCH_ADDR'):
+        # where the sweeps' streams sit (probe of the per-process fwd / bwd split): inputs, and the output /
+        # gradient blocks the caching allocator hands the op (the same block every step)
+        (o,) = fn.apply(uu)
+        o.backward(d)
+        torch.cuda.synchronize()
+        print(json.dumps({'workload': name, 'rank': rank, 'u': hex(u.data_ptr()), 'diffout': hex(d.data_ptr()),
+                          'out': hex(o.data_ptr()), 'diffu': hex(uu.grad.data_ptr()), 'fwd_ms': round(fwd_ms, 4),
+                          'bwd_ms': round(bwd_ms, 4),
+                          'fwd_each': [round(a.elapsed_time(b), 4) for a, b, _ in ev],
+                          'bwd_each': [round(b.elapsed_time(c), 4) for _, b, c in ev]}), file=sys.stderr)
+        del o
+        uu.grad = None
     cells_total = n ** 3
     value = cells_total * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3

@@ -75,7 +75,8 @@ class KernelIR:
     compute_dtype: np.dtype
     symbol_names: Dict[sp.Symbol, str] = dc_field(default_factory=dict)
     periodic: bool = False                 # reads / offset writes wrap around, full iteration space
-    islice: Optional[Tuple] = None         # pystencils' iteration_slice: per-axis (start, stop), unit step
+    islice: Optional[Tuple] = None         # pystencils' iteration_slice: per-axis (start, stop)
+    isteps: Optional[Tuple] = None         # ... and its per-axis steps (None: all 1)
 
     @cached_property
     def pointwise(self):
@@ -99,33 +100,39 @@ class KernelIR:
     def iteration_bounds(self, shape):
         """Per-axis [lo, hi) of the cells this kernel writes."""
         if self.islice is not None:
+            # strided slices: [lo, lo + count) numbers the cells the kernel writes, cell k at lo + k·step
             out = []
-            for (a, b), n in zip(self.islice, shape):
-                lo, hi, _ = slice(a, b).indices(int(n))
-                out.append((lo, max(lo, hi)))
+            steps = self.isteps or (1,) * len(self.islice)
+            for (a, b), s, n in zip(self.islice, steps, shape):
+                lo, hi, _ = slice(a, b, s).indices(int(n))
+                out.append((lo, lo + len(range(lo, hi, s))))
             return out
         g = 0 if self.zeros or self.periodic else self.ghost_layers
         return [(g, max(g, int(n) - g)) for n in shape]
 
 
 def normalize_slice(iteration_slice, ndim):
-    """``iteration_slice`` (a slice / int per spatial axis, e.g. ``make_slice[1:-1, 2]``) as ``((start, stop), …)``
-    with unit steps; missing trailing axes are whole."""
+    """``iteration_slice`` (a slice / int per spatial axis, e.g. ``make_slice[1:-1, 2]`` or ``make_slice[::2, 1::3]``)
+    as ``(((start, stop), …), steps or None)``; missing trailing axes are whole. Steps are positive (pystencils'
+    ``create_kernel`` iterates ``start, start + step, … < stop``)."""
     items = iteration_slice if isinstance(iteration_slice, tuple) else (iteration_slice,)
     if len(items) > ndim:
         raise ValueError(f'iteration_slice {iteration_slice} has more axes than the {ndim}-d kernel')
-    out = []
+    out, steps = [], []
     for it in list(items) + [slice(None)] * (ndim - len(items)):
         if isinstance(it, slice):
-            if it.step not in (None, 1):
-                raise NotImplementedError(f'iteration_slice with step {it.step}: unit steps only')
+            step = 1 if it.step is None else int(it.step)
+            if step < 1:
+                raise NotImplementedError(f'iteration_slice with step {it.step}: positive steps only')
             out.append((it.start, it.stop))
+            steps.append(step)
         elif isinstance(it, (int, np.integer)):
             i = int(it)
             out.append((i, i + 1 if i != -1 else None))
+            steps.append(1)
         else:
             raise TypeError(f'iteration_slice entry {it!r}: a slice or an int')
-    return tuple(out)
+    return tuple(out), (tuple(steps) if any(s != 1 for s in steps) else None)
 
 
 def _strip_conditionals(expr):
@@ -306,7 +313,7 @@ class StencilKernel:
             # (absolute cell coordinates, ghost layers ignored); cells outside it are not touched. A read that
             # leaves the domain reads zero here (pystencils reads out of bounds); the one-thread-per-cell schedule
             self.ir = lower(assignments, 'zeros', data_type)
-            self.ir.islice = normalize_slice(iteration_slice, self.ir.ndim)
+            self.ir.islice, self.ir.isteps = normalize_slice(iteration_slice, self.ir.ndim)
         else:
             self.ir = lower(assignments, boundary_handling, data_type)
         self.cpu_openmp = cpu_openmp

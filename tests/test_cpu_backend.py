@@ -270,11 +270,13 @@ def test_create_forward_backward_kernel_like_reference():
 
 @pytest.mark.parametrize('target', ['cpu', pytest.param('gpu', marks=pytest.mark.gpu)])
 @pytest.mark.parametrize('islice', [(slice(1, -1), slice(2, 5)), (slice(0, 3), 4, slice(None)), (-1,),
-                                    (slice(2, 2),)])
+                                    (slice(2, 2),), (slice(0, None, 2),), (slice(1, -1, 3), slice(None), slice(7, 0, 1)),
+                                    (slice(None, None, 2), 3, slice(1, None, 3)), (slice(5, 6, 4), slice(0, 7, 5))])
 def test_create_kernel_iteration_slice(target, islice):
     """create_forward_kernel(iteration_slice=...) like pystencils' create_kernel: only the cells of the slice are
-    written (absolute coordinates, ghost layers ignored), the rest keeps its contents; reads that leave the domain
-    read zeros. CPU (C) and GPU (the one-thread-per-cell HIP schedule)."""
+    written (absolute coordinates, ghost layers ignored, strided slices: every step-th cell from the start), the rest
+    keeps its contents; reads that leave the domain read zeros. CPU (C) and GPU (the one-thread-per-cell HIP
+    schedule)."""
     from pystencils_autodiff_amd.lbm import make_slice  # noqa: F401 (the same make_slice surface)
     op = pa.AutoDiffOp(W.asym_7pt(), boundary_handling='zeros')
     rng = np.random.default_rng(9)
@@ -297,7 +299,7 @@ def test_create_kernel_iteration_slice(target, islice):
     assert np.array_equal(out == 7.0, expect == 7.0) or np.allclose(out, expect, atol=1e-6)
     assert_close_rel(out, expect, 1e-6, f'slice {islice}')
     with pytest.raises(NotImplementedError):
-        op.create_forward_kernel(target, iteration_slice=(slice(0, None, 2),))
+        op.create_forward_kernel(target, iteration_slice=(slice(None, None, -1),))
 
 
 @pytest.mark.parametrize('gl', [1, 2, [(1, 2), 3, (2, 1)], [1, 1, (1, 1)]])
