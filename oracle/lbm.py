@@ -43,9 +43,17 @@ def stream(f, stencil, xp):
     return xp.stack(comps, -1) if xp.__name__ != 'torch' else xp.stack(comps, dim=-1)
 
 
-def collide(f, omega, stencil, compressible, xp, force_model=None, force=None):
-    """SRT collision; ``force_model`` 'simple' (+3 w_i c_i·F) or 'guo' (velocity shifted by F/2, + w_i (1 − ω/2)
-    (3 (c_i − u)·F + 9 (c_i·u)(c_i·F))) with a constant body force ``force`` (lbmpy's published force models)."""
+def trt_odd_rate(omega, magic=3.0 / 16.0):
+    """ω₋ of a TRT method from ω₊ and the magic number Λ = (1/ω₊ − 1/2)(1/ω₋ − 1/2) (lbmpy's published
+    relation, default Λ = 3/16)."""
+    return 1.0 / (magic / (1.0 / omega - 0.5) + 0.5)
+
+
+def collide(f, omega, stencil, compressible, xp, force_model=None, force=None, omega_odd=None):
+    """SRT collision, or TRT with ``omega_odd`` (the antisymmetric part of each population pair (f_i − f_ī)/2
+    relaxes with ω₋, the symmetric part with ω); ``force_model`` 'simple' (+3 w_i c_i·F) or 'guo' (velocity shifted
+    by F/2, + w_i (1 − ω/2) (3 (c_i − u)·F + 9 (c_i·u)(c_i·F))) with a body force ``force`` (lbmpy's published force
+    models)."""
     dirs, w = SETS[stencil]
     D = len(dirs[0])
     rho = f.sum(-1)
@@ -56,12 +64,23 @@ def collide(f, omega, stencil, compressible, xp, force_model=None, force=None):
             m = m + force[a] / 2
         u.append(m / rho if compressible else m)
     usq = sum(ua * ua for ua in u)
-    out = []
+    feqs = []
     for i, c in enumerate(dirs):
         cu = sum(ca * ua for ca, ua in zip(c, u) if ca)
         poly = 3 * cu + 4.5 * cu * cu - 1.5 * usq
-        feq = float(w[i]) * rho * (1 + poly) if compressible else float(w[i]) * (rho + poly)
-        g = f[..., i] + omega * (feq - f[..., i])
+        feqs.append(float(w[i]) * rho * (1 + poly) if compressible else float(w[i]) * (rho + poly))
+    opp = [dirs.index(tuple(-x for x in c)) for c in dirs]
+    out = []
+    for i, c in enumerate(dirs):
+        cu = sum(ca * ua for ca, ua in zip(c, u) if ca)
+        feq = feqs[i]
+        if omega_odd is None:
+            g = f[..., i] + omega * (feq - f[..., i])
+        else:
+            j = opp[i]
+            fs, fa = (f[..., i] + f[..., j]) / 2, (f[..., i] - f[..., j]) / 2
+            es, ea = (feq + feqs[j]) / 2, (feq - feqs[j]) / 2
+            g = f[..., i] - omega * (fs - es) - omega_odd * (fa - ea)
         if force_model is not None:
             cF = sum(ca * Fa for ca, Fa in zip(c, force) if ca)
             if force_model == 'simple':
@@ -73,16 +92,16 @@ def collide(f, omega, stencil, compressible, xp, force_model=None, force=None):
     return xp.stack(out, -1) if xp.__name__ != 'torch' else xp.stack(out, dim=-1)
 
 
-def step(f, omega, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None):
+def step(f, omega, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None, omega_odd=None):
     """One stream-pull-collide time step on a periodic domain (``f``: ``[*spatial, q]``)."""
     if xp is None:
         import numpy as xp
-    return collide(stream(f, stencil, xp), omega, stencil, compressible, xp, force_model, force)
+    return collide(stream(f, stencil, xp), omega, stencil, compressible, xp, force_model, force, omega_odd)
 
 
-def run(f, omega, steps, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None):
+def run(f, omega, steps, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None, omega_odd=None):
     for _ in range(steps):
-        f = step(f, omega, stencil, compressible, xp, force_model, force)
+        f = step(f, omega, stencil, compressible, xp, force_model, force, omega_odd)
     return f
 
 
@@ -127,19 +146,21 @@ def stream_walls(f, stencil, wall, xp):
     return xp.stack(comps, -1) if xp.__name__ != 'torch' else xp.stack(comps, dim=-1)
 
 
-def step_walls(f, omega, wall, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None):
+def step_walls(f, omega, wall, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None,
+               omega_odd=None):
     """One stream-pull-collide step with no-slip obstacles (and optionally a body force on the fluid cells, as
     ``collide``); obstacle cells keep their state."""
     if xp is None:
         import numpy as xp
-    new = collide(stream_walls(f, stencil, wall, xp), omega, stencil, compressible, xp, force_model, force)
+    new = collide(stream_walls(f, stencil, wall, xp), omega, stencil, compressible, xp, force_model, force, omega_odd)
     keep = wall[..., None] if xp.__name__ != 'torch' else wall.unsqueeze(-1)
     return xp.where(keep, f, new)
 
 
-def run_walls(f, omega, wall, steps, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None):
+def run_walls(f, omega, wall, steps, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None,
+              omega_odd=None):
     for _ in range(steps):
-        f = step_walls(f, omega, wall, stencil, compressible, xp, force_model, force)
+        f = step_walls(f, omega, wall, stencil, compressible, xp, force_model, force, omega_odd)
     return f
 
 

@@ -444,7 +444,7 @@ class AutoDiffOp:
         """``ps.create_kernel(assignments, *args, **kwargs).compile()`` (``_autodiff.py:592-598``): a
         compiled kernel of this op's forward / backward assignments with pystencils' defaults — interior
         only unless ``ghost_layers=0`` (then out-of-domain reads are zeros, the only defined meaning);
-        ``iteration_slice`` (unit-step slices / ints per axis, absolute coordinates) restricts the cells written,
+        ``iteration_slice`` (slices — strided too — / ints per axis, absolute coordinates) restricts the cells written,
         as in pystencils (ghost layers are then ignored; reads leaving the domain read zeros)."""
         from .backends.kernel_ir import StencilKernel
         ac = self._forward_assignments if which == 'forward' else self._backward_assignments

@@ -211,10 +211,20 @@ class AutoDiffLatticeBoltzmannStep:
                 if force is None or all(sp.sympify(v).is_number for v in force) else None
         extras_ok = not self._additional_fields or (self._force_field is not None and
                                                     self._additional_fields == [self._force_field])
+        # TRT: the odd rate from the magic number (a function of the ω argument) or a constant
+        self._lattice_trt = None
+        trt_ok = True
+        if getattr(update_rule, 'method', 'srt') == 'trt':
+            if getattr(update_rule, 'magic_number', None) is not None:
+                self._lattice_trt = ('magic', float(update_rule.magic_number))
+            elif sp.sympify(update_rule.relaxation_rate_odd).is_number:
+                self._lattice_trt = ('rate', float(update_rule.relaxation_rate_odd))
+            else:
+                trt_ok = False                      # a symbolic odd rate: the AutoDiffOp kernels
         self._lattice = {} if (getattr(update_rule, 'stencil', None) is not None and not time_constant_fields
                                and self._lattice_force is not None
                                and os.environ.get('PSAD_LBM_LATTICE', '1') != '0'
-                               and extras_ok and self._omega_of is not None
+                               and extras_ok and trt_ok and self._omega_of is not None
                                and np.dtype(src.dtype.numpy_dtype) in (np.float32, np.float64)
                                and (self._force_field is None or
                                     self._force_field.dtype.numpy_dtype == src.dtype.numpy_dtype)) else None
@@ -410,7 +420,8 @@ class AutoDiffLatticeBoltzmannStep:
         if k is None:
             k = self._lattice[(walls, links)] = LatticeKernels(
                 self.method, getattr(self._update_rule, 'compressible', False), self.pdf_field.dtype.numpy_dtype,
-                walls, self._target, links, *self._lattice_force, force_field=self._force_field is not None)
+                walls, self._target, links, *self._lattice_force, force_field=self._force_field is not None,
+                trt=self._lattice_trt)
         return k
 
     # -- kernels -----------------------------------------------------------------------------------

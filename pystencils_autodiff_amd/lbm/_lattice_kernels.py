@@ -45,7 +45,7 @@ SELF_BIT = 30      # bit of a cell's neighbour mask: the cell itself is an obsta
 
 
 def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=None, force_model=None, force=None,
-          force_field=False):
+          force_field=False, trt=None):
     """Source of the forward (``lbm_fwd``) and adjoint (``lbm_adj``) kernels.
 
     ``addr='buf'`` (HIP): every pdf array is one buffer resource (its bytes below 2³²); a component's plane
@@ -66,7 +66,11 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     adjoint ACCUMULATES the force adjoint into ``dforce`` (same strides; every cell by one thread, so the T steps of
     the time-step op sum into one zeroed array): 'simple' ``dF_a = 3 Σ_i g_i w_i c_ia``; 'guo' — through the explicit
     term and the velocity shift ``∂u_a/∂F_a = 1/2 (/ρ)`` — ``dF_a = (1 − ω/2) Bf_a + ω B_a / 2 (/ρ)`` with ``Bf_a`` the
-    equilibrium part of the velocity sensitivity (before the ρ scaling) and ``B_a`` the full one."""
+    equilibrium part of the velocity sensitivity (before the ρ scaling) and ``B_a`` the full one.
+    ``trt``: the TRT method (``_method.create_lb_update_rule(method='trt')``): ``('magic', Λ)`` (ω₋ from ω and the
+    magic number, computed per launch from the ω argument) or ``('rate', ω₋)`` (a constant). With a = (ω₊ + ω₋)/2,
+    b = (ω₊ − ω₋)/2 the collision is ``dst_i = (1 − a) f_i − b f_ī + a feq_i + b feq_ī`` and the adjoint takes the
+    equilibrium sums over h_i = a g_i + b g_ī: ``v_j = (1 − a) g_j − b g_ĵ + A_h + Σ_a B_h,a ∂u_a/∂f_j``."""
     D, Q = stencil.D, stencil.Q
     dirs = [tuple(d) for d in stencil.directions]
     w = [float(x) for x in stencil.weights]
@@ -75,6 +79,8 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     F = [float(v) for v in force] if fm and not ff else None
     cF = [sum(c * f for c, f in zip(d, F)) for d in dirs] if fm and not ff else None
     inv = [stencil.inverse_direction_index(i) for i in range(Q)]
+    if trt is not None and fm == 'guo':
+        raise NotImplementedError('TRT lattice kernels with the Guo force model')
     axes = ['z', 'y', 'x'][3 - D:]          # spatial axes, axis 0 slowest; x fastest
     ct = ctype
     hip = target == 'hip'
@@ -232,6 +238,14 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         if fm == 'guo':
             L.append(f'  const {ct} uF = ' + ' + '.join(f'u{a} * {Fa(a)}' for a in range(D)) + ';')
             L.append(f'  const {ct} kg = ({ct})1 - ({ct})0.5 * omega;')
+        if trt is not None:
+            if trt[0] == 'magic':
+                lam = c_(trt[1])
+                wo = f'(({ct})4 - ({ct})2 * omega) / (({ct})4 * {lam} * omega + ({ct})2 - omega)'
+            else:
+                wo = c_(trt[1])
+            L.append(f'  const {ct} w_odd = {wo};')
+            L.append(f'  const {ct} ta = ({ct})0.5 * (omega + w_odd), tb = ({ct})0.5 * (omega - w_odd);')
 
     def cu_expr(i):
         t = [('+ ' if dirs[i][a] > 0 else '- ') + f'u{a}' for a in range(D) if dirs[i][a]]
@@ -280,6 +294,14 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     force_loads(L)
     pull_loads(L, 's', 'src')
     moments(L)
+    if trt is not None:
+        # TRT: every population's equilibrium first (the collision of i reads feq of ī too)
+        for i in range(Q):
+            L.append(f'  {ct} fe{i};')
+            L.append(f'  {{ const {ct} cu = {cu_expr(i)};')
+            L.append(f'    const {ct} poly = cu * (({ct})3 + ({ct})4.5 * cu) - ({ct})1.5 * usq;')
+            L.append(f'    fe{i} = ' + (f'{c_(w[i])} * rho * (({ct})1 + poly);' if compressible
+                                        else f'{c_(w[i])} * (rho + poly);') + ' }')
     for i in range(Q):
         L.append(f'  {{ const {ct} cu = {cu_expr(i)};')
         L.append(f'    const {ct} poly = cu * (({ct})3 + ({ct})4.5 * cu) - ({ct})1.5 * usq;')
@@ -290,7 +312,13 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         elif fm == 'guo':
             term = (f' + {c_(w[i])} * kg * (({ct})3 * ({cFi(i) or c_(0)} - uF)'
                     + (f' + {cFi(i, 9)} * cu' if cFi(i) else '') + ')')
-        L.append('    ' + store('d', 'dst', i, dcoff, f'f{i} + omega * ({feq} - f{i}){term}') + ' }')
+        if trt is not None:
+            j = inv[i]
+            val = (f'(({ct})1 - ta) * f{i} - tb * f{j} + ta * fe{i} + tb * fe{j}{term}' if j != i else
+                   f'f{i} + omega * (fe{i} - f{i}){term}')
+        else:
+            val = f'f{i} + omega * ({feq} - f{i}){term}'
+        L.append('    ' + store('d', 'dst', i, dcoff, val) + ' }')
     L.append('}')
 
     # ---- adjoint (scatter to where the forward pulled from)
@@ -326,7 +354,12 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             L.append(f'  {ct} M{a} = 0;')           # Σ_i g_i w_i c_ia (the 'simple' force adjoint / 3)
     for i in range(Q):
         L.append(f'  {{ const {ct} cu = {cu_expr(i)};')
-        L.append(f'    const {ct} gw = g{i} * {c_(w[i])};')
+        if trt is not None:
+            # the equilibrium sums over h_i = a g_i + b g_ī (rest population: ω g_0)
+            hi = f'(ta * g{i} + tb * g{inv[i]})' if inv[i] != i else f'omega * g{i}'
+            L.append(f'    const {ct} gw = {hi} * {c_(w[i])};')
+        else:
+            L.append(f'    const {ct} gw = g{i} * {c_(w[i])};')
         L.append('    S += gw;')
         if compressible:
             L.append(f'    A += gw * (({ct})1 + cu * (({ct})3 + ({ct})4.5 * cu) - ({ct})1.5 * usq);')
@@ -341,9 +374,10 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                     if dirs[i][a]:
                         L.append(f'    E{a} {"+" if dirs[i][a] > 0 else "-"}= tf;')
             if ff and fm == 'simple':
+                gwm = f'(g{i} * {c_(w[i])})' if trt is not None else 'gw'
                 for a in range(D):
                     if dirs[i][a]:
-                        L.append(f'    M{a} {"+" if dirs[i][a] > 0 else "-"}= gw;')
+                        L.append(f'    M{a} {"+" if dirs[i][a] > 0 else "-"}= {gwm};')
         L.append('  }')
     if not compressible:
         L.append('  A = S;')
@@ -371,8 +405,13 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         cbs = ' '.join(cb)
         cbs = (cbs[2:] if cbs.startswith('+ ') else cbs) if cb else f'({ct})0'
         du = f'(({cbs}) - Bu) * irho' if compressible else f'({cbs})'
-        L.append(f'  {{ {"" if links is not None and walls and any(dirs[j]) else "const "}{ct} v = (({ct})1 - omega) '
-                 f'* g{j} + omega * (A + {du});')
+        vq = "" if links is not None and walls and any(dirs[j]) else "const "
+        if trt is not None and inv[j] != j:
+            L.append(f'  {{ {vq}{ct} v = (({ct})1 - ta) * g{j} - tb * g{inv[j]} + (A + {du});')
+        elif trt is not None:
+            L.append(f'  {{ {vq}{ct} v = (({ct})1 - omega) * g{j} + (A + {du});')
+        else:
+            L.append(f'  {{ {vq}{ct} v = (({ct})1 - omega) * g{j} + omega * (A + {du});')
         k = key(dirs[j])
         if walls and any(dirs[j]) and links is not None:
             L.append(f'    if ((msk >> {j}) & 1u) v *= lk_g[id{j} * {Q} + {j}];')
@@ -487,8 +526,9 @@ class LatticeKernels:
     bounce-back)."""
 
     def __init__(self, stencil, compressible, dtype, walls, target, links=None, force_model=None, force=None,
-                 force_field=False):
+                 force_field=False, trt=None):
         self.stencil = stencil
+        self.trt = None if trt is None else (str(trt[0]), float(trt[1]))
         self.force_model = force_model
         self.force_field = bool(force_model) and bool(force_field)
         self.force = None if force_model is None or self.force_field else tuple(float(v) for v in force)
@@ -506,9 +546,9 @@ class LatticeKernels:
     def source(self, idx='int', addr='buf'):
         if self.target != 'gpu':
             return _emit(self.stencil, self.compressible, self.ct, self.walls, 'c', 'i64', 'ptr', self.links,
-                         self.force_model, self.force, self.force_field)
+                         self.force_model, self.force, self.force_field, self.trt)
         return _emit(self.stencil, self.compressible, self.ct, self.walls, 'hip', idx, addr, self.links,
-                     self.force_model, self.force, self.force_field)
+                     self.force_model, self.force, self.force_field, self.trt)
 
     # -- GPU ---------------------------------------------------------------------------------------
     def _gpu_fn(self, which, idx, addr, device):

@@ -26,7 +26,7 @@ import sympy as sp
 from .. import ps
 
 __all__ = ['LBStencil', 'create_lb_update_rule', 'create_lb_adjoint_rule', 'macroscopic_getter',
-           'equilibrium_setter']
+           'equilibrium_setter', 'relaxation_rate_from_magic_number']
 
 
 class LBStencil:
@@ -136,32 +136,70 @@ def _feq(stencil, i, rho, us, compressible):
     return w * rho * (1 + poly) if compressible else w * (rho + poly)
 
 
+def relaxation_rate_from_magic_number(relaxation_rate, magic_number=sp.Rational(3, 16)):
+    """The odd-moment rate of a TRT method from the even one and the magic number
+    Λ = (1/ω₊ − 1/2)(1/ω₋ − 1/2) (lbmpy ``relaxation_rate_from_magic_number`` [ext], default Λ = 3/16)."""
+    w = sp.sympify(relaxation_rate)
+    lam = sp.sympify(magic_number)
+    return (4 - 2 * w) / (4 * lam * w + 2 - w)
+
+
+METHODS = ('srt', 'trt')
+
+
 def create_lb_update_rule(stencil='D2Q9', relaxation_rate=None, compressible=False, src_field=None, dst_field=None,
                           data_type='float64', layout='fzyx', kernel_type='stream_pull_collide', force_model=None,
-                          force=None):
-    """SRT (BGK) ``stream_pull_collide`` update rule (lbmpy ``create_lb_update_rule(stencil=…, method='srt',
-    relaxation_rate=…, compressible=…, kernel_type='stream_pull_collide')`` [ext]). ``relaxation_rate`` =
-    ω: a number, or a sympy symbol left as a kernel parameter (default: the symbol ``omega``). Fields:
-    ``src(q)``/``dst(q)`` vector fields in ``layout`` (``'fzyx'``: components slowest, lbmpy's default)
-    unless given. ``force_model`` ('simple' or 'guo') with ``force``: a body force — constant (numbers or symbols per
-    axis) or per cell (a vector field of D components: an additional input of the rule, its adjoint accumulated over
-    the steps) — such rules run on the rule's own AutoDiffOp kernels, not the lattice schedule."""
+                          force=None, method='srt', relaxation_rates=None, magic_number=sp.Rational(3, 16)):
+    """SRT (BGK) or TRT ``stream_pull_collide`` update rule (lbmpy ``create_lb_update_rule(stencil=…,
+    method='srt' | 'trt', relaxation_rate=…, compressible=…, kernel_type='stream_pull_collide')`` [ext]).
+    ``relaxation_rate`` = ω: a number, or a sympy symbol left as a kernel parameter (default: the symbol ``omega``).
+    TRT relaxes the symmetric part of each population pair (f_i + f_ī)/2 with ω (= ω₊, the shear rate) and the
+    antisymmetric part with ω₋ — ``relaxation_rates=[ω₊, ω₋]``, or ω₋ from the magic number Λ
+    (``relaxation_rate_from_magic_number``, lbmpy's default 3/16):
+
+        dst_i = f_i − ω₊ (f_i⁺ − feq_i⁺) − ω₋ (f_i⁻ − feq_i⁻),   x_i^± = (x_i ± x_ī) / 2.
+
+    Fields: ``src(q)``/``dst(q)`` vector fields in ``layout`` (``'fzyx'``: components slowest, lbmpy's default)
+    unless given. ``force_model`` ('simple' or 'guo'; TRT: 'simple') with ``force``: a body force — constant (numbers
+    or symbols per axis) or per cell (a vector field of D components: an additional input of the rule, its adjoint
+    accumulated over the steps)."""
     if kernel_type != 'stream_pull_collide':
         raise NotImplementedError("only kernel_type='stream_pull_collide' is restated")
+    method = str(method).lower()
+    if method not in METHODS:
+        raise NotImplementedError(f"method '{method}': one of {METHODS} is restated (lbmpy's MRT / cumulant methods "
+                                  'are not)')
     st = stencil if isinstance(stencil, LBStencil) else LBStencil(stencil)
     if src_field is None or dst_field is None:
         src_field, dst_field = ps.fields(f"src({st.Q}), dst({st.Q}): {data_type}[{st.D}D]", layout=layout)
+    if relaxation_rates is not None:
+        if method != 'trt' or len(relaxation_rates) != 2:
+            raise ValueError('relaxation_rates: [even, odd] for the TRT method')
+        relaxation_rate = relaxation_rates[0]
     omega = sp.Symbol('omega') if relaxation_rate is None else sp.sympify(relaxation_rate)
     f = [src_field[tuple(-c for c in st.directions[i])](i) for i in range(st.Q)]
+    if method == 'trt' and force_model is not None and str(force_model).lower() != 'simple':
+        raise NotImplementedError("TRT with force_model 'guo' (its prefactor per moment) is not restated: 'simple'")
     shift, term = _force(force_model, force, st)
     rho, us, subs = _moments(st, f, compressible, shift)
-    main = [ps.Assignment(dst_field.center(i), f[i] + omega * (_feq(st, i, rho, us, compressible) - f[i]) +
-                          (term(i, us, omega) if term else 0))
-            for i in range(st.Q)]
+    feq = [_feq(st, i, rho, us, compressible) for i in range(st.Q)]
+    if method == 'srt':
+        omega_odd = None
+        coll = [f[i] + omega * (feq[i] - f[i]) for i in range(st.Q)]
+    else:
+        omega_odd = sp.sympify(relaxation_rates[1]) if relaxation_rates is not None else \
+            relaxation_rate_from_magic_number(omega, magic_number)
+        inv = [st.inverse_direction_index(i) for i in range(st.Q)]
+        coll = [f[i] - omega * ((f[i] + f[inv[i]]) / 2 - (feq[i] + feq[inv[i]]) / 2)
+                - omega_odd * ((f[i] - f[inv[i]]) / 2 - (feq[i] - feq[inv[i]]) / 2) for i in range(st.Q)]
+    main = [ps.Assignment(dst_field.center(i), coll[i] + (term(i, us, omega) if term else 0)) for i in range(st.Q)]
     ac = ps.AssignmentCollection(main, subs)
     ac.stencil = st
     ac.compressible = compressible
     ac.relaxation_rate = omega
+    ac.method = method
+    ac.relaxation_rate_odd = omega_odd
+    ac.magic_number = sp.sympify(magic_number) if method == 'trt' and relaxation_rates is None else None
     ac.force_model = None if force_model is None else str(force_model).lower()
     ac.force = None if force is None else tuple(force_components(force, st.D))
     return ac
@@ -177,10 +215,13 @@ def create_lb_adjoint_rule(update_rule, diff_fields_prefix='diff'):
         ∂u_a/∂f_j = (c_ja − u_a)/ρ  (compressible)   or   c_ja  (incompressible)
 
     — O(q·d) arithmetic per cell instead of O(q²). For a fixed component j the map y ↦ y − c_j is a
-    bijection of the (periodic) lattice, so every (j, cell) of diffsrc is written exactly once."""
+    bijection of the (periodic) lattice, so every (j, cell) of diffsrc is written exactly once. TRT
+    (dst_i = (1 − a) f_i − b f_ī + a feq_i + b feq_ī, a = (ω₊ + ω₋)/2, b = (ω₊ − ω₋)/2): the same sums over
+    h_i = a g_i + b g_ī, and diffsrc_j(y − c_j) = (1 − a) g_j − b g_ĵ + A_h + Σ_a B_h,a ∂u_a/∂f_j."""
     st = update_rule.stencil
     comp = update_rule.compressible
     omega = update_rule.relaxation_rate
+    trt = getattr(update_rule, 'method', 'srt') == 'trt'
     src = update_rule.free_fields
     dst = update_rule.bound_fields
     (src,), (dst,) = tuple(src), tuple(dst)
@@ -192,16 +233,28 @@ def create_lb_adjoint_rule(update_rule, diff_fields_prefix='diff'):
     feq = [_feq(st, i, rho, us, comp) for i in range(st.Q)]
     A = sp.Symbol('adj_rho')
     B = sp.symbols(f'adj_u_:{st.D}')
-    subs.append(ps.Assignment(A, sum(gi * sp.diff(fe, rho) for gi, fe in zip(g, feq))))
+    if trt:
+        opp = [st.inverse_direction_index(i) for i in range(st.Q)]
+        ka, kb = sp.Symbol('trt_a'), sp.Symbol('trt_b')
+        subs += [ps.Assignment(ka, (omega + update_rule.relaxation_rate_odd) / 2),
+                 ps.Assignment(kb, (omega - update_rule.relaxation_rate_odd) / 2)]
+        h = [ka * g[i] + kb * g[opp[i]] for i in range(st.Q)]
+    else:
+        h = g
+    subs.append(ps.Assignment(A, sum(gi * sp.diff(fe, rho) for gi, fe in zip(h, feq))))
     for a in range(st.D):
-        subs.append(ps.Assignment(B[a], sum(gi * sp.diff(fe, us[a]) for gi, fe in zip(g, feq))))
+        subs.append(ps.Assignment(B[a], sum(gi * sp.diff(fe, us[a]) for gi, fe in zip(h, feq))))
     if comp:
         inv = sp.Symbol('inv_rho')
         subs.append(ps.Assignment(inv, 1 / rho))
     main = []
     for j, c in enumerate(st.directions):
         du = [(c[a] - us[a]) * inv if comp else c[a] for a in range(st.D)]
-        rhs = (1 - omega) * g[j] + omega * (A + sum(B[a] * du[a] for a in range(st.D) if du[a] != 0))
+        eq = A + sum(B[a] * du[a] for a in range(st.D) if du[a] != 0)
+        if trt:
+            rhs = (1 - ka) * g[j] - kb * g[opp[j]] + eq
+        else:
+            rhs = (1 - omega) * g[j] + omega * eq
         main.append(ps.Assignment(dsrc[tuple(-ci for ci in c)](j), rhs))
     return ps.AssignmentCollection(main, subs)
 

@@ -781,3 +781,137 @@ def test_lbm_force_driven_channel(target, model, compressible):
         prof = F[1] * y * (H - y) / (2 * nu)
         inner = slice(1, shape[0] - 1)
         assert np.abs(u1[inner].mean(1) - prof[inner]).max() <= 0.03 * prof[inner].max()
+
+
+# ------------------------------------------------------------------------------------------------------ TRT method
+# create_lb_update_rule(method='trt'): lbmpy's two-relaxation-time method restated (parity unpinned vs lbmpy, absent);
+# checked against the oracle's TRT collision (oracle/lbm.py collide(omega_odd=…)) and torch's reverse mode through it
+TRT_CASES = [('D2Q9', (9, 7), True, 'magic', 'fzyx', False), ('D2Q9', (8, 6), False, 'rate', 'numpy', True),
+             ('D3Q19', (5, 4, 6), True, 'rate', 'fzyx', True), ('D3Q19', (4, 5, 4), False, 'magic', 'numpy', False)]
+
+
+def _trt_case(stencil, shape, compressible, odd, layout, walls, target, schedule, force=None):
+    import os
+    rr = 1.4
+    kw = dict(relaxation_rates=[rr, 1.1]) if odd == 'rate' else {}
+    rule = lbm.create_lb_update_rule(stencil, compressible=compressible, layout=layout, method='trt',
+                                     force_model='simple' if force else None, force=force, **kw)
+    old = os.environ.get('PSAD_LBM_LATTICE')
+    os.environ['PSAD_LBM_LATTICE'] = '1' if schedule == 'lattice' else '0'
+    try:
+        step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=rr, target=target)
+    finally:
+        if old is None:
+            os.environ.pop('PSAD_LBM_LATTICE')
+        else:
+            os.environ['PSAD_LBM_LATTICE'] = old
+    assert (step._lattice is not None) == (schedule == 'lattice')
+    w_odd = 1.1 if odd == 'rate' else OL.trt_odd_rate(rr)
+    wall = None
+    if walls:
+        _set_channel(step, shape)
+        wall = _channel(shape)
+    return step, rr, w_odd, wall
+
+
+@pytest.mark.parametrize('schedule', ['lattice', 'autodiffop'])
+@pytest.mark.parametrize('stencil,shape,compressible,odd,layout,walls', TRT_CASES)
+def test_lbm_trt_cpu_vs_oracle(stencil, shape, compressible, odd, layout, walls, schedule):
+    """TRT (ω₋ from lbmpy's magic number 3/16, or given): T steps and the adjoint of T steps on the C kernels (the
+    lattice kernels, or the rule's AutoDiffOp kernels with the structured TRT adjoint) vs the oracle and torch's
+    reverse mode, periodic and with no-slip walls."""
+    import torch
+    if schedule == 'autodiffop' and walls:
+        pytest.skip('walls need the lattice schedule')
+    step, rr, w_odd, wall = _trt_case(stencil, shape, compressible, odd, layout, walls, 'cpu', schedule)
+    f0 = _init(stencil, shape, compressible, seed=4)
+    T = 3
+    step.set_pdfs(f0)
+    step.run(T, record=True)
+    ft = torch.tensor(f0, requires_grad=True)
+    ref = (OL.run_walls(ft, rr, torch.tensor(wall), T, stencil, compressible, xp=torch, omega_odd=w_odd) if walls else
+           OL.run(ft, rr, T, stencil, compressible, xp=torch, omega_odd=w_odd))
+    srt = OL.run(torch.tensor(f0), rr, T, stencil, compressible, xp=torch)
+    assert float((ref.detach() - srt).abs().max()) > 1e-6            # TRT is not SRT here
+    assert np.abs(step.pdf_array - ref.detach().numpy()).max() <= 1e-13 * np.abs(f0).max()
+    g = np.random.default_rng(5).standard_normal(f0.shape)
+    (gref,) = torch.autograd.grad(ref, ft, torch.tensor(g))
+    step.set_adjoint_pdfs(g)
+    step.run_backward(T)
+    assert np.abs(step.adjoint_pdf_array - gref.numpy()).max() <= 1e-12 * np.abs(gref.numpy()).max()
+
+
+def test_lbm_trt_rule_api():
+    """The TRT rule: ω₊ = ω₋ is SRT; lbmpy's magic-number relation; the odd rate as a kernel symbol runs on the
+    AutoDiffOp kernels; unsupported combinations raise."""
+    import sympy as sp
+    w = sp.Symbol('omega')
+    wo = lbm.relaxation_rate_from_magic_number(w)
+    lam = sp.simplify((1 / w - sp.Rational(1, 2)) * (1 / wo - sp.Rational(1, 2)))
+    assert lam == sp.Rational(3, 16)
+    assert abs(float(wo.subs(w, 1.4)) - OL.trt_odd_rate(1.4)) < 1e-14
+    rule = lbm.create_lb_update_rule('D2Q9', method='trt', relaxation_rates=[1.3, 1.3])
+    srt = lbm.create_lb_update_rule('D2Q9', relaxation_rate=1.3)
+    for a, b in zip(rule.main_assignments, srt.main_assignments):
+        assert sp.simplify(a.rhs - b.rhs) == 0
+    sym = lbm.create_lb_update_rule('D2Q9', method='trt', relaxation_rates=[w, sp.Symbol('omega_odd')])
+    step = lbm.AutoDiffLatticeBoltzmannStep(sym, domain_size=(6, 5), kernel_params={'omega': 1.2, 'omega_odd': 1.0},
+                                            target='cpu')
+    assert step._lattice is None
+    with pytest.raises(NotImplementedError):
+        lbm.create_lb_update_rule('D2Q9', method='mrt')
+    with pytest.raises(NotImplementedError):
+        lbm.create_lb_update_rule('D2Q9', method='trt', force_model='guo', force=(1e-3, 0))
+    with pytest.raises(ValueError):
+        lbm.create_lb_update_rule('D2Q9', relaxation_rates=[1.2, 1.1])
+
+
+def test_lbm_trt_force_field_cpu():
+    """TRT with a per-cell 'simple' force field on the lattice kernels: pdfs, pdf adjoint and force adjoint vs the
+    oracle and torch's reverse mode."""
+    import torch
+    shape, D, T = (7, 8), 2, 3
+    F = ps.fields(f"F({D}): float64[{D}D]")
+    step, rr, w_odd, _ = _trt_case('D2Q9', shape, True, 'magic', 'fzyx', False, 'cpu', 'lattice', force=F)
+    op = step.create_timestep_op(T)
+    rng = np.random.default_rng(2)
+    f0 = _init('D2Q9', shape, True, seed=3)
+    Fv = 1e-3 * rng.standard_normal(shape + (D,))
+    x, Ft = torch.tensor(f0, requires_grad=True), torch.tensor(Fv, requires_grad=True)
+    out = op.apply(x, Ft)
+    ft, Fr = torch.tensor(f0, requires_grad=True), torch.tensor(Fv, requires_grad=True)
+    ref = OL.run(ft, rr, T, 'D2Q9', True, xp=torch, force_model='simple', force=tuple(Fr[..., a] for a in range(D)),
+                 omega_odd=w_odd)
+    assert float((out - ref).detach().abs().max()) <= 1e-13 * float(ref.detach().abs().max())
+    g = torch.tensor(rng.standard_normal(f0.shape))
+    out.backward(g)
+    gx, gF = torch.autograd.grad(ref, (ft, Fr), g)
+    assert float((x.grad - gx).abs().max()) <= 1e-12 * float(gx.abs().max())
+    assert float((Ft.grad - gF).abs().max()) <= 1e-12 * float(gF.abs().max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('schedule', ['lattice', 'autodiffop'])
+@pytest.mark.parametrize('stencil,shape,compressible,odd,layout,walls', TRT_CASES)
+def test_lbm_trt_gpu_vs_oracle(stencil, shape, compressible, odd, layout, walls, schedule):
+    """TRT on the HIP kernels (lattice kernels and the rule's AutoDiffOp kernels) vs the oracle and torch's reverse
+    mode."""
+    import torch
+    if schedule == 'autodiffop' and walls:
+        pytest.skip('walls need the lattice schedule')
+    step, rr, w_odd, wall = _trt_case(stencil, shape, compressible, odd, layout, walls, 'gpu', schedule)
+    f0 = _init(stencil, shape, compressible, seed=4)
+    T = 3
+    step.set_pdfs(torch.tensor(f0, device='cuda'))
+    step.run(T, record=True)
+    ft = torch.tensor(f0, requires_grad=True)
+    ref = (OL.run_walls(ft, rr, torch.tensor(wall), T, stencil, compressible, xp=torch, omega_odd=w_odd) if walls else
+           OL.run(ft, rr, T, stencil, compressible, xp=torch, omega_odd=w_odd))
+    got = step.pdf_array.double().cpu().numpy()
+    assert np.abs(got - ref.detach().numpy()).max() <= 1e-12 * np.abs(f0).max()
+    g = np.random.default_rng(5).standard_normal(f0.shape)
+    (gref,) = torch.autograd.grad(ref, ft, torch.tensor(g))
+    step.set_adjoint_pdfs(torch.tensor(g, device='cuda'))
+    step.run_backward(T)
+    gg = step.adjoint_pdf_array.double().cpu().numpy()
+    assert np.abs(gg - gref.numpy()).max() <= 1e-11 * np.abs(gref.numpy()).max()
