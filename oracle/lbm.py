@@ -164,30 +164,35 @@ def run_walls(f, omega, wall, steps, stencil='D2Q9', compressible=False, xp=None
     return f
 
 
-def stream_moving_walls(f, stencil, wall, wall_velocity, xp):
+def stream_moving_walls(f, stencil, wall, wall_velocity, xp, density_weighted=False):
     """Pull streaming with bounce-back at wall cells that may move (lbmpy's ``UBB`` [ext], ``NoSlip`` where the
     velocity is 0): where ``x − c_i`` is a wall cell with velocity ``u_w``, ``f_i(x) = f_ī(x) + 6 w_i (c_i · u_w)``
     (the population that left ``x`` towards the wall, reflected with the wall's momentum: 2/c_s² = 6), else
     ``f_i(x − c_i)`` (periodic). ``wall_velocity``: ``[*spatial, d]`` (axis-0 component first; only read at wall
-    cells)."""
+    cells). ``density_weighted``: the wall term times the fluid cell's density Σ_k f_k(x) (lbmpy's compressible UBB)."""
     dirs, w = SETS[stencil]
     inv = inverse(stencil)
+    rho = f.sum(-1)
     comps = []
     for i, c in enumerate(dirs):
         pulled = _roll_all(xp, f[..., i], c)
         nb_wall = _roll_all(xp, wall, c)
         cu = sum(ca * _roll_all(xp, wall_velocity[..., a], c) for a, ca in enumerate(c) if ca)
+        if density_weighted and any(c):
+            cu = cu * rho
         bounced = f[..., inv[i]] + 6 * float(w[i]) * cu if any(c) else f[..., inv[i]]
         comps.append(xp.where(nb_wall, bounced, pulled))
     return xp.stack(comps, -1) if xp.__name__ != 'torch' else xp.stack(comps, dim=-1)
 
 
-def run_moving_walls(f, omega, wall, wall_velocity, steps, stencil='D2Q9', compressible=False, xp=None):
+def run_moving_walls(f, omega, wall, wall_velocity, steps, stencil='D2Q9', compressible=False, xp=None,
+                     density_weighted=False, omega_odd=None):
     """``steps`` stream-pull-collide steps with (moving) bounce-back walls; wall cells keep their state."""
     if xp is None:
         import numpy as xp
     keep = wall[..., None] if xp.__name__ != 'torch' else wall.unsqueeze(-1)
     for _ in range(steps):
-        new = collide(stream_moving_walls(f, stencil, wall, wall_velocity, xp), omega, stencil, compressible, xp)
+        new = collide(stream_moving_walls(f, stencil, wall, wall_velocity, xp, density_weighted), omega, stencil,
+                      compressible, xp, omega_odd=omega_odd)
         f = xp.where(keep, f, new)
     return f

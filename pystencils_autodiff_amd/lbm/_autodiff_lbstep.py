@@ -71,6 +71,9 @@ def _lattice_sweeps(step, which, launches, force=None, dforce=None):
     if force is not None:
         mptr += (force.data_ptr(),) + ((dforce.data_ptr(),) if which == 'adj' else ())
     stream = _torch()._C._cuda_getCurrentRawStream(launches[0][0].device.index)
+    rho = K.rho_buffer(launches[0][0]) if which == 'adj' and K.rho_links else None
+    if rho is not None:
+        mptr += (rho.data_ptr(),)
     plans = {}
     for ts in launches:
         sig = tuple(t.stride() for t in ts)
@@ -78,6 +81,9 @@ def _lattice_sweeps(step, which, launches, force=None, dforce=None):
         if plan is None:
             plan = plans[sig] = K.plan(which, list(ts), mask, om, ids, force, dforce if which == 'adj' else None)
         plan(tuple(t.data_ptr() for t in ts) + mptr, stream, om)
+        if rho is not None:
+            # the density pass of the density-weighted walls, on this launch's output
+            K.rho_plan(ts[2], mask, rho)((ts[2].data_ptr(), mask.data_ptr(), rho.data_ptr()), stream)
 
 
 def _plain_force_field(force, D):

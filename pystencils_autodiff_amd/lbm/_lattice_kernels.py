@@ -93,14 +93,20 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     L.append(f'typedef {ctype} T;\ntypedef {idx} IDX;')
     if hip:
         L.append('typedef unsigned u32x2 __attribute__((ext_vector_type(2)));')
+    # links whose value also depends on the fluid cell's density ρ(x) = Σ_k src_k(x) (a density-weighted moving wall):
+    # forward f_j += βρ·ρ(x); the adjoint adds Σ_j βρ_j v_j to every component of the cell in a second pass
+    rho_links = links is not None and any(len(t) > 3 and t[3] != 0 for lk in links for t in lk)
     if links is not None:
         # per (wall id, pulled component j): the link of direction d = ī_j (the population that left x towards the
         # wall cell x + c_d = x − c_j comes back as j)
         inv0 = [stencil.inverse_direction_index(i) for i in range(Q)]
         qual = '__constant__ T' if hip else 'static const T'
-        for nm, col in (('lk_a', 0), ('lk_b', 1), ('lk_g', 2)):
-            vals = [repr(float(links[k][inv0[j]][col])) for k in range(len(links)) for j in range(Q)]
+        cols = (('lk_a', 0), ('lk_b', 1), ('lk_g', 2)) + ((('lk_r', 3), ('lk_gr', 4)) if rho_links else ())
+        for nm, col in cols:
+            vals = [repr(float(links[k][inv0[j]][col] if col < len(links[k][inv0[j]]) else 0.0))
+                    for k in range(len(links)) for j in range(Q)]
             L.append(f'{qual} {nm}[{len(vals)}] = {{{", ".join(vals)}}};')
+    low = f'{(1 << Q) - 1}u'                 # neighbour-mask bits of the Q directions
 
     def c_(v):
         return f'({ct}){_c(v)}'
@@ -216,11 +222,20 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                              f'{prefix}o_{centre} : (IDX){i} * {prefix}_q + {prefix}o_{k}];')
                 if links is not None:
                     # the wall cell's link (moving wall: α = 1, β = 6 w (c·u)); its id is loaded on this path only
+                    rterm = f' + lk_r[id{i} * {Q} + {i}] * rs' if rho_links else ''
                     L.append(f'  unsigned id{i} = 0;')
                     L.append(f'  if ((msk >> {i}) & 1u) {{ id{i} = wallid[{ncell(k)}]; '
-                             f'f{i} = lk_a[id{i} * {Q} + {i}] * f{i} + lk_b[id{i} * {Q} + {i}]; }}')
+                             f'f{i} = lk_a[id{i} * {Q} + {i}] * f{i} + lk_b[id{i} * {Q} + {i}]{rterm}; }}')
             else:
                 L.append(f'  const {ct} f{i} = {load(prefix, arr, i, f"{prefix}o_{k}")};')
+
+    def cell_density(L, prefix, arr):
+        """ρ(x) of the cell's own (pre-streaming) pdfs, for density-weighted links, on cells next to a wall."""
+        if not rho_links:
+            return
+        L.append(f'  {ct} rs = 0;')
+        L.append(f'  if (msk & {low}) rs = ' + ' + '.join(load(prefix, arr, q, f'{prefix}o_{centre}')
+                                                      for q in range(Q)) + ';')
 
     def moments(L):
         L.append(f'  const {ct} rho = ' + ' + '.join(f'f{i}' for i in range(Q)) + ';')
@@ -256,7 +271,8 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
 
     mask_param = 'const unsigned* __restrict__ nbmask, const unsigned char* __restrict__ wallid'
     fptr_f = ', const T* __restrict__ force' if ff else ''
-    fptr_a = ', const T* __restrict__ force, T* __restrict__ dforce' if ff else ''
+    fptr_a = (', const T* __restrict__ force, T* __restrict__ dforce' if ff else '') + \
+        (', T* __restrict__ rho_adj' if rho_links else '')
     fstr = 'const IDX f_c, const IDX f_z, const IDX f_y, const IDX f_x, ' if ff else ''
     sig_fwd = (f'const T* __restrict__ src, T* __restrict__ dst, {mask_param}{fptr_f}, const int Z, const int Y, '
                'const int X, const IDX s_q, const IDX s_z, const IDX s_y, const IDX s_x, '
@@ -273,6 +289,8 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     else:
         fstr_unused = ''
     cell = '((IDX)z * Y + y) * X + x' if D == 3 else '(IDX)y * X + x'
+    sig_rho = ('T* __restrict__ out, const unsigned* __restrict__ nbmask, const T* __restrict__ rho_adj, const int Z, '
+               'const int Y, const int X, const IDX o_q, const IDX o_z, const IDX o_y, const IDX o_x')
 
     # ---- forward
     L.append(f'{fn} void lbm_fwd_cell({sig_fwd}, const int z, const int y, const int x)\n{{')
@@ -292,6 +310,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             L.append('    ' + store('d', 'dst', i, dcoff, load('s', 'src', i, f'so_{centre}')))
         L.append('    return;\n  }')
     force_loads(L)
+    cell_density(L, 's', 'src')
     pull_loads(L, 's', 'src')
     moments(L)
     if trt is not None:
@@ -343,8 +362,11 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     for i in range(Q):
         L.append(f'  const {ct} g{i} = {load("g", "g", i, gcoff)};')
     force_loads(L)
+    cell_density(L, 's', 'src')
     pull_loads(L, 's', 'src')
     moments(L)
+    if rho_links:
+        L.append(f'  {ct} Rr = 0;')             # Σ_j βρ_j v_j over the cell's density-weighted links
     L.append(f'  {ct} S = 0, A = 0;')
     for a in range(D):
         L.append(f'  {ct} B{a} = 0;')
@@ -414,6 +436,8 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             L.append(f'  {{ {vq}{ct} v = (({ct})1 - omega) * g{j} + omega * (A + {du});')
         k = key(dirs[j])
         if walls and any(dirs[j]) and links is not None:
+            if rho_links:
+                L.append(f'    if ((msk >> {j}) & 1u) Rr += lk_gr[id{j} * {Q} + {j}] * v;')
             L.append(f'    if ((msk >> {j}) & 1u) v *= lk_g[id{j} * {Q} + {j}];')
         if walls and any(dirs[j]):
             if buf:
@@ -425,10 +449,26 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                          f'= (T)v; }}')
         else:
             L.append('    ' + store('o', 'out', j, f'oo_{k}', 'v') + ' }')
+    if rho_links:
+        L.append(f'  if (msk & {low}) rho_adj[{cell}] = Rr;')
     L.append('}')
+    if rho_links:
+        # second adjoint pass: the density term of the cell's links reaches every component of the cell, whose
+        # adjoint entries the first pass wrote from other threads
+        L.append(f'{fn} void lbm_adj_rho_cell({sig_rho}, const int z, const int y, const int x)\n{{')
+        L.append('  (void)Z;')
+        L.append(f'  const unsigned msk = nbmask[{cell}];')
+        L.append(f'  if ((msk >> {SELF_BIT}) || !(msk & {low})) return;')
+        L.append(f'  const {ct} R = rho_adj[{cell}];')
+        L.append('  const IDX oc = ' + ' + '.join(f'(IDX){a} * o_{a}' for a in axes) + ';')
+        for q in range(Q):
+            L.append(f'  out[(IDX){q} * o_q + oc] += R;')
+        L.append('}')
 
     # ---- entry points
     fa_f, fa_a, fs = (', force', ', force, dforce', 'f_c, f_z, f_y, f_x, ') if ff else ('', '', '')
+    fa_a += ', rho_adj' if rho_links else ''
+    args_r = 'out, nbmask, rho_adj, Z, Y, X, o_q, o_z, o_y, o_x'
     args_f = (f'src, dst, nbmask, wallid{fa_f}, Z, Y, X, s_q, s_z, s_y, s_x, d_q, d_z, d_y, d_x, {fs}s_bytes, d_bytes, '
               'omega')
     args_a = (f'src, g, out, nbmask, wallid{fa_a}, Z, Y, X, s_q, s_z, s_y, s_x, g_q, g_z, g_y, g_x, o_q, o_z, o_y, o_x, '
@@ -438,7 +478,8 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         # (bijective remap of the round-robin dispatch): a lattice row's x-shifted loads and the adjoint's
         # x-shifted stores cover cache lines that the neighbouring wave also touches — in one block, or in a
         # block on the same XCD's L2, not split between two L2s (partial-line write-backs)
-        for nm, sig, args in (('lbm_fwd', sig_fwd, args_f), ('lbm_adj', sig_adj, args_a)):
+        for nm, sig, args in (('lbm_fwd', sig_fwd, args_f), ('lbm_adj', sig_adj, args_a)) + \
+                ((('lbm_adj_rho', sig_rho, args_r),) if rho_links else ()):
             L.append(f'extern "C" __global__ void __launch_bounds__(256) {nm}({sig})\n{{')
             L.append('  const unsigned nb = gridDim.x, b = blockIdx.x;')
             L.append('  const unsigned per = nb >> 3, rem = nb & 7, xcd = b & 7, bi = b >> 3;')
@@ -474,11 +515,19 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                 if ff:
                     L.append('  const T* force = (const T*)P[5]; T* dforce = (T*)P[6];')
                     L.append('  const IDX f_c = S[12], f_z = S[13], f_y = S[14], f_x = S[15];')
+                if rho_links:
+                    L.append(f'  T* rho_adj = (T*)P[{7 if ff else 5}];')
                 L.append('  const long long s_bytes = 0, g_bytes = 0, o_bytes = 0;')
                 call = f'lbm_adj_cell({args_a}, z, y, x);'
             L.append('  #pragma omp parallel for collapse(2) schedule(static)')
             L.append('  for (int z = 0; z < Z; ++z)\n    for (int y = 0; y < Y; ++y)\n      for (int x = 0; x < X; ++x)')
-            L.append(f'        {call}\n}}')
+            L.append(f'        {call}')
+            if kind == 'a' and rho_links:
+                # the density pass after every cell's scatter (the C target runs both passes in one call)
+                L.append('  #pragma omp parallel for collapse(2) schedule(static)')
+                L.append('  for (int z = 0; z < Z; ++z)\n    for (int y = 0; y < Y; ++y)\n      for (int x = 0; x < X; ++x)')
+                L.append(f'        lbm_adj_rho_cell({args_r}, z, y, x);')
+            L.append('}')
     return '\n'.join(L) + '\n'
 
 
@@ -539,6 +588,9 @@ class LatticeKernels:
         self.ct = 'double' if self.dtype == np.float64 else 'float'
         self.walls = bool(walls)
         self.links = links if walls else None
+        # density-weighted links: the adjoint takes a second pass (lbm_adj_rho) over a per-cell scratch array
+        self.rho_links = self.links is not None and any(len(t) > 3 and t[3] != 0 for lk in self.links for t in lk)
+        self._rho_bufs = {}
         self.target = target
         self._fns = {}
         self._plans = {}
@@ -657,10 +709,39 @@ class LatticeKernels:
                                                   ids.data_ptr() if ids is not None else 0]
         if force is not None:
             ptrs += [force.data_ptr()] + ([dforce.data_ptr()] if which == 'adj' else [])
+        if which == 'adj' and self.rho_links:
+            ptrs += [0]                                  # the density scratch array (patched per launch)
         fmt = 'Q' * len(ptrs) + 'iii' + code * len(strides) + 'q' * len(tensors) + \
             ('d' if self.ct == 'double' else 'f')
         args = _pack(fmt, *ptrs, Z, Y, X, *strides, *reach, float(omega))
         plan = self._plans[key] = LaunchPlan(fn, nblocks, args, len(ptrs), dev, _offset(fmt, len(fmt) - 1), fmt[-1])
+        return plan
+
+    def rho_buffer(self, t):
+        """The per-cell scratch array of the density pass (one per domain and device, reused: stream-ordered)."""
+        import torch
+        key = (tuple(int(n) for n in t.shape[:self.stencil.D]), t.device, t.dtype)
+        b = self._rho_bufs.get(key)
+        if b is None:
+            b = self._rho_bufs[key] = torch.empty(key[0], dtype=t.dtype, device=t.device)
+        return b
+
+    def rho_plan(self, out, mask, rho):
+        """The density pass of the adjoint (``lbm_adj_rho``: every component of a cell next to a density-weighted
+        wall gets the cell's Σ_j βρ_j v_j added) on ``out``'s shape and strides."""
+        key = ('rho', tuple(out.shape), tuple(out.stride()), out.dtype, out.device)
+        plan = self._plans.get(key)
+        if plan is not None:
+            return plan
+        idx, addr = self._mode([out])
+        dev = out.device.index
+        fn = self._gpu_fn('adj_rho', idx, addr, dev)
+        Z, Y, X = self._extent(out)
+        code = 'i' if idx == 'int' else 'q'
+        fmt = 'QQQ' + 'iii' + code * 4
+        args = _pack(fmt, out.data_ptr(), mask.data_ptr(), rho.data_ptr(), Z, Y, X,
+                     *lattice_strides(out, self.stencil.D))
+        plan = self._plans[key] = LaunchPlan(fn, self._blocks(X, Y, Z), args, 3, dev, None, None)
         return plan
 
     def forward(self, src, dst, omega, mask=None, stream=None, ids=None, force=None):
@@ -678,10 +759,15 @@ class LatticeKernels:
         ``dforce``."""
         if self.target != 'gpu':
             return self._cpu('adj', [src, g, out], omega, mask, ids, force, dforce)
+        st = _stream(stream, src)
+        rho = self.rho_buffer(src) if self.rho_links else None
         self.plan('adj', [src, g, out], mask, omega, ids, force, dforce)(
             (src.data_ptr(), g.data_ptr(), out.data_ptr(), mask.data_ptr() if mask is not None else 0,
              ids.data_ptr() if ids is not None else 0) +
-            ((force.data_ptr(), dforce.data_ptr()) if force is not None else ()), _stream(stream, src), omega)
+            ((force.data_ptr(), dforce.data_ptr()) if force is not None else ()) +
+            ((rho.data_ptr(),) if rho is not None else ()), st, omega)
+        if rho is not None:
+            self.rho_plan(out, mask, rho)((out.data_ptr(), mask.data_ptr(), rho.data_ptr()), st)
 
     def _extent(self, t):
         shape = [int(n) for n in t.shape[:self.stencil.D]]
@@ -736,6 +822,10 @@ class LatticeKernels:
         if force is not None:
             ptrs += [force.ctypes.data] + ([dforce.ctypes.data] if which == 'adj' else [])
             strides += list(lattice_strides(force, D))
+        rho = None
+        if which == 'adj' and self.rho_links:
+            rho = np.empty(shape[:D], self.dtype)          # the density pass's scratch (both passes in one call)
+            ptrs += [rho.ctypes.data]
         ext = list(shape[:D]) if D == 3 else [1] + list(shape[:D])
         P = (ctypes.c_void_p * len(ptrs))(*ptrs)
         N = (ctypes.c_longlong * 3)(*ext)
@@ -759,7 +849,7 @@ class LaunchPlan:
         from ..backends import hip_runtime as rt
         buf = bytearray(self.template)
         struct.pack_into(self.fmt, buf, 0, *ptrs)
-        if omega is not None:
+        if omega is not None and self.om_off is not None:
             struct.pack_into(self.om_fmt, buf, self.om_off, float(omega))
         import torch
         if self.device is not None and self.device != torch.cuda.current_device():

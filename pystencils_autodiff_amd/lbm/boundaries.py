@@ -24,9 +24,13 @@ at component 0 (``_autodiff.py:120-151``, the quirk its own ``AdjointNoSlip`` do
 which is not the gradient; the transposed form is what ``AdjointNoSlip`` spells out, for any affine link. The cells
 a boundary covers are a flag array (one id per boundary object): no index list, no separate boundary kernel.
 
-UBB: lbmpy multiplies the velocity term by the fluid cell's density for one of its two method families (the
-``compressible`` branch differs between lbmpy versions); the density-free form above is the one built — its link is
-affine in one pdf, so it fuses. A density-weighted variant is not affine and raises.
+UBB: lbmpy multiplies the velocity term by the fluid cell's density ρ(x) = Σ_k pdf(k) for one of its two method
+families (the ``compressible`` branch differs between lbmpy versions): ``UBB(u, density_weighted=True)`` prints that
+link, ``pdf[c_d](ī_d) ← pdf(d) − 6 w_d (c_d · u) ρ(x)`` — affine in ALL the cell's pdfs. The lattice kernels fuse it
+too: the forward adds ``βρ·ρ(x)`` (ρ from the cell's own pre-streaming pdfs, loaded on cells next to a wall), the
+adjoint scatters ``γ v`` as for any link and adds the density term ``Σ_j γρ_j v_j`` to every component of the cell in
+a second pass (``lbm_adj_rho``; those entries are written by other threads in the first). Links of any other form
+(a pressure / outflow condition, a nonlinear link) raise.
 """
 import numpy as np
 import sympy as sp
@@ -91,11 +95,14 @@ class NoSlip(Boundary):
 
 class UBB(Boundary):
     """Velocity bounce-back (lbmpy ``UBB`` [ext]): a wall moving with ``velocity`` (one component per spatial axis,
-    axis 0 first), e.g. the lid of a lid-driven cavity: ``pdf[c_d](ī_d) ← pdf(d) − 6 w_d (c_d · u)``."""
+    axis 0 first), e.g. the lid of a lid-driven cavity: ``pdf[c_d](ī_d) ← pdf(d) − 6 w_d (c_d · u)``;
+    ``density_weighted=True``: lbmpy's compressible form, the velocity term times the fluid cell's density
+    ``ρ = Σ_k pdf(k)`` (a subexpression, as lbmpy prints it)."""
 
-    def __init__(self, velocity, name=None):
+    def __init__(self, velocity, name=None, density_weighted=False):
         super().__init__(name if name is not None else 'UBB')
         self.velocity = tuple(velocity)
+        self.density_weighted = bool(density_weighted)
 
     def __call__(self, pdf_field, direction, lb_method, **kwargs):
         st = _directions(lb_method)
@@ -104,16 +111,22 @@ class UBB(Boundary):
             raise ValueError(f'UBB velocity {self.velocity} has not one component per axis of {st.name}')
         vel_term = 6 * st.weights[direction] * sum(ci * sp.sympify(ui) for ci, ui in zip(c, self.velocity) if ci)
         from .. import ps
-        return [ps.Assignment(pdf_field[c](st.inverse_direction_index(direction)), pdf_field(direction) - vel_term)]
+        link = pdf_field[c](st.inverse_direction_index(direction))
+        if self.density_weighted:
+            rho = sp.Symbol('rho')
+            return [ps.Assignment(rho, sum(pdf_field(k) for k in range(st.Q))),
+                    ps.Assignment(link, pdf_field(direction) - vel_term * rho)]
+        return [ps.Assignment(link, pdf_field(direction) - vel_term)]
 
     def __hash__(self):
-        return hash(('UBB', self.name, self.velocity))
+        return hash(('UBB', self.name, self.velocity, self.density_weighted))
 
     def __eq__(self, other):
-        return isinstance(other, UBB) and self.name == other.name and self.velocity == other.velocity
+        return isinstance(other, UBB) and self.name == other.name and self.velocity == other.velocity and \
+            self.density_weighted == other.density_weighted
 
     def __repr__(self):
-        return f'UBB({self.velocity!r}, {self.name!r})'
+        return f'UBB({self.velocity!r}, {self.name!r}' + (', density_weighted=True)' if self.density_weighted else ')')
 
 
 class AdjointNoSlip(Boundary):
@@ -183,10 +196,23 @@ def _affine(expr, var):
     return float(a), float(b)
 
 
+def _inline(assignments, lhs):
+    """The right-hand side of the assignment to ``lhs`` with the list's symbol assignments substituted."""
+    sym = [a for a in assignments if isinstance(a.lhs, sp.Symbol) and not hasattr(a.lhs, 'field')]
+    main = [a for a in assignments if a.lhs == lhs]
+    if len(main) != 1:
+        return None
+    rhs = main[0].rhs
+    for a in reversed(sym):
+        rhs = rhs.subs(a.lhs, a.rhs)
+    return rhs
+
+
 def link_coefficients(forward_bc, adjoint_bc, lb_method):
-    """Per direction ``d`` of ``lb_method``'s stencil: ``(α, β, γ)`` with the forward link
-    ``f_{ī_d}(x + c_d) = α·f_d(x) + β`` and the adjoint link ``g_d(x) = γ·g_{ī_d}(x + c_d)`` — the form the lattice
-    kernels fuse. Raises ``NotImplementedError`` for a boundary of another form."""
+    """Per direction ``d`` of ``lb_method``'s stencil: ``(α, β, γ, βρ, γρ)`` with the forward link
+    ``f_{ī_d}(x + c_d) = α·f_d(x) + βρ·Σ_k f_k(x) + β`` and the adjoint link
+    ``g_k(x) += (γ δ_kd + γρ)·g_{ī_d}(x + c_d)`` — the form the lattice kernels fuse (βρ = γρ = 0: a link in one pdf;
+    nonzero: a density-weighted link). Raises ``NotImplementedError`` for a boundary of another form."""
     from .. import ps
     from .._adjoint_field import AdjointField
     st = _directions(lb_method)
@@ -196,30 +222,48 @@ def link_coefficients(forward_bc, adjoint_bc, lb_method):
     for d in range(st.Q):
         c = st.directions[d]
         if not any(c):
-            out.append((1.0, 0.0, 1.0))
+            out.append((1.0, 0.0, 1.0, 0.0, 0.0))
             continue
         inv = st.inverse_direction_index(d)
         fwd = list(forward_bc(f, d, lb_method))
-        if len(fwd) != 1 or fwd[0].lhs != f[c](inv):
+        rhs = _inline(fwd, f[c](inv))
+        if rhs is None or any(a.lhs != f[c](inv) and hasattr(a.lhs, 'field') for a in fwd):
             raise NotImplementedError(f'{forward_bc!r}: the lattice kernels fuse one link assignment '
-                                      f'pdf[c_d](inv_d) <- alpha*pdf(d) + beta per direction, got {fwd}')
-        ab = _affine(fwd[0].rhs, f(d))
-        if ab is None:
-            raise NotImplementedError(f'{forward_bc!r}: link {fwd[0]} is not affine in pdf(d) with constant '
-                                      'coefficients (e.g. a density-weighted velocity term)')
+                                      f'pdf[c_d](inv_d) <- alpha*pdf(d) + beta (+ beta_rho*rho) per direction, got {fwd}')
+        coef = [_affine(sp.diff(rhs, f(k)) * f(k), f(k)) for k in range(st.Q)]
+        const = sp.expand(rhs - sum(sp.diff(rhs, f(k)) * f(k) for k in range(st.Q)))
+        if any(ck is None for ck in coef) or const.free_symbols or \
+                any(sp.diff(rhs, f(k)).free_symbols for k in range(st.Q)):
+            raise NotImplementedError(f'{forward_bc!r}: link {fwd} is not affine in the cell\'s pdfs with constant '
+                                      'coefficients')
+        a_k = [ck[0] for ck in coef]
+        others = [a_k[k] for k in range(st.Q) if k != d]
+        if max(others) - min(others) > 1e-15 * max(1.0, max(abs(v) for v in others)):
+            raise NotImplementedError(f'{forward_bc!r}: link {fwd} weights the other pdfs unequally (only a density '
+                                      'term Σ_k pdf(k) is fused)')
+        br = others[0]
+        alpha, beta = a_k[d] - br, float(const)
         bwd = adjoint_bc(g, d, lb_method)
-        mains = list(getattr(bwd, 'main_assignments', bwd))
-        if len(mains) != 1 or mains[0].lhs != g(d):
-            raise NotImplementedError(f'{adjoint_bc!r}: expected one adjoint link diffpdf(d) <- gamma * '
-                                      f'diffpdf[c_d](inv_d), got {mains}')
-        rhs = mains[0].rhs
-        subs = getattr(bwd, 'subexpressions', [])
-        for s in reversed(list(subs)):
-            rhs = rhs.subs(s.lhs, s.rhs)
-        gb = _affine(rhs, g[c](inv))
-        if gb is None or gb[1] != 0:
-            raise NotImplementedError(f'{adjoint_bc!r}: adjoint link {mains[0]} is not linear in diffpdf[c_d](inv_d)')
-        out.append((ab[0], ab[1], gb[0]))
+        allb = list(getattr(bwd, 'all_assignments', bwd))
+        gk = []
+        for k in range(st.Q):
+            r = _inline(allb, g(k))
+            if r is None:
+                gk.append(0.0)
+                continue
+            gb = _affine(r, g[c](inv))
+            if gb is None or gb[1] != 0:
+                raise NotImplementedError(f'{adjoint_bc!r}: adjoint link of pdf({k}) is not linear in '
+                                          f'diffpdf[c_d](inv_d): {r}')
+            gk.append(gb[0])
+        if any(hasattr(a.lhs, 'field') and a.lhs not in [g(k) for k in range(st.Q)] for a in allb):
+            raise NotImplementedError(f'{adjoint_bc!r}: adjoint assignments beyond diffpdf(k) <- gamma_k * '
+                                      f'diffpdf[c_d](inv_d): {allb}')
+        gothers = [gk[k] for k in range(st.Q) if k != d]
+        if max(gothers) - min(gothers) > 1e-15 * max(1.0, max(abs(v) for v in gothers)):
+            raise NotImplementedError(f'{adjoint_bc!r}: adjoint link weights the pdfs unequally')
+        gr = gothers[0]
+        out.append((alpha, beta, gk[d] - gr, br, gr))
     return tuple(out)
 
 
@@ -312,10 +356,10 @@ class BoundaryHandling:
         for k in range(1, len(objs)):
             obj = objs[k]
             t = link_coefficients(obj, self.adjoints[k], lb_method)
-            plain &= all(a == 1.0 and b == 0.0 and g == 1.0 for a, b, g in t)
+            plain &= all(a == 1.0 and b == 0.0 and g == 1.0 and br == 0.0 and gr == 0.0 for a, b, g, br, gr in t)
             tables.append(t)
         if plain:
             return None
         st = _directions(lb_method)
-        tables[0] = tuple((1.0, 0.0, 1.0) for _ in range(st.Q))
+        tables[0] = tuple((1.0, 0.0, 1.0, 0.0, 0.0) for _ in range(st.Q))
         return tuple(tables)

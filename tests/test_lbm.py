@@ -424,8 +424,8 @@ def _set_cavity(step, shape, adjoint=None):
 
 
 def test_boundary_links_and_generic_adjoint():
-    """The link assignments of NoSlip / UBB (lbmpy's form), the adjoint derived from them, and the (α, β, γ) the
-    lattice kernels fuse; a density-weighted (non-affine) link is refused."""
+    """The link assignments of NoSlip / UBB (lbmpy's form), the adjoint derived from them, and the (α, β, γ, βρ, γρ)
+    the lattice kernels fuse (density-weighted links too); a link of another form is refused."""
     import sympy as sp
     from pystencils_autodiff_amd import AdjointField, ps
     st = lbm.LBStencil('D2Q9')
@@ -442,23 +442,40 @@ def test_boundary_links_and_generic_adjoint():
     assert lbm.AdjointBoundaryCondition(ubb)(ps.fields('difff(9): [2D]'), 6, st).main_assignments[0].lhs.field.name == \
         'difff'
     co = lbm.link_coefficients(ubb, lbm.AdjointBoundaryCondition(ubb), st)
-    for d, (al, be, ga) in enumerate(co):
+    for d, (al, be, ga, br, gr) in enumerate(co):
         c = st.directions[d]
-        assert al == 1.0 and ga == 1.0
+        assert al == 1.0 and ga == 1.0 and br == 0.0 and gr == 0.0
         assert be == pytest.approx(-6 * float(st.weights[d]) * (0.1 * c[0] - 0.2 * c[1]))
-    assert lbm.link_coefficients(lbm.NoSlip(), lbm.AdjointNoSlip(), st) == tuple((1.0, 0.0, 1.0) for _ in range(9))
+    assert lbm.link_coefficients(lbm.NoSlip(), lbm.AdjointNoSlip(), st) == \
+        tuple((1.0, 0.0, 1.0, 0.0, 0.0) for _ in range(9))
 
     class DensityUBB(lbm.Boundary):
+        """A link weighted by the cell's density, inline (no subexpression): fused as βρ = -0.1."""
         def __call__(self, pdf_field, direction, lb_method, **kw):
             c = st.directions[direction]
             rho = sum(pdf_field(i) for i in range(9))
             return [ps.Assignment(pdf_field[c](st.inverse_direction_index(direction)), pdf_field(direction) - 0.1 * rho)]
+    co = lbm.link_coefficients(DensityUBB(), lbm.AdjointBoundaryCondition(DensityUBB()), st)
+    assert all(tuple(t) == pytest.approx((1.0, 0.0, 1.0, -0.1, -0.1)) for t in co[1:])
+    # lbmpy's compressible UBB (density subexpression): βρ = −6 w_d (c_d·u)
+    dub = lbm.UBB((0.1, -0.2), density_weighted=True)
+    for d, (al, be, ga, br, gr) in enumerate(lbm.link_coefficients(dub, lbm.AdjointBoundaryCondition(dub), st)):
+        c = st.directions[d]
+        assert al == pytest.approx(1.0) and be == 0.0 and ga == pytest.approx(1.0)
+        assert br == pytest.approx(-6 * float(st.weights[d]) * (0.1 * c[0] - 0.2 * c[1])) and gr == pytest.approx(br)
+
+    class Skewed(lbm.Boundary):
+        """Not of the fused form (another pdf weighted on its own)."""
+        def __call__(self, pdf_field, direction, lb_method, **kw):
+            c = st.directions[direction]
+            return [ps.Assignment(pdf_field[c](st.inverse_direction_index(direction)),
+                                  pdf_field(direction) - 0.1 * pdf_field(0))]
     with pytest.raises(NotImplementedError):
-        lbm.link_coefficients(DensityUBB(), lbm.AdjointBoundaryCondition(DensityUBB()), st)
+        lbm.link_coefficients(Skewed(), lbm.AdjointBoundaryCondition(Skewed()), st)
     step = lbm.AutoDiffLatticeBoltzmannStep(lbm.create_lb_update_rule('D2Q9', compressible=True),
                                             domain_size=(6, 5), relaxation_rate=1.0, target='cpu')
     with pytest.raises(NotImplementedError):
-        step.set_boundary_including_adjoint(DensityUBB())
+        step.set_boundary_including_adjoint(Skewed())
 
 
 @pytest.mark.parametrize('adjoint', ['derived', 'noslip'])
@@ -915,3 +932,68 @@ def test_lbm_trt_gpu_vs_oracle(stencil, shape, compressible, odd, layout, walls,
     step.run_backward(T)
     gg = step.adjoint_pdf_array.double().cpu().numpy()
     assert np.abs(gg - gref.numpy()).max() <= 1e-11 * np.abs(gref.numpy()).max()
+
+
+def _density_cavity(target, compressible, trt=False):
+    shape, T = (14, 11), 5
+    kw = dict(method='trt') if trt else {}
+    rule = lbm.create_lb_update_rule('D2Q9', compressible=compressible, **kw)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.3, target=target)
+    step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[0, :])
+    step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[-1, :])
+    step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[:, 0])
+    step.set_boundary_including_adjoint(lbm.UBB((LID_U, 0.0), density_weighted=True), lbm.make_slice[1:-1, -1])
+    wall, vel = _cavity(shape)
+    assert step._lattice_kernels().rho_links
+    return step, shape, T, wall, vel, (OL.trt_odd_rate(1.3) if trt else None)
+
+
+@pytest.mark.parametrize('compressible,trt', [(True, False), (False, False), (True, True)])
+def test_lbm_density_weighted_ubb_cpu(compressible, trt):
+    """Lid-driven cavity with lbmpy's compressible UBB (the wall term times the fluid cell's density): the link is
+    affine in all the cell's pdfs, fused into the C lattice kernels (ρ(x) from the cell's own pdfs in the forward, a
+    second adjoint pass for the density term); T steps vs the oracle, the adjoint vs torch's reverse mode."""
+    import torch
+    step, shape, T, wall, vel, w_odd = _density_cavity('cpu', compressible, trt)
+    f0 = _init('D2Q9', shape, compressible, seed=23)
+    step.set_pdfs(f0)
+    step.run(T, record=True)
+    ft = torch.tensor(f0, requires_grad=True)
+    ref = OL.run_moving_walls(ft, 1.3, torch.tensor(wall), torch.tensor(vel), T, 'D2Q9', compressible, xp=torch,
+                              density_weighted=True, omega_odd=w_odd)
+    plain = OL.run_moving_walls(torch.tensor(f0), 1.3, torch.tensor(wall), torch.tensor(vel), T, 'D2Q9', compressible,
+                                xp=torch, omega_odd=w_odd)
+    assert float((ref.detach() - plain).abs().max()) > 1e-4        # the density weighting is in
+    assert np.abs(step.pdf_array - ref.detach().numpy()).max() <= 1e-13 * np.abs(f0).max()
+    g = np.random.default_rng(24).standard_normal(f0.shape)
+    (gref,) = torch.autograd.grad(ref, ft, torch.tensor(g))
+    step.set_adjoint_pdfs(g)
+    step.run_backward(T)
+    assert np.abs(step.adjoint_pdf_array - gref.numpy()).max() <= 1e-12 * np.abs(gref.numpy()).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('compressible,trt', [(True, False), (False, False), (True, True)])
+def test_lbm_density_weighted_ubb_gpu(compressible, trt):
+    """The density-weighted UBB cavity on the HIP lattice kernels (two adjoint passes), through ``run`` and the
+    timestep op, vs the oracle and torch's reverse mode."""
+    import torch
+    step, shape, T, wall, vel, w_odd = _density_cavity('gpu', compressible, trt)
+    f0 = _init('D2Q9', shape, compressible, seed=23)
+    ft = torch.tensor(f0, requires_grad=True)
+    ref = OL.run_moving_walls(ft, 1.3, torch.tensor(wall), torch.tensor(vel), T, 'D2Q9', compressible, xp=torch,
+                              density_weighted=True, omega_odd=w_odd)
+    g = np.random.default_rng(24).standard_normal(f0.shape)
+    (gref,) = torch.autograd.grad(ref, ft, torch.tensor(g))
+    step.set_pdfs(torch.tensor(f0, device='cuda'))
+    step.run(T, record=True)
+    assert np.abs(step.pdf_array.cpu().numpy() - ref.detach().numpy()).max() <= 1e-12 * np.abs(f0).max()
+    step.set_adjoint_pdfs(torch.tensor(g, device='cuda'))
+    step.run_backward(T)
+    assert np.abs(step.adjoint_pdf_array.cpu().numpy() - gref.numpy()).max() <= 1e-11 * np.abs(gref.numpy()).max()
+    op = step.create_timestep_op(T)
+    x = torch.tensor(f0, device='cuda', requires_grad=True)
+    out = op.apply(x)
+    out.backward(torch.tensor(g, device='cuda'))
+    assert float((out.detach().cpu() - ref.detach()).abs().max()) <= 1e-12 * np.abs(f0).max()
+    assert float((x.grad.cpu() - gref).abs().max()) <= 1e-11 * float(gref.abs().max())
