@@ -74,7 +74,8 @@ TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZS
 
 
 def _band_config(ir, ve, shape, over):
-    """The row-band schedule (``hip_band``) for fp16 stencils it fits, when the row length is known and no tile
+    """The row-band schedule (``hip_band``) for the stencils it fits — fp16 storage, and fp32 star stencils on rows of
+    up to ``BAND_F32_STAR_MAX_X`` / ``BAND_F32_IDLE_MAX_X`` elements — when the row length is known and no tile
     override asks for another schedule (``BAND=0`` or ``PSAD_BAND=0`` turn it off, ``BAND=R`` / ``BTY`` pick
     rows per lane / band height)."""
     if shape is None or ir.ndim != 3 or os.environ.get('PSAD_BAND', '1') == '0':
