@@ -193,7 +193,8 @@ struct Exchange {
     // a sweep enqueued on another compute stream (torch.cuda.stream(s2), a second Python thread) would let the halo
     // stream pass early, so such sweeps take the event record + wait path instead
     mutable uint32_t seq = 0;
-    mutable hipStream_t sig_stream = nullptr;
+    mutable hipStream_t sig_stream = nullptr;   // (torch's default stream IS nullptr: sig_bound says whether it is set)
+    mutable bool sig_bound = false;
 };
 
 std::mutex g_sweep_mutex;               // serialises the enqueue of exchanging sweeps (counter order = stream order)
@@ -237,10 +238,11 @@ void run_sweep(const Sweep& w, const std::vector<at::Tensor>& table, const std::
     const size_t n = ex.slot.size();
     std::unique_lock<std::mutex> lock(g_sweep_mutex, std::defer_lock);
     if (n) lock.lock();
-    const bool sig = n && ex.sig && (ex.sig_stream == nullptr || ex.sig_stream == cur);
+    const bool sig = n && ex.sig && (!ex.sig_bound || ex.sig_stream == cur);
     uint32_t seq = 0;
     if (sig) {
         ex.sig_stream = cur;
+        ex.sig_bound = true;
         seq = ++ex.seq;
     }
     if (sig) {

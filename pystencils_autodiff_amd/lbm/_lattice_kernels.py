@@ -843,7 +843,7 @@ class LaunchPlan:
 
     def __init__(self, fn, nblocks, template, nptr, device, om_off, om_code):
         self.fn, self.nblocks, self.template, self.fmt = fn, nblocks, template, f'<{nptr}Q'
-        self.device, self.om_off, self.om_fmt = device, om_off, '<' + om_code
+        self.device, self.om_off, self.om_fmt = device, om_off, None if om_code is None else '<' + om_code
 
     def __call__(self, ptrs, stream, omega=None):
         from ..backends import hip_runtime as rt
