@@ -102,16 +102,31 @@ def _fits(X, TY, R, D, es=2, pad=0, reg=0, idle=False):
     return (idle or g['ntask'] % 64 == 0) and g['NCT'] <= 960 and D * g['NI'] <= 63 and g['lds_bytes'] <= 80 * 1024
 
 
-def band_choice(X, nstore=1, es=2, pad=0, reg=0, idle=False):
+def band_choice(X, nstore=1, es=2, pad=0, reg=0, idle=False, star=False, wide16=True):
     """(TY, R, D) for rows of X elements, or None. fp16, measured (scripts/probes/band_ab.py,
     profiles/r03_band_ab*.log): 8-row bands of 4 rows per lane with 2 planes in flight at X = 768 and 1024
     (27-point 1024³: 0.895 ms vs 0.921 for 4-row bands of 2 rows per lane, 3 planes in flight); three workgroups
     per CU. fp32 rows hold half the cells per 16-byte chunk: 4-row bands of 4 rows per lane first (the loader's
-    vmcnt budget and 80 KB of LDS)."""
+    vmcnt budget and 80 KB of LDS).
+
+    Round 5 (profiles/r05_band_geo1.log, through the op, same process): fp16 rows of at least 96 chunks whose
+    16-row band of 2 rows per lane fills whole compute waves (X = 768: 12 compute waves, one workgroup per CU)
+    take that band first — 27-point 768³ fwd+bwd 0.675 vs 0.705-0.711 ms with 8-row bands of 4 rows (2 planes in
+    flight; 18 rows read per 16 stored instead of 10 per 8: the memory pattern alone 0.640 vs 0.662 ms), fp16
+    7-point 768³ 0.604 vs 0.630 (``star``: 1 plane in flight, 0.626 with 2). 512-wide rows (8 compute waves) keep the
+    8-row bands (0.210 vs 0.198 ms); 1024-wide rows do not fit 16 row groups of 128 chunks."""
     VE = 16 // es
     if X < 16 * VE:
         return None
     rmax = 4 if nstore == 1 else 2
+    CPR = -(-X // VE)
+    if wide16 and es == 2 and CPR >= 96 and X % VE == 0:
+        first = (16, 2, 1 if star else 2)
+        g = band_geometry(X, *first, es, pad, reg)
+        # one workgroup per CU (up to 160 KB of LDS; the padded image at X = 768 takes 84 KB)
+        if first[1] <= rmax and g['ntask'] % 64 == 0 and g['NCT'] <= 960 and first[2] * g['NI'] <= 63 and \
+                g['lds_bytes'] <= 160 * 1024:
+            return first
     # fp16: 16-row bands of 2 rows per lane before 4- / 8-row bands with 3 planes in flight (27-point 512²×640 0.279 vs
     # 0.335 ms, ×384 0.166 vs 0.170; fp16 7-point ×640 0.248 vs 0.252, ×384 0.149 vs 0.153: profiles/r04_op_band_823.log)
     cands = [(8, 4, 2), (16, 2, 2), (4, 2, 3), (8, 2, 3)] if es == 2 else [(4, 4, 2), (8, 4, 2), (4, 2, 2), (8, 2, 2)]

@@ -89,7 +89,15 @@ def _band_config(ir, ve, shape, over):
     X = int(shape[-1])
     es = band_esize(ir) if plans else 0
     ntaps = max(len(pl['w']) for pl in plans) if plans else 0
-    whole = band_choice(X, len(plans), es) if plans else None
+    whole = band_choice(X, len(plans), es, star=ntaps <= 12) if plans else None
+    if whole is not None and whole[:2] == (16, 2) and 'BAND' not in over:
+        # the wide-row 16-row band (one workgroup per CU) only where its launch still fills three rounds of the
+        # chip with the chunk length it would take (a 96×768² slab would get 576 workgroups: 8-row bands there)
+        nty16, Z = -(-int(shape[-2]) // 16), int(shape[0])
+        zc16 = BAND_ZC_STAR if ntaps <= 12 else next((c for c in BAND_ZC_BOX_LADDER if nty16 * -(-Z // c) >=
+                                                      BAND_ROUND_WG), BAND_ZC_BOX_LADDER[-1])
+        if nty16 * -(-Z // zc16) < BAND_ROUND_WG:
+            whole = band_choice(X, len(plans), es, star=ntaps <= 12, wide16=False)
     if plans and es == 4 and 'BAND' not in over and \
             not (ntaps <= 12 and X <= (BAND_F32_STAR_MAX_X if whole else BAND_F32_IDLE_MAX_X)):
         return None

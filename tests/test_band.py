@@ -49,8 +49,10 @@ def test_band_eligibility():
 
 
 def test_band_choice_and_geometry():
-    assert band_choice(768) == (8, 4, 2)
-    assert band_choice(1024) == (8, 4, 2) and band_choice(768, 2)[1] == 2
+    # rows of >= 96 chunks: 16-row bands of 2 rows per lane (one workgroup per CU; star stencils 1 plane in flight)
+    assert band_choice(768) == (16, 2, 2) and band_choice(768, star=True) == (16, 2, 1)
+    assert band_choice(768, wide16=False) == (8, 4, 2)
+    assert band_choice(1024) == (8, 4, 2) and band_choice(768, 2)[1] == 2 and band_choice(512) == (8, 4, 2)
     assert band_choice(264) is None and band_choice(100) is None and band_choice(96) is None
     for X in (256, 512, 768, 1024, 640, 2048):
         c = band_choice(X)
@@ -58,10 +60,11 @@ def test_band_choice_and_geometry():
             continue
         TY, R, D = c
         g = band_geometry(X, TY, R, D)
-        assert g['ntask'] % 64 == 0 and g['NCT'] <= 960 and D * g['NI'] <= 63 and g['lds_bytes'] <= 80 * 1024
+        assert g['ntask'] % 64 == 0 and g['NCT'] <= 960 and D * g['NI'] <= 63
+        assert g['lds_bytes'] <= (160 if (TY, R) == (16, 2) else 80) * 1024
 
 
-@pytest.mark.parametrize('shape,expect,zc', [((768, 768, 768), 4, 48), ((1024, 1024, 1024), 4, 32),
+@pytest.mark.parametrize('shape,expect,zc', [((768, 768, 768), 2, 48), ((1024, 1024, 1024), 4, 32),
                                              ((96, 768, 768), 4, 12), ((512, 512, 512), 4, 32), ((256, 256, 256), 4, 8),
                                              ((255, 255, 255), 4, 8), ((64, 256, 256), 0, 0), ((40, 40, 264), 0, 0),
                                              ((512, 1024, 1024), 4, 48)])
@@ -85,7 +88,9 @@ def test_band_default_selection_star(shape, zc):
     """fp16 7-point: 8-plane chunks, 64-plane ones on rows of <= 512 elements (>= 512 workgroups)."""
     op = pa.AutoDiffOp(W.diffusion_7pt(dtype='float16'), boundary_handling='zeros')
     cfg = default_march_config(HipStencilKernel(_kernel(op.forward_assignments)).ir, 8, shape)
-    assert cfg.BAND == 4 and cfg.ZMIN == cfg.ZMAX == zc and cfg.BPAD == 0, cfg
+    wide = shape[-1] == 768           # 16-row bands of 2 rows per lane, one plane in flight
+    assert (cfg.BTY, cfg.BAND, cfg.D) == ((16, 2, 1) if wide else (8, 4, 2)), cfg
+    assert cfg.ZMIN == cfg.ZMAX == zc and cfg.BPAD == 0, cfg
     assert cfg.BREG == shape[-1] % 2, cfg                      # odd rows: the register-staged padded image
 
 
