@@ -257,10 +257,17 @@ def run_workload(name, edge, args, world, rank, distributed, extras, warmup=None
         if record:
             ev.append((e0, e1, e2))
 
-    # (the secondary 27-point sweep gets >= 60 warmup steps, ~50 ms: its first dispatches after the 1024^3 run
-    # land in a power-management transient, profiles/r02_power_transient_27pt.txt)
-    for _ in range(args.warmup if warmup is None else warmup):
+    # (the secondary 27-point sweep gets >= 60 warmup steps and at least 0.5 s of them: its first dispatches after the
+    # 1024^3 run land in a power-management transient, profiles/r02_power_transient_27pt.txt; alone with 10 warmup
+    # steps config 5 measured 0.760 ms per step, with 300 0.704, profiles/r05_b27_warmup.log)
+    nwarm = args.warmup if warmup is None else warmup
+    t_warm = time.perf_counter()
+    i = 0
+    while i < nwarm or (warmup is not None and time.perf_counter() - t_warm < 0.5):
         step(False)
+        i += 1
+        if i % 8 == 0:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
