@@ -260,14 +260,26 @@ def run_workload(name, edge, args, world, rank, distributed, extras, warmup=None
     # (the secondary 27-point sweep gets >= 60 warmup steps and at least 0.5 s of them: its first dispatches after the
     # 1024^3 run land in a power-management transient, profiles/r02_power_transient_27pt.txt; alone with 10 warmup
     # steps config 5 measured 0.760 ms per step, with 300 0.704, profiles/r05_b27_warmup.log)
-    nwarm = args.warmup if warmup is None else warmup
-    t_warm = time.perf_counter()
     i = 0
-    while i < nwarm or (warmup is not None and time.perf_counter() - t_warm < 0.5):
-        step(False)
-        i += 1
-        if i % 8 == 0:
+    if warmup is None:
+        for i in range(1, args.warmup + 1):        # the line's contract: exactly W warmup steps
+            step(False)
+    else:
+        # blocks of 8 steps until both the count and the time are reached; at N>1 the ranks agree after each block
+        # (every step exchanges halos, so all ranks must run the same number of steps)
+        t_warm = time.perf_counter()
+        while True:
+            for _ in range(8):
+                step(False)
+                i += 1
             torch.cuda.synchronize()
+            more = i < warmup or time.perf_counter() - t_warm < 0.5
+            if distributed:
+                flag = torch.tensor([1.0 if more else 0.0], device='cuda')
+                dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+                more = flag.item() > 0
+            if not more:
+                break
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -342,7 +354,7 @@ def run_workload(name, edge, args, world, rank, distributed, extras, warmup=None
     zop_keep = zop if distributed else None
     kname = fwd_k.source(fwd_k.last_variant)[1] if fwd_k.last_variant else fwd_k.name
     out = dict(n=n, zl=zl, value=value, ms_per_step=ms_per_step, fwd_ms=fwd_ms, bwd_ms=bwd_ms, achieved=achieved,
-               ksha=kernel_sha(fwd_k, bwd_k),
+               ksha=kernel_sha(fwd_k, bwd_k), warmup_steps=i,
                achieved_fwd=achieved_fwd, achieved_bwd=achieved_bwd, bytes_fwd=bytes_fwd, kname=kname,
                cells=cells_total, extra=result_extra, zop=zop_keep)
     del uu, u, d, fn, op
@@ -427,7 +439,7 @@ def main():
             res['secondary'] = {
                 'metric': f'Mcells/s forward+backward, {w2["label"]} {n2}^3', 'name': args.secondary,
                 'value': round(secondary['value'], 1), 'unit': 'Mcells/s', 'n_gpus': world, 'steps': args.steps,
-                'warmup': max(args.warmup, 60), 'ms_per_step': round(secondary['ms_per_step'], 4),
+                'warmup': secondary['warmup_steps'], 'ms_per_step': round(secondary['ms_per_step'], 4),
                 'fwd_ms': round(secondary['fwd_ms'], 4), 'bwd_ms': round(secondary['bwd_ms'], 4),
                 'dtype': w2['dtype_tag'], 'cells': secondary['cells'],
                 'decomposition': f'z-slab x{world}' if world > 1 else 'single GPU',
