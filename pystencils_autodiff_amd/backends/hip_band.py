@@ -68,12 +68,12 @@ def band_padded(X, es, pad):
     return bool(pad) and (X * es) % 16 == 0
 
 
-def band_geometry(X, TY, R, D, es=2, pad=0, reg=0):
+def band_geometry(X, TY, R, D, es=2, pad=0, reg=0, lw=1):
     """Launch / LDS geometry of a band of ``TY`` rows (``R`` per lane) on rows of ``X`` elements of ``es`` bytes.
     Rows whose pitch is not a multiple of 16 bytes (``X % VE``) take ``ceil(X / VE)`` chunks, the last one partial.
     ``pad``: every image row is preceded by one zero 16-byte piece and the slot ends with one (x neighbours of a row's
     end chunks read as zeros straight from LDS). ``reg``: rows of a partial last chunk on a padded image filled through
-    registers (``BREG``)."""
+    registers (``BREG``). ``lw``: loader waves sharing each plane's pieces (the piece count rounded up to a multiple)."""
     VE = 16 // es
     CPR = -(-X // VE)
     reg = bool(reg) and X % VE != 0
@@ -89,10 +89,12 @@ def band_geometry(X, TY, R, D, es=2, pad=0, reg=0):
     NCT = -(-ntask // 64) * 64
     NPIECE = (TY + 2) * (XP // VE) + (1 if padded else 0)
     NI = -(-NPIECE // 64)
+    lw = 1 if reg else max(1, int(lw))
+    NI = -(-NI // lw) * lw
     SLOT = NI * 64 * VE
     NS = 3 if reg else D + 1
-    return dict(VE=VE, CPR=CPR, XP=XP, G=G, ntask=ntask, NCT=NCT, NT=NCT + 64, NPIECE=NPIECE, NI=NI, SLOT=SLOT,
-                NS=NS, lds_bytes=(NS * SLOT + 64) * es)
+    return dict(VE=VE, CPR=CPR, XP=XP, G=G, ntask=ntask, NCT=NCT, NT=NCT + 64 * lw, NPIECE=NPIECE, NI=NI, SLOT=SLOT,
+                NS=NS, lds_bytes=(NS * SLOT + 64) * es, LW=lw, NIL=NI // lw)
 
 
 def _fits(X, TY, R, D, es=2, pad=0, reg=0, idle=False):
@@ -207,10 +209,12 @@ def emit_band(ir, name, cfg):
     TY, R, D = cfg.BTY, cfg.BAND, cfg.D
     breg = bool(cfg.BREG) and X % (16 // es) != 0     # partial rows on a padded image filled through registers
     padded = breg or band_padded(X, es, cfg.BPAD)
-    g = band_geometry(X, TY, R, D, es, padded, breg)
+    g = band_geometry(X, TY, R, D, es, padded, breg, cfg.BLW)
     VE, CPR, G, NCT, NT, NPIECE, NI, SLOT, NS = (g[k] for k in ('VE', 'CPR', 'G', 'NCT', 'NT', 'NPIECE', 'NI', 'SLOT',
                                                                  'NS'))
-    assert D * NI <= 63 and NCT <= 960, (X, TY, R, D)
+    LW, NIL = g['LW'], g['NIL']            # loader waves, pieces per plane each
+    assert D * NIL <= 63 and NT <= 1024, (X, TY, R, D, LW)
+    assert LW == 1 or not cfg.BLDR, 'the rotating loader role takes one loader wave'
     assert not fixed or int(fixed[0].spatial_shape[-1]) == X, 'band kernel compiled for another row length'
     S = ir.stencil_fields[0]
     half = es == 2
@@ -223,6 +227,8 @@ def emit_band(ir, name, cfg):
     bo = not breg and (X * es) % 4 != 0             # rows on half dwords (fp16, X odd): realigned in registers
     assert not partial or cfg.BMASK, 'rows of a partial last chunk need the masked stores'
     czf = bu and not cfg.BZF                        # BZF=0: the first element past a row zeroed in registers
+    # (the loader's zero fill of unaligned rows needs every piece of the plane landed: one loader wave there)
+    assert LW == 1 or not (bu or bo), 'several loader waves need rows of a multiple of 16 bytes'
     dpp_edges = padded and not breg and cfg.BPE == 3 and band_dpp_edges_ok(CPR)
     pr = KernelExprPrinter('float', dict(ir.symbol_names))
     W = []
@@ -286,17 +292,22 @@ def emit_band(ir, name, cfg):
         L.append(f'  const int ldw = blockIdx.x % {NCT // 64 + 1};')
     else:
         L.append(f'  const int ldw = {NCT // 64};')
-    L.append('  if (wave == ldw) {')
+    if LW > 1:
+        # several loader waves: wave ldw + l streams pieces [l·NIL, (l+1)·NIL) of every plane, counts its own vmcnt
+        L.append(f'  if (wave >= ldw) {{')
+        L.append(f'    const int lw0 = (wave - ldw) * {NIL};')
+    else:
+        L.append('  if (wave == ldw) {')
     if cfg.BPRIO:
         L.append(f'    __builtin_amdgcn_s_setprio({int(cfg.BPRIO)});')
     if not breg:
-        L.append(f'    int vo[{NI}];')
+        L.append(f'    int vo[{NIL}];')
         if bo:
-            L.append(f'    int vo1[{NI}];')
+            L.append(f'    int vo1[{NIL}];')
             L.append('    auto hpar = [&](const void* b) { return b ? (int)(((unsigned long long)b >> 1) & 1) : 0; };')
         L.append('    #pragma unroll')
-        L.append(f'    for (int i = 0; i < {NI}; ++i) {{')
-        L.append('      const int k = i * 64 + lane;')
+        L.append(f'    for (int i = 0; i < {NIL}; ++i) {{')
+        L.append('      const int k = ' + ('(lw0 + i)' if LW > 1 else 'i') + ' * 64 + lane;')
         if padded:
             # image row rr = one zero piece (out of range: the DMA writes zeros) + the row's pieces; one zero piece ends
             # the slot (the right neighbour of the last row's end)
@@ -330,11 +341,11 @@ def emit_band(ir, name, cfg):
         else:
             L.append(f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? pb : '
                      f'f_{S.name}), (short)0, pb ? (int)(YX * {es}) : 0, 0x00020000);')
-        L.append(f'      {et}* dst = lds + slot * {SLOT};')
+        L.append(f'      {et}* dst = lds + slot * {SLOT}' + (f' + lw0 * {64 * VE};' if LW > 1 else ';'))
         if cfg.BABL == 3:
             L.append('      if (Z < 0)   // ablation probe: no plane loads')
         L.append('      #pragma unroll')
-        L.append(f'      for (int i = 0; i < {NI}; ++i)')
+        L.append(f'      for (int i = 0; i < {NIL}; ++i)')
         L.append(f'        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + i * '
                  f'{64 * VE}), 16, {"pp ? vo1[i] : vo[i]" if bo else "vo[i]"}, 0, 0, {int(cfg.BLAUX)});')
         L.append('    };')
@@ -349,7 +360,7 @@ def emit_band(ir, name, cfg):
         L.append(f'      const int after = min({D - 1}, nplanes - 1 - j);')
         L.append('      switch (after) {')
         for a in range(D):
-            L.append(f'        case {a}: asm volatile("s_waitcnt vmcnt({a * NI})" ::: "memory"); break;')
+            L.append(f'        case {a}: asm volatile("s_waitcnt vmcnt({a * NIL})" ::: "memory"); break;')
         L.append('      }')
         if bo and not czf:
             # plane j has landed: zeros over the image columns past each row's last element (X + the row's parity .. XP)
@@ -469,7 +480,8 @@ def emit_band(ir, name, cfg):
     # ---- compute lanes
     if bo:
         L.append('  auto hpar = [&](const void* b) { return b ? (int)(((unsigned long long)b >> 1) & 1) : 0; };')
-    L.append('  const int ctid = (wave - (wave > ldw ? 1 : 0)) * 64 + lane;   // compute task')
+    L.append('  const int ctid = (wave - (wave > ldw ? 1 : 0)) * 64 + lane;   // compute task' if LW == 1 else
+             '  const int ctid = wave * 64 + lane;                          // compute task (loaders: the last waves)')
     L.append(f'  const bool active = ctid < {g["ntask"]};')
     L.append(f'  const int t = active ? ctid : {g["ntask"] - 1};')
     L.append(f'  const int grp = t / {CPR}, col = t - grp * {CPR};')

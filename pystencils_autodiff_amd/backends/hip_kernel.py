@@ -70,7 +70,7 @@ BAND_F32_IDLE_MAX_X = 1024
 # keys are this layer's tile parameters; an unknown one is a typo and raises.
 TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
              'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE', 'BLDR', 'BLAUX', 'BPAD', 'BZF', 'BREG', 'BMBR', 'BNT', 'BPE', 'BSI',
-             'BPRIO', 'BABL')
+             'BPRIO', 'BABL', 'BLW')
 
 
 def _band_config(ir, ve, shape, over):
@@ -158,7 +158,8 @@ def _band_config(ir, ve, shape, over):
                        BSTAG=int(over.get('BSTAG', 0)), BWPE=int(over.get('BWPE', 0)), BLDR=int(over.get('BLDR', 0)),
                        BLAUX=int(over.get('BLAUX', 0)), BPAD=pad, BZF=int(over.get('BZF', 1)), BREG=reg,
                        BMBR=int(over.get('BMBR', 0)), BNT=int(over.get('BNT', 2)), BPE=int(over.get('BPE', 0)),
-                       BSI=int(over.get('BSI', 0)), BPRIO=int(over.get('BPRIO', 0)), BABL=int(over.get('BABL', 0)))
+                       BSI=int(over.get('BSI', 0)), BPRIO=int(over.get('BPRIO', 0)), BABL=int(over.get('BABL', 0)),
+                       BLW=int(over.get('BLW', 1)))
 
 
 def default_march_config(ir, ve, shape=None, tuning=None, band=True):
@@ -800,7 +801,7 @@ class HipStencilKernel:
                                           'nty')]
         kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics) + \
             [self._scalar_kind()] * len(ir.scalars)
-        block = ws['block'] if ws else (band_geometry(cfg.BX, cfg.BTY, cfg.BAND, cfg.D, esize, cfg.BPAD, cfg.BREG)['NT'] if cfg.BAND else
+        block = ws['block'] if ws else (band_geometry(cfg.BX, cfg.BTY, cfg.BAND, cfg.D, esize, cfg.BPAD, cfg.BREG, cfg.BLW)['NT'] if cfg.BAND else
                                         cfg.NT)
         return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics, xb=cfg.XB, block=block)
 

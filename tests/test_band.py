@@ -183,8 +183,9 @@ def test_band_vs_oracle(case, shape, bh):
 @pytest.mark.parametrize('case', CASES, ids=lambda c: c[0])
 @pytest.mark.parametrize('shape', [(9, 21, 256), (7, 16, 768)])
 @pytest.mark.parametrize('bh', ['zeros', None])
-@pytest.mark.parametrize('knob', [{'BPAD': 1}, {'BPAD': 1, 'BPE': 3}, {'BPAD': 1, 'BSI': 1}, {'BPAD': 0}],
-                         ids=['pad', 'pad-dppedge', 'pad-storeil', 'dpp'])
+@pytest.mark.parametrize('knob', [{'BPAD': 1}, {'BPAD': 1, 'BPE': 3}, {'BPAD': 1, 'BSI': 1}, {'BPAD': 0},
+                                  {'BPAD': 1, 'BLW': 2}, {'BPAD': 0, 'BLW': 3}],
+                         ids=['pad', 'pad-dppedge', 'pad-storeil', 'dpp', 'pad-2loaders', 'dpp-3loaders'])
 def test_band_padded_rows_vs_oracle(case, shape, bh, knob):
     """Zero-padded LDS image rows (``BPAD=1``: row ends meet the zero pads) with the x-edge dwords read from LDS
     (``BPE=0``) or taken from the neighbour lanes by DPP within 16-lane rows (``BPE=3``, the rows' end lanes read
@@ -325,7 +326,8 @@ def test_band_chunk_length_and_band_height_bitwise():
               # both chunk ends peeled with a compile-time chunk length (ragged chunks: the BTRIM=1 path)
               {'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13}, {'BTRIM': 3, 'ZMIN': 37, 'ZMAX': 37}, {'BTRIM': 3, 'ZMIN': 3, 'ZMAX': 3},
               {'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13, 'BLDR': 1},  # the loader role rotating over waves
-              {'BSI': 1}, {'BSI': 1, 'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13})
+              {'BSI': 1}, {'BSI': 1, 'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13},
+              {'BLW': 2}, {'BLW': 3, 'D': 3, 'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13})      # several loader waves
     layouts = {'BPAD=1': [{'BAND': 4, 'BPAD': 1, **t} for t in common],
                'BPAD=0': [{'BAND': 4, 'BPAD': 0, **t} for t in common],
                # x-edge dwords by DPP within 16-lane rows on the padded image: the compiler contracts these FMAs as on
