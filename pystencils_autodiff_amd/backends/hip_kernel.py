@@ -128,8 +128,8 @@ def _band_config(ir, ve, shape, over):
         R = int(over['BAND'])
     TY = int(over.get('BTY', TY if TY % R == 0 else R * max(1, TY // R)))
     D = int(over.get('D', D))
-    g = band_geometry(X, TY, R, D, es, pad, reg)
-    if TY % R or g['NCT'] > 960 or D * g['NI'] > 63 or g['lds_bytes'] > 160 * 1024:
+    g = band_geometry(X, TY, R, D, es, pad, reg, int(over.get('BLW', 1)))
+    if TY % R or g['NCT'] > 960 or D * g['NIL'] > 63 or g['lds_bytes'] > 160 * 1024 or g['NT'] > 1024:
         raise ValueError(f'band schedule: BTY={TY} BAND={R} D={D} do not fit rows of {X} elements')
     nty, Z = -(-int(shape[-2]) // TY), int(shape[0])
     min_wg = BAND_MIN_WG
