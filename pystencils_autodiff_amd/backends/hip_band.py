@@ -304,7 +304,7 @@ def emit_band(ir, name, cfg):
         L.append(f'    int vo[{NIL}];')
         if bo:
             L.append(f'    int vo1[{NIL}];')
-            L.append('    auto hpar = [&](const void* b) { return b ? (int)(((unsigned long long)b >> 1) & 1) : 0; };')
+            L.append('    auto hpar = [&](const void* b) { return (int)(((unsigned long long)b >> 1) & 1); };   // 0 for nullptr')
         L.append('    #pragma unroll')
         L.append(f'    for (int i = 0; i < {NIL}; ++i) {{')
         L.append('      const int k = ' + ('(lw0 + i)' if LW > 1 else 'i') + ' * 64 + lane;')
@@ -479,7 +479,7 @@ def emit_band(ir, name, cfg):
         L.append('  }')
     # ---- compute lanes
     if bo:
-        L.append('  auto hpar = [&](const void* b) { return b ? (int)(((unsigned long long)b >> 1) & 1) : 0; };')
+        L.append('  auto hpar = [&](const void* b) { return (int)(((unsigned long long)b >> 1) & 1); };   // 0 for nullptr')
     L.append('  const int ctid = (wave - (wave > ldw ? 1 : 0)) * 64 + lane;   // compute task' if LW == 1 else
              '  const int ctid = wave * 64 + lane;                          // compute task (loaders: the last waves)')
     L.append(f'  const bool active = ctid < {g["ntask"]};')
@@ -488,6 +488,13 @@ def emit_band(ir, name, cfg):
     L.append(f'  const int lofs = grp * {R * XP} + {c0} + col * {VE};   // slot row grp*R = input row y0 + grp*R - 1')
     L.append(f'  const int x = col * {VE};')
     L.append(f'  const bool lmask = col == 0, rmask = col == {CPR - 1};')
+    if bo:
+        # the x-boundary zeros of half-dword rows as per-lane AND masks held in VGPRs (opaque to the compiler, so they
+        # are not folded back into selects on 64-bit lane masks: those, with the per-plane v_perm selectors, ran the
+        # kernel out of SGPRs — v_writelane / v_readlane spills in the plane loop)
+        L.append('  unsigned lk0 = lmask ? 0xffff0000u : 0xffffffffu, rk = rmask ? 0u : 0xffffffffu, '
+                 'rk0 = rmask ? 0xffff0000u : 0xffffffffu;')
+        L.append('  asm volatile("" : "+v"(lk0), "+v"(rk), "+v"(rk0));')
     if cfg.BMASK:
         L.append(f'  const bool xfull = x >= xlo && x + {VE} <= xhi;')
         L.append(f'  const bool xtail = x + {VE} > {X};                 // the row\'s partial last chunk (unaligned rows)')
@@ -528,17 +535,16 @@ def emit_band(ir, name, cfg):
                   f'{ind}    const unsigned e = *(const unsigned*)(rp + eoff);',
                   f'{ind}    const unsigned lw = __builtin_amdgcn_update_dpp(e, d.w, 0x138, 0xf, 0xf, false);   // wave_shr:1',
                   f'{ind}    const unsigned rw = __builtin_amdgcn_update_dpp(e, d.x, 0x130, 0xf, 0xf, false);   // wave_shl:1',
-                  f'{ind}    {cq}f16x2 w0 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.x, lw, {sel})), '
+                  f'{ind}    {cq}f16x2 w0 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.x, lw, {sel}) & lk0), '
                   f'w1 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.y, d.x, {sel}));',
                   f'{ind}    {cq}f16x2 w2 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.z, d.y, {sel})), '
                   f'w3 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(d.w, d.z, {sel}));',
                   # the row's last chunk: x+7 and x+8 both lie at or past X (8·CPR - 1 >= X for odd X) and on a row
                   # loaded one element early both come from the next lane, which may hold another row: zeros
-                  f'{ind}    const f16x2 w4 = rmask ? (f16x2)((_Float16)0) : '
-                  f'__builtin_bit_cast(f16x2, __builtin_amdgcn_perm(rw, d.w, {sel}));',
-                  f'{ind}    const _Float16 l = lmask ? (_Float16)0 : w0[0], rr = w4[1];',
-                  *([f'{ind}    w{(X % VE + 1) // 2}[0] = rmask ? (_Float16)0 : w{(X % VE + 1) // 2}[0];   '
-                     '// the first element past the row end (no loader zero fill)']
+                  f'{ind}    const f16x2 w4 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(rw, d.w, {sel}) & rk);',
+                  f'{ind}    const _Float16 l = w0[0], rr = w4[1];',
+                  *([f'{ind}    w{(X % VE + 1) // 2} = __builtin_bit_cast(f16x2, __builtin_bit_cast(unsigned, '
+                     f'w{(X % VE + 1) // 2}) & rk0);   // the first element past the row end (no loader zero fill)']
                     if czf and (X % VE + 1) // 2 < 4 else []),
                   f'{ind}    const f32x2 P0 = {{(float)l, (float)w2[0]}}, P1 = {{(float)w0[1], (float)w2[1]}}, '
                   'P2 = {(float)w1[0], (float)w3[0]};',
@@ -638,10 +644,13 @@ def emit_band(ir, name, cfg):
         vt = 'f16x8' if half else 'f32x4'
         for o in (range(R) if rows is None else rows):
             vals = ', '.join(cell(si, sp, o, q) for q in range(VE))
-            st = f'__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ov), ors, sofs + {o * X * es}u, 0, 2);'
+            st = (f'__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ov), ors, sofs + '
+                  f'{o * X * es + cfg.BSHIFT}u, 0, 2);')
             if not cfg.BMASK:
                 # every row of every band inside [ylo, yhi), x range = whole rows (checked at plan time)
-                B.append(f'{ind}  {{ const {vt} ov = {{{vals}}}; {st} }}')
+                dead = (f' __builtin_amdgcn_raw_buffer_store_b96((u32x3)__builtin_bit_cast(u32x4, ov).xyz, ors, '
+                        f'0x7ffffff0u + {cfg.BDEAD - 1}u * lane, 0, 2);' if cfg.BDEAD else '')
+                B.append(f'{ind}  {{ const {vt} ov = {{{vals}}}; {st}{dead} }}')
                 continue
             nb_t = (X % VE) * es if partial else 0           # bytes of a row's partial last chunk
             ndw_t, nh_t = nb_t // 4, (nb_t % 4) // 2       # whole dwords, then one half (X odd)
@@ -655,13 +664,22 @@ def emit_band(ir, name, cfg):
                     c = 'xyzw'
                     B.append(f'{ind}    const u32x4 ow = __builtin_bit_cast(u32x4, ov);')
                     B.append(f'{ind}    __builtin_amdgcn_raw_buffer_store_b128(ow, ors, xtail ? 0x7ffffff0u : ro, 0, 2);')
-                    B.append(f'{ind}    const unsigned rt = xtail ? ro : 0x7ffffff0u;')
+                    # the tail store under a branch on the tail lanes (BTB=1): a store whose 64 lanes all move data
+                    # costs the memory pipe about a full store even where the range check drops 63 of them
+                    # (profiles/r05_pitch_ablation.log: without output stores 510-wide rows run as fast as 512)
+                    B.append(f'{ind}    const unsigned rt = ro;' if cfg.BTB else
+                             f'{ind}    const unsigned rt = xtail ? ro : 0x7ffffff0u;')
+                    tb = []
                     if ndw_t:
                         ty = {1: 'unsigned', 2: 'u32x2', 3: 'u32x3'}[ndw_t]
-                        B.append(f'{ind}    __builtin_amdgcn_raw_buffer_store_b{32 * ndw_t}(({ty})ow.{c[:ndw_t]}, ors, rt, 0, 2);')
+                        tb.append(f'__builtin_amdgcn_raw_buffer_store_b{32 * ndw_t}(({ty})ow.{c[:ndw_t]}, ors, rt, 0, 2);')
                     if nh_t:
-                        B.append(f'{ind}    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)ow.{c[ndw_t]}, ors, '
-                                 f'rt + {4 * ndw_t}u, 0, 2);')
+                        tb.append(f'__builtin_amdgcn_raw_buffer_store_b16((unsigned short)ow.{c[ndw_t]}, ors, '
+                                  f'rt + {4 * ndw_t}u, 0, 2);')
+                    if cfg.BTB:
+                        B.append(f'{ind}    if (xtail) {{ ' + ' '.join(tb) + ' }')
+                    else:
+                        B += [f'{ind}    {t}' for t in tb]
                 else:
                     B.append(f'{ind}    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ov), ors, ro, 0, 2);')
                 B.append(f'{ind}  }}')
@@ -768,7 +786,9 @@ def emit_band(ir, name, cfg):
             # the lane take the plane's parity (selA), even rows the other one (selB); 0x05040302 = elements shifted
             # by one (the row was loaded one element early), 0x07060504 = the dword as it is
             B += [f'{ind}  const int ppq = hpar({_ws_plane_base(S, 1, "(zb - 1 + jj)")});',
-                  f'{ind}  const unsigned selA = ppq ? 0x07060504u : 0x05040302u, selB = ppq ? 0x05040302u : 0x07060504u;']
+                  # (scalar arithmetic, not selects: a select becomes a 64-bit lane mask per unrolled step)
+                  f'{ind}  const unsigned selA = 0x05040302u + (unsigned)ppq * 0x02020202u, '
+                  'selB = 0x07060504u - (unsigned)ppq * 0x02020202u;']
         # sets a trimmed step leaves alone are dead (outputs already stored or outside the chunk): overwrite them first
         # so their old values are not live through the step (a full step overwrites its q+1 set; +16-45 VGPRs else)
         for s_ in sorted({sp, s0, sn} - {st for st, _ in sets}):

@@ -70,7 +70,7 @@ BAND_F32_IDLE_MAX_X = 1024
 # keys are this layer's tile parameters; an unknown one is a typo and raises.
 TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
              'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE', 'BLDR', 'BLAUX', 'BPAD', 'BZF', 'BREG', 'BMBR', 'BNT', 'BPE', 'BSI',
-             'BPRIO', 'BABL', 'BLW')
+             'BPRIO', 'BABL', 'BLW', 'BTB', 'BSHIFT', 'BDEAD')
 
 
 def _band_config(ir, ve, shape, over):
@@ -159,7 +159,8 @@ def _band_config(ir, ve, shape, over):
                        BLAUX=int(over.get('BLAUX', 0)), BPAD=pad, BZF=int(over.get('BZF', 1)), BREG=reg,
                        BMBR=int(over.get('BMBR', 0)), BNT=int(over.get('BNT', 2)), BPE=int(over.get('BPE', 0)),
                        BSI=int(over.get('BSI', 0)), BPRIO=int(over.get('BPRIO', 0)), BABL=int(over.get('BABL', 0)),
-                       BLW=int(over.get('BLW', 1)))
+                       BLW=int(over.get('BLW', 1)), BTB=int(over.get('BTB', 0)),
+                       BSHIFT=int(over.get('BSHIFT', 0)), BDEAD=int(over.get('BDEAD', 0)))
 
 
 def default_march_config(ir, ve, shape=None, tuning=None, band=True):

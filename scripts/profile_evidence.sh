@@ -50,5 +50,7 @@ python scripts/pmc_summary.py "$F" "$W" --workload "diffusion7_f32_1024^3" --byt
     --json "$OUT/traffic_$TAG.json" --source "$SRC" --git-head "$HEAD" --kernel-sha "$KS1" > "$OUT/traffic_$TAG.txt"; fatal $? sum1
 python scripts/pmc_summary.py "$F" "$W" --workload "stencil27_f16_768^3" --bytes 1811939328 --select stencil27_f16 \
     --json "$OUT/traffic_$TAG.json" --source "$SRC" --git-head "$HEAD" --kernel-sha "$KS2" >> "$OUT/traffic_$TAG.txt"; fatal $? sum2
+python scripts/sq_summary.py "$OUT/pmcband_${TAG}_1/pmc_counter_collection.csv" "$OUT/pmcband_${TAG}_2/pmc_counter_collection.csv" \
+    --select stencil27_f16 > "$OUT/pmc_band_sq_$TAG.txt"; fatal $? sq
 cut -c1-160 "$OUT/prof_$TAG/trace_kernel_stats.csv" | head -8
 echo done-profile
