@@ -196,3 +196,51 @@ def run_moving_walls(f, omega, wall, wall_velocity, steps, stencil='D2Q9', compr
                       compressible, xp, omega_odd=omega_odd)
         f = xp.where(keep, f, new)
     return f
+
+
+def stream_pressure_walls(f, stencil, wall, pressure, rho_wall, compressible, xp, wall_velocity=None):
+    """Pull streaming with bounce-back walls and pressure cells (lbmpy's ``FixedDensity`` [ext], anti-bounce-back):
+    where ``x − c_i`` is a pressure cell of density ``ρ_w`` (``pressure``: bool over the domain, a subset of
+    ``wall``; ``rho_wall``: per cell, read at pressure cells), with ``d = ī`` the direction that left ``x`` towards
+    it, ``f_i(x) = 2 w_d ρ_w (1 + 4.5 (c_d·u)² − 1.5 u²) − f_d(x)`` (incompressible: ``2 w_d (ρ_w + 4.5 (c_d·u)² −
+    1.5 u²) − f_d(x)``) with ``u = Σ_k c_k f_k(x) / ρ_w`` (incompressible: without the division) of the fluid cell's
+    own pdfs — lbmpy prints the equilibrium's velocity subexpression with its density symbol replaced by ρ_w. Other
+    wall cells bounce back (moving with ``wall_velocity`` where given, as ``stream_moving_walls``)."""
+    dirs, w = SETS[stencil]
+    inv = inverse(stencil)
+    D = len(dirs[0])
+    m = [sum(c[a] * f[..., k] for k, c in enumerate(dirs) if c[a]) for a in range(D)]
+    comps = []
+    for i, c in enumerate(dirs):
+        pulled = _roll_all(xp, f[..., i], c)
+        if not any(c):
+            comps.append(pulled)
+            continue
+        d = inv[i]
+        nb_wall = _roll_all(xp, wall, c)
+        nb_p = _roll_all(xp, pressure, c)
+        rw = _roll_all(xp, rho_wall, c)
+        bounced = f[..., d]
+        if wall_velocity is not None:
+            bounced = bounced + 6 * float(w[i]) * sum(ca * _roll_all(xp, wall_velocity[..., a], c)
+                                                       for a, ca in enumerate(c) if ca)
+        u = [ma / rw if compressible else ma for ma in m]
+        cu = sum(dirs[d][a] * u[a] for a in range(D) if dirs[d][a])
+        usq = sum(ua * ua for ua in u)
+        sym = rw * (1 + 4.5 * cu * cu - 1.5 * usq) if compressible else rw + 4.5 * cu * cu - 1.5 * usq
+        anti = 2 * float(w[d]) * sym - f[..., d]
+        comps.append(xp.where(nb_wall, xp.where(nb_p, anti, bounced), pulled))
+    return xp.stack(comps, -1) if xp.__name__ != 'torch' else xp.stack(comps, dim=-1)
+
+
+def run_pressure_walls(f, omega, wall, pressure, rho_wall, steps, stencil='D2Q9', compressible=False, xp=None,
+                       omega_odd=None):
+    """``steps`` stream-pull-collide steps with no-slip walls and pressure cells; wall cells keep their state."""
+    if xp is None:
+        import numpy as xp
+    keep = wall[..., None] if xp.__name__ != 'torch' else wall.unsqueeze(-1)
+    for _ in range(steps):
+        new = collide(stream_pressure_walls(f, stencil, wall, pressure, rho_wall, compressible, xp), omega, stencil,
+                      compressible, xp, omega_odd=omega_odd)
+        f = xp.where(keep, f, new)
+    return f

@@ -38,8 +38,8 @@ from .. import ps
 from ..autodiff import AutoDiffOp
 from ._lattice_kernels import LatticeKernels, neighbour_mask
 from ._method import LBStencil
-from .boundaries import (AdjointBoundaryCondition, AdjointNoSlip, Boundary, BoundaryHandling, NoSlip,  # noqa: F401
-                         link_coefficients)
+from .boundaries import (AdjointBoundaryCondition, AdjointNoSlip, Boundary, BoundaryHandling, LBMethodView,  # noqa: F401
+                         NoSlip, link_form)
 
 __all__ = ['AutoDiffLatticeBoltzmannStep', 'PdfFieldNotDetectedException', 'SimulationResultsTensors']
 
@@ -71,7 +71,7 @@ def _lattice_sweeps(step, which, launches, force=None, dforce=None):
     if force is not None:
         mptr += (force.data_ptr(),) + ((dforce.data_ptr(),) if which == 'adj' else ())
     stream = _torch()._C._cuda_getCurrentRawStream(launches[0][0].device.index)
-    rho = K.rho_buffer(launches[0][0]) if which == 'adj' and K.rho_links else None
+    rho = K.rho_buffer(launches[0][0]) if which == 'adj' and K.link_pass else None
     if rho is not None:
         mptr += (rho.data_ptr(),)
     plans = {}
@@ -82,7 +82,7 @@ def _lattice_sweeps(step, which, launches, force=None, dforce=None):
             plan = plans[sig] = K.plan(which, list(ts), mask, om, ids, force, dforce if which == 'adj' else None)
         plan(tuple(t.data_ptr() for t in ts) + mptr, stream, om)
         if rho is not None:
-            # the density pass of the density-weighted walls, on this launch's output
+            # the second pass of density-weighted walls / link programs, on this launch's output
             K.rho_plan(ts[2], mask, rho)((ts[2].data_ptr(), mask.data_ptr(), rho.data_ptr()), stream)
 
 
@@ -235,6 +235,8 @@ class AutoDiffLatticeBoltzmannStep:
                                and (self._force_field is None or
                                     self._force_field.dtype.numpy_dtype == src.dtype.numpy_dtype)) else None
         self._boundary = BoundaryHandling(self.domain_size, on_change=self._flags_changed)
+        # the lb_method the boundaries see: the stencil plus the rule's compressibility (FixedDensity reads it)
+        self._bc_method = LBMethodView(self.method, getattr(update_rule, 'compressible', False))
         self._adjoint_boundary_conditions = {}
         self._flag_dev = None
         self._ids_dev = None
@@ -355,10 +357,10 @@ class AutoDiffLatticeBoltzmannStep:
 
     def set_boundary_including_adjoint(self, boundary_condition, slice_obj=None, mask_callback=None, mask_array=None,
                                        adjoint_boundary_condition=None):
-        """Set ``boundary_condition`` (a ``Boundary``: ``NoSlip``, ``UBB``, or any boundary whose link is affine,
-        ``boundaries.link_coefficients``) on the selected cells for the forward AND the adjoint steps (the
-        reference's signature; the adjoint condition defaults to ``AdjointBoundaryCondition(bc)``, derived from the
-        forward link by AD)."""
+        """Set ``boundary_condition`` (a ``Boundary``: ``NoSlip``, ``UBB``, ``FixedDensity``, or any boundary whose
+        link reads only the fluid cell's own pdfs, ``boundaries.link_form``) on the selected cells for the forward
+        AND the adjoint steps (the reference's signature; the adjoint condition defaults to
+        ``AdjointBoundaryCondition(bc)``, derived from the forward link by AD)."""
         if not isinstance(boundary_condition, Boundary) or \
                 isinstance(boundary_condition, (AdjointNoSlip, AdjointBoundaryCondition)):
             raise NotImplementedError(f'boundary {boundary_condition!r}: needs a forward Boundary object')
@@ -367,12 +369,12 @@ class AutoDiffLatticeBoltzmannStep:
                                       'time-constant or additional fields)')
         if adjoint_boundary_condition is None:
             adjoint_boundary_condition = self._adjoint_boundary_conditions.setdefault(
-                boundary_condition, AdjointBoundaryCondition(boundary_condition,
-                                                             time_constant_fields=self._autodiff.time_constant_fields,
-                                                             constant_fields=self._autodiff.constant_fields))
+                boundary_condition, AdjointBoundaryCondition(
+                    boundary_condition, time_constant_fields=list(self._autodiff_args['time_constant_fields'] or []),
+                    constant_fields=list(self._autodiff_args['constant_fields'] or []) + ['indexVector']))
         elif not isinstance(adjoint_boundary_condition, (AdjointNoSlip, AdjointBoundaryCondition)):
             raise NotImplementedError(f'adjoint boundary {adjoint_boundary_condition!r}')
-        link_coefficients(boundary_condition, adjoint_boundary_condition, self.method)   # the kernels' form, or raise
+        link_form(boundary_condition, adjoint_boundary_condition, self._bc_method)   # the kernels' form, or raise
         self._boundary.set_boundary(boundary_condition, slice_obj, mask_callback=mask_callback, mask_array=mask_array,
                                     adjoint=adjoint_boundary_condition)
 
@@ -398,13 +400,19 @@ class AutoDiffLatticeBoltzmannStep:
 
     def _links(self):
         """The wall kernels' link tables (None: every wall a plain bounce-back, or no walls), derived once per
-        boundary change (``link_coefficients`` differentiates each boundary's sympy link: milliseconds, not per
-        step)."""
+        boundary change (``link_form`` differentiates each boundary's sympy link: not per step)."""
+        return self._link_data()[0]
+
+    def _programs(self):
+        """The link programs of the walls the fused form does not take (None if there are none)."""
+        return self._link_data()[1]
+
+    def _link_data(self):
         cached = getattr(self, '_links_cached', None)
         if cached is None:
-            cached = self._links_cached = (self._boundary.link_tables(self.method) if self._boundary.has_walls
-                                           else None,)
-        return cached[0]
+            cached = self._links_cached = (self._boundary.link_tables(self._bc_method) if self._boundary.has_walls
+                                           else (None, None))
+        return cached
 
     def _ids_arg(self):
         """The cells' wall ids for kernels with link tables (the flag array on the kernels' device), else None."""
@@ -421,13 +429,13 @@ class AutoDiffLatticeBoltzmannStep:
 
     def _lattice_kernels(self):
         walls = self._boundary.has_walls
-        links = self._links()
-        k = self._lattice.get((walls, links))
+        links, programs = self._link_data()
+        k = self._lattice.get((walls, links, programs))
         if k is None:
-            k = self._lattice[(walls, links)] = LatticeKernels(
+            k = self._lattice[(walls, links, programs)] = LatticeKernels(
                 self.method, getattr(self._update_rule, 'compressible', False), self.pdf_field.dtype.numpy_dtype,
                 walls, self._target, links, *self._lattice_force, force_field=self._force_field is not None,
-                trt=self._lattice_trt)
+                trt=self._lattice_trt, programs=programs)
         return k
 
     # -- kernels -----------------------------------------------------------------------------------

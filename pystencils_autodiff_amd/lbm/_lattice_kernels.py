@@ -45,7 +45,7 @@ SELF_BIT = 30      # bit of a cell's neighbour mask: the cell itself is an obsta
 
 
 def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=None, force_model=None, force=None,
-          force_field=False, trt=None):
+          force_field=False, trt=None, programs=None):
     """Source of the forward (``lbm_fwd``) and adjoint (``lbm_adj``) kernels.
 
     ``addr='buf'`` (HIP): every pdf array is one buffer resource (its bytes below 2³²); a component's plane
@@ -70,7 +70,11 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     ``trt``: the TRT method (``_method.create_lb_update_rule(method='trt')``): ``('magic', Λ)`` (ω₋ from ω and the
     magic number, computed per launch from the ω argument) or ``('rate', ω₋)`` (a constant). With a = (ω₊ + ω₋)/2,
     b = (ω₊ − ω₋)/2 the collision is ``dst_i = (1 − a) f_i − b f_ī + a feq_i + b feq_ī`` and the adjoint takes the
-    equilibrium sums over h_i = a g_i + b g_ī: ``v_j = (1 − a) g_j − b g_ĵ + A_h + Σ_a B_h,a ∂u_a/∂f_j``."""
+    equilibrium sums over h_i = a g_i + b g_ī: ``v_j = (1 − a) g_j − b g_ĵ + A_h + Σ_a B_h,a ∂u_a/∂f_j``.
+    ``programs``: per wall id None or the boundary's ``link_program`` (links of the cell's own pdfs the fused form does
+    not take, ``boundaries.link_program``; their table rows are zeros): the forward evaluates the link from the
+    cell's own pdfs ``c0 … c{Q-1}``, the adjoint accumulates ``G_k = Σ_j J_jk v_j`` over the cell's program links and a
+    second pass (``lbm_adj_rho``, with the density term folded into ``G``) adds ``G_k`` to component k of the cell."""
     D, Q = stencil.D, stencil.Q
     dirs = [tuple(d) for d in stencil.directions]
     w = [float(x) for x in stencil.weights]
@@ -96,6 +100,8 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     # links whose value also depends on the fluid cell's density ρ(x) = Σ_k src_k(x) (a density-weighted moving wall):
     # forward f_j += βρ·ρ(x); the adjoint adds Σ_j βρ_j v_j to every component of the cell in a second pass
     rho_links = links is not None and any(len(t) > 3 and t[3] != 0 for lk in links for t in lk)
+    gen = links is not None and programs is not None and any(p is not None for p in programs)
+    two = rho_links or gen                  # the adjoint's second pass over a per-cell scratch array
     if links is not None:
         # per (wall id, pulled component j): the link of direction d = ī_j (the population that left x towards the
         # wall cell x + c_d = x − c_j comes back as j)
@@ -206,6 +212,12 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             return f'((IDX){coord(k, "z")} * Y + {coord(k, "y")}) * X + {coord(k, "x")}'
         return f'(IDX){coord(k, "y")} * X + {coord(k, "x")}'
 
+    def program_cases(i):
+        """(wall id, program of the link pulled as component i: direction ī) for the ids with link programs."""
+        if not gen or not any(dirs[i]):
+            return []
+        return [(wid, pg[inv[i]]) for wid, pg in enumerate(programs) if pg is not None and pg[inv[i]] is not None]
+
     def pull_loads(L, prefix, arr):
         for i in range(Q):
             k = key(dirs[i])
@@ -226,11 +238,26 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                     L.append(f'  unsigned id{i} = 0;')
                     L.append(f'  if ((msk >> {i}) & 1u) {{ id{i} = wallid[{ncell(k)}]; '
                              f'f{i} = lk_a[id{i} * {Q} + {i}] * f{i} + lk_b[id{i} * {Q} + {i}]{rterm}; }}')
+                    cases = program_cases(i)
+                    if cases:
+                        L.append(f'  if ((msk >> {i}) & 1u) switch (id{i}) {{')
+                        for wid, pg in cases:
+                            lines, val, _ = pg
+                            L.append(f'    case {wid}: {{ ' + ' '.join(lines) + f' f{i} = {val}; }} break;')
+                        L.append('    default: break;\n  }')
             else:
                 L.append(f'  const {ct} f{i} = {load(prefix, arr, i, f"{prefix}o_{k}")};')
 
     def cell_density(L, prefix, arr):
-        """ρ(x) of the cell's own (pre-streaming) pdfs, for density-weighted links, on cells next to a wall."""
+        """ρ(x) of the cell's own (pre-streaming) pdfs, for density-weighted links, on cells next to a wall (with
+        link programs: the cell's own pdfs c0 … c{Q-1} themselves, which the programs read)."""
+        if gen:
+            L.append(f'  {ct} ' + ', '.join(f'c{q} = 0' for q in range(Q)) + ';')
+            L.append(f'  if (msk & {low}) {{ ' + ' '.join(f'c{q} = {load(prefix, arr, q, f"{prefix}o_{centre}")};'
+                                                           for q in range(Q)) + ' }')
+            if rho_links:
+                L.append(f'  const {ct} rs = ' + ' + '.join(f'c{q}' for q in range(Q)) + ';')
+            return
         if not rho_links:
             return
         L.append(f'  {ct} rs = 0;')
@@ -272,7 +299,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     mask_param = 'const unsigned* __restrict__ nbmask, const unsigned char* __restrict__ wallid'
     fptr_f = ', const T* __restrict__ force' if ff else ''
     fptr_a = (', const T* __restrict__ force, T* __restrict__ dforce' if ff else '') + \
-        (', T* __restrict__ rho_adj' if rho_links else '')
+        (', T* __restrict__ rho_adj' if two else '')
     fstr = 'const IDX f_c, const IDX f_z, const IDX f_y, const IDX f_x, ' if ff else ''
     sig_fwd = (f'const T* __restrict__ src, T* __restrict__ dst, {mask_param}{fptr_f}, const int Z, const int Y, '
                'const int X, const IDX s_q, const IDX s_z, const IDX s_y, const IDX s_x, '
@@ -367,6 +394,8 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     moments(L)
     if rho_links:
         L.append(f'  {ct} Rr = 0;')             # Σ_j βρ_j v_j over the cell's density-weighted links
+    if gen:
+        L.append(f'  {ct} ' + ', '.join(f'G{q} = 0' for q in range(Q)) + ';')   # Σ_j J_jq v_j (link programs)
     L.append(f'  {ct} S = 0, A = 0;')
     for a in range(D):
         L.append(f'  {ct} B{a} = 0;')
@@ -438,6 +467,13 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         if walls and any(dirs[j]) and links is not None:
             if rho_links:
                 L.append(f'    if ((msk >> {j}) & 1u) Rr += lk_gr[id{j} * {Q} + {j}] * v;')
+            cases = program_cases(j)
+            if cases:
+                L.append(f'    if ((msk >> {j}) & 1u) switch (id{j}) {{')
+                for wid, pg in cases:
+                    rows = ' '.join('{ ' + ' '.join(jl) + f' G{q} += ({je}) * v; }}' for q, jl, je in pg[2])
+                    L.append(f'      case {wid}: {{ {rows} }} break;')
+                L.append('      default: break;\n    }')
             L.append(f'    if ((msk >> {j}) & 1u) v *= lk_g[id{j} * {Q} + {j}];')
         if walls and any(dirs[j]):
             if buf:
@@ -449,25 +485,33 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                          f'= (T)v; }}')
         else:
             L.append('    ' + store('o', 'out', j, f'oo_{k}', 'v') + ' }')
-    if rho_links:
+    ncells = '(IDX)Z * Y * X'
+    if gen:
+        L.append(f'  if (msk & {low}) {{ ' + ' '.join(f'rho_adj[(IDX){q} * {ncells} + {cell}] = G{q}'
+                                                     + (' + Rr;' if rho_links else ';') for q in range(Q)) + ' }')
+    elif rho_links:
         L.append(f'  if (msk & {low}) rho_adj[{cell}] = Rr;')
     L.append('}')
-    if rho_links:
+    if two:
         # second adjoint pass: the density term of the cell's links reaches every component of the cell, whose
         # adjoint entries the first pass wrote from other threads
         L.append(f'{fn} void lbm_adj_rho_cell({sig_rho}, const int z, const int y, const int x)\n{{')
         L.append('  (void)Z;')
         L.append(f'  const unsigned msk = nbmask[{cell}];')
         L.append(f'  if ((msk >> {SELF_BIT}) || !(msk & {low})) return;')
-        L.append(f'  const {ct} R = rho_adj[{cell}];')
         L.append('  const IDX oc = ' + ' + '.join(f'(IDX){a} * o_{a}' for a in axes) + ';')
-        for q in range(Q):
-            L.append(f'  out[(IDX){q} * o_q + oc] += R;')
+        if gen:
+            for q in range(Q):
+                L.append(f'  out[(IDX){q} * o_q + oc] += rho_adj[(IDX){q} * {ncells} + {cell}];')
+        else:
+            L.append(f'  const {ct} R = rho_adj[{cell}];')
+            for q in range(Q):
+                L.append(f'  out[(IDX){q} * o_q + oc] += R;')
         L.append('}')
 
     # ---- entry points
     fa_f, fa_a, fs = (', force', ', force, dforce', 'f_c, f_z, f_y, f_x, ') if ff else ('', '', '')
-    fa_a += ', rho_adj' if rho_links else ''
+    fa_a += ', rho_adj' if two else ''
     args_r = 'out, nbmask, rho_adj, Z, Y, X, o_q, o_z, o_y, o_x'
     args_f = (f'src, dst, nbmask, wallid{fa_f}, Z, Y, X, s_q, s_z, s_y, s_x, d_q, d_z, d_y, d_x, {fs}s_bytes, d_bytes, '
               'omega')
@@ -479,7 +523,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         # x-shifted stores cover cache lines that the neighbouring wave also touches — in one block, or in a
         # block on the same XCD's L2, not split between two L2s (partial-line write-backs)
         for nm, sig, args in (('lbm_fwd', sig_fwd, args_f), ('lbm_adj', sig_adj, args_a)) + \
-                ((('lbm_adj_rho', sig_rho, args_r),) if rho_links else ()):
+                ((('lbm_adj_rho', sig_rho, args_r),) if two else ()):
             L.append(f'extern "C" __global__ void __launch_bounds__(256) {nm}({sig})\n{{')
             L.append('  const unsigned nb = gridDim.x, b = blockIdx.x;')
             L.append('  const unsigned per = nb >> 3, rem = nb & 7, xcd = b & 7, bi = b >> 3;')
@@ -515,14 +559,14 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                 if ff:
                     L.append('  const T* force = (const T*)P[5]; T* dforce = (T*)P[6];')
                     L.append('  const IDX f_c = S[12], f_z = S[13], f_y = S[14], f_x = S[15];')
-                if rho_links:
+                if two:
                     L.append(f'  T* rho_adj = (T*)P[{7 if ff else 5}];')
                 L.append('  const long long s_bytes = 0, g_bytes = 0, o_bytes = 0;')
                 call = f'lbm_adj_cell({args_a}, z, y, x);'
             L.append('  #pragma omp parallel for collapse(2) schedule(static)')
             L.append('  for (int z = 0; z < Z; ++z)\n    for (int y = 0; y < Y; ++y)\n      for (int x = 0; x < X; ++x)')
             L.append(f'        {call}')
-            if kind == 'a' and rho_links:
+            if kind == 'a' and two:
                 # the density pass after every cell's scatter (the C target runs both passes in one call)
                 L.append('  #pragma omp parallel for collapse(2) schedule(static)')
                 L.append('  for (int z = 0; z < Z; ++z)\n    for (int y = 0; y < Y; ++y)\n      for (int x = 0; x < X; ++x)')
@@ -575,7 +619,7 @@ class LatticeKernels:
     bounce-back)."""
 
     def __init__(self, stencil, compressible, dtype, walls, target, links=None, force_model=None, force=None,
-                 force_field=False, trt=None):
+                 force_field=False, trt=None, programs=None):
         self.stencil = stencil
         self.trt = None if trt is None else (str(trt[0]), float(trt[1]))
         self.force_model = force_model
@@ -590,6 +634,10 @@ class LatticeKernels:
         self.links = links if walls else None
         # density-weighted links: the adjoint takes a second pass (lbm_adj_rho) over a per-cell scratch array
         self.rho_links = self.links is not None and any(len(t) > 3 and t[3] != 0 for lk in self.links for t in lk)
+        # link programs (boundaries.link_program): a Q-component scratch array per cell, the same second pass
+        self.programs = programs if self.links is not None and programs is not None and \
+            any(p is not None for p in programs) else None
+        self.link_pass = self.rho_links or self.programs is not None
         self._rho_bufs = {}
         self.target = target
         self._fns = {}
@@ -598,9 +646,9 @@ class LatticeKernels:
     def source(self, idx='int', addr='buf'):
         if self.target != 'gpu':
             return _emit(self.stencil, self.compressible, self.ct, self.walls, 'c', 'i64', 'ptr', self.links,
-                         self.force_model, self.force, self.force_field, self.trt)
+                         self.force_model, self.force, self.force_field, self.trt, self.programs)
         return _emit(self.stencil, self.compressible, self.ct, self.walls, 'hip', idx, addr, self.links,
-                     self.force_model, self.force, self.force_field, self.trt)
+                     self.force_model, self.force, self.force_field, self.trt, self.programs)
 
     # -- GPU ---------------------------------------------------------------------------------------
     def _gpu_fn(self, which, idx, addr, device):
@@ -709,8 +757,8 @@ class LatticeKernels:
                                                   ids.data_ptr() if ids is not None else 0]
         if force is not None:
             ptrs += [force.data_ptr()] + ([dforce.data_ptr()] if which == 'adj' else [])
-        if which == 'adj' and self.rho_links:
-            ptrs += [0]                                  # the density scratch array (patched per launch)
+        if which == 'adj' and self.link_pass:
+            ptrs += [0]                                  # the second pass's scratch array (patched per launch)
         fmt = 'Q' * len(ptrs) + 'iii' + code * len(strides) + 'q' * len(tensors) + \
             ('d' if self.ct == 'double' else 'f')
         args = _pack(fmt, *ptrs, Z, Y, X, *strides, *reach, float(omega))
@@ -718,12 +766,14 @@ class LatticeKernels:
         return plan
 
     def rho_buffer(self, t):
-        """The per-cell scratch array of the density pass (one per domain and device, reused: stream-ordered)."""
+        """The per-cell scratch array of the second adjoint pass (one per domain and device, reused: stream-ordered):
+        one value per cell (density-weighted links), Q per cell with link programs."""
         import torch
         key = (tuple(int(n) for n in t.shape[:self.stencil.D]), t.device, t.dtype)
         b = self._rho_bufs.get(key)
         if b is None:
-            b = self._rho_bufs[key] = torch.empty(key[0], dtype=t.dtype, device=t.device)
+            shape = ((self.stencil.Q,) if self.programs is not None else ()) + key[0]
+            b = self._rho_bufs[key] = torch.empty(shape, dtype=t.dtype, device=t.device)
         return b
 
     def rho_plan(self, out, mask, rho):
@@ -760,7 +810,7 @@ class LatticeKernels:
         if self.target != 'gpu':
             return self._cpu('adj', [src, g, out], omega, mask, ids, force, dforce)
         st = _stream(stream, src)
-        rho = self.rho_buffer(src) if self.rho_links else None
+        rho = self.rho_buffer(src) if self.link_pass else None
         self.plan('adj', [src, g, out], mask, omega, ids, force, dforce)(
             (src.data_ptr(), g.data_ptr(), out.data_ptr(), mask.data_ptr() if mask is not None else 0,
              ids.data_ptr() if ids is not None else 0) +
@@ -823,8 +873,9 @@ class LatticeKernels:
             ptrs += [force.ctypes.data] + ([dforce.ctypes.data] if which == 'adj' else [])
             strides += list(lattice_strides(force, D))
         rho = None
-        if which == 'adj' and self.rho_links:
-            rho = np.empty(shape[:D], self.dtype)          # the density pass's scratch (both passes in one call)
+        if which == 'adj' and self.link_pass:
+            # the second pass's scratch (both passes in one call)
+            rho = np.empty(((self.stencil.Q,) if self.programs is not None else ()) + shape[:D], self.dtype)
             ptrs += [rho.ctypes.data]
         ext = list(shape[:D]) if D == 3 else [1] + list(shape[:D])
         P = (ctypes.c_void_p * len(ptrs))(*ptrs)

@@ -29,14 +29,20 @@ families (the ``compressible`` branch differs between lbmpy versions): ``UBB(u, 
 link, ``pdf[c_d](ī_d) ← pdf(d) − 6 w_d (c_d · u) ρ(x)`` — affine in ALL the cell's pdfs. The lattice kernels fuse it
 too: the forward adds ``βρ·ρ(x)`` (ρ from the cell's own pre-streaming pdfs, loaded on cells next to a wall), the
 adjoint scatters ``γ v`` as for any link and adds the density term ``Σ_j γρ_j v_j`` to every component of the cell in
-a second pass (``lbm_adj_rho``; those entries are written by other threads in the first). Links of any other form
-(a pressure / outflow condition, a nonlinear link) raise.
+a second pass (``lbm_adj_rho``; those entries are written by other threads in the first).
+
+Links of any other form that read only the fluid cell's own pdfs — lbmpy's ``FixedDensity`` (a pressure boundary,
+quadratic in the cell's velocity), a link that weights another population of the cell, any user link of that
+kind — are LINK PROGRAMS (``link_program``): the forward value and its Jacobian row ``∂f_in/∂pdf(k)`` (read off
+the adjoint object's assignments) printed as C per (wall id, direction) and compiled into the same lattice kernels:
+the forward evaluates the link from the cell's own pre-streaming pdfs, the adjoint accumulates ``Σ_j J_jk v_j`` per
+component k of the cell and adds it in the second pass. A link that reads another cell or another field raises.
 """
 import numpy as np
 import sympy as sp
 
-__all__ = ['Boundary', 'NoSlip', 'UBB', 'AdjointNoSlip', 'AdjointBoundaryCondition', 'BoundaryHandling',
-           'make_slice', 'link_coefficients']
+__all__ = ['Boundary', 'NoSlip', 'UBB', 'FixedDensity', 'AdjointNoSlip', 'AdjointBoundaryCondition',
+           'BoundaryHandling', 'LBMethodView', 'make_slice', 'link_coefficients', 'link_program', 'link_form']
 
 
 class _MakeSlice:
@@ -127,6 +133,118 @@ class UBB(Boundary):
 
     def __repr__(self):
         return f'UBB({self.velocity!r}, {self.name!r}' + (', density_weighted=True)' if self.density_weighted else ')')
+
+
+class FixedDensity(Boundary):
+    """lbmpy's ``FixedDensity`` [ext] — a pressure boundary by anti-bounce-back with the symmetric part of the
+    equilibrium: ``pdf[c_d](ī_d) ← 2 feq_sym_d − pdf(d)`` with ``feq_sym_d = w_d ρ_w (1 + 4.5 (c_d·u)² − 1.5 u²)``
+    (compressible) or ``w_d (ρ_w + 4.5 (c_d·u)² − 1.5 u²)`` (incompressible). lbmpy prints the equilibrium's
+    subexpressions of the fluid cell's own pdfs with the density symbol replaced by the prescribed density, so the
+    velocity is ``u = Σ_k c_k pdf(k) / ρ_w`` (compressible) or ``Σ_k c_k pdf(k)``. ``compressible``: the method's
+    (None: read from ``lb_method.compressible``, which ``AutoDiffLatticeBoltzmannStep`` passes). Nonlinear in the
+    cell's pdfs: a link program (parity with lbmpy itself unpinned, lbmpy absent)."""
+
+    def __init__(self, density, name=None, compressible=None):
+        super().__init__(name if name is not None else 'FixedDensity')
+        self.density = density
+        self.compressible = compressible
+
+    def __call__(self, pdf_field, direction, lb_method, **kwargs):
+        st = _directions(lb_method)
+        comp = self.compressible if self.compressible is not None else getattr(lb_method, 'compressible', None)
+        if comp is None:
+            raise ValueError('FixedDensity: the method\'s compressibility is unknown (pass compressible=)')
+        c = st.directions[direction]
+        from .. import ps
+        rho_w = sp.sympify(self.density)
+        us = sp.symbols(f'fd_u_:{st.D}')
+        sub = []
+        for a in range(st.D):
+            m = sum(st.directions[k][a] * pdf_field(k) for k in range(st.Q) if st.directions[k][a])
+            sub.append(ps.Assignment(us[a], m / rho_w if comp else m))
+        cu = sum(ci * ua for ci, ua in zip(c, us) if ci)
+        usq = sum(ua * ua for ua in us)
+        poly = sp.Rational(9, 2) * cu * cu - sp.Rational(3, 2) * usq
+        w = sp.sympify(st.weights[direction])
+        feq_sym = w * rho_w * (1 + poly) if comp else w * (rho_w + poly)
+        link = pdf_field[c](st.inverse_direction_index(direction))
+        return sub + [ps.Assignment(link, 2 * feq_sym - pdf_field(direction))]
+
+    def program(self, lb_method):
+        """The link program (``link_program``'s form, adjoint = the derivative) written out: per direction d with
+        u = m/ρ_w (m = Σ_k c_k c_k-th pdf; incompressible u = m), ``L_d = 2 w_d ρ_w (1 + 4.5 (c_d·u)² − 1.5 u²) − c_d``
+        and ``∂L_d/∂c_k = 2 w_d (9 (c_d·u)(c_d·c_k) − 3 u·c_k) − δ_dk`` (the same in both families). Equal to the
+        general derivation (``tests/test_lbm.py::test_lbm_link_program_paths_agree``), at a fraction of its sympy
+        time (a D3Q19 program: milliseconds instead of seconds)."""
+        st = _directions(lb_method)
+        comp = self.compressible if self.compressible is not None else getattr(lb_method, 'compressible', None)
+        if comp is None:
+            raise ValueError('FixedDensity: the method\'s compressibility is unknown (pass compressible=)')
+        rw = float(sp.sympify(self.density))
+        pr = _c_printer()
+        D, Q = st.D, st.Q
+        dirs = [tuple(int(v) for v in c) for c in st.directions]
+        mom = []
+        for a in range(D):
+            t = ' '.join(('+ ' if dirs[k][a] > 0 else '- ') + f'c{k}' for k in range(Q) if dirs[k][a])
+            t = t[2:] if t.startswith('+ ') else t
+            mom.append(f'({t}) / (T){rw!r}' if comp else f'({t})')
+        ulines = tuple(f'const T fu{a} = {mom[a]};' for a in range(D))
+        usq = ' + '.join(f'fu{a} * fu{a}' for a in range(D))
+        out = []
+        for d in range(Q):
+            c = dirs[d]
+            if not any(c):
+                out.append(None)
+                continue
+            w = pr.doprint(sp.sympify(st.weights[d]))
+            cu = ' + '.join(f'{"" if v > 0 else "-"}fu{a}' for a, v in enumerate(c) if v)
+            lines = ulines + (f'const T fcu = {cu};', f'const T fusq = {usq};')
+            sym = f'(T){rw!r} * ((T)1 + (T)4.5 * fcu * fcu - (T)1.5 * fusq)' if comp else \
+                f'((T){rw!r} + (T)4.5 * fcu * fcu - (T)1.5 * fusq)'
+            val = f'(T)2 * {w} * {sym} - c{d}'
+            rows = []
+            for k in range(Q):
+                cc = sum(x * y for x, y in zip(c, dirs[k]))
+                uc = ' + '.join(f'{"" if v > 0 else "-"}fu{a}' for a, v in enumerate(dirs[k]) if v)
+                terms = []
+                if cc:
+                    terms.append(f'(T){9 * cc} * fcu')
+                if uc:
+                    terms.append(f'(T)-3 * ({uc})')
+                e = f'(T)2 * {w} * (' + ' + '.join(terms) + ')' if terms else None
+                if k == d:
+                    e = f'{e} - (T)1' if e else '(T)-1'
+                if e is not None:
+                    rows.append((k, lines, e))
+            out.append((lines, val, tuple(rows)))
+        return tuple(out)
+
+    def __hash__(self):
+        return hash(('FixedDensity', self.name, str(self.density), self.compressible))
+
+    def __eq__(self, other):
+        return isinstance(other, FixedDensity) and self.name == other.name and \
+            sp.sympify(self.density) == sp.sympify(other.density) and self.compressible == other.compressible
+
+    def __repr__(self):
+        return f'FixedDensity({self.density!r}, {self.name!r})'
+
+
+class LBMethodView:
+    """The ``lb_method`` a boundary sees (lbmpy passes its method object): the stencil's attributes plus the rule's
+    ``compressible`` flag (``FixedDensity`` needs it)."""
+
+    def __init__(self, stencil, compressible):
+        self.stencil = stencil
+        self.compressible = bool(compressible)
+
+    def __getattr__(self, name):
+        return getattr(self.__dict__['stencil'], name)
+
+    @property
+    def dim(self):
+        return self.stencil.D
 
 
 class AdjointNoSlip(Boundary):
@@ -267,6 +385,149 @@ def link_coefficients(forward_bc, adjoint_bc, lb_method):
     return tuple(out)
 
 
+def _c_printer():
+    """sympy → C for the link programs: constants as casts to the kernels' compute type ``T``, small integer powers
+    as products (no ``pow`` on the device)."""
+    from sympy.printing.c import C99CodePrinter
+
+    class P(C99CodePrinter):
+        def _print_Float(self, e):
+            return f'(T){float(e)!r}'
+
+        def _print_Rational(self, e):
+            return f'((T){int(e.p)} / (T){int(e.q)})'
+
+        def _print_Integer(self, e):
+            return f'(T){int(e)}'
+
+        def _print_Pow(self, e):
+            b, x = e.args
+            if x.is_Integer and 1 <= int(x) <= 4:
+                return '(' + ' * '.join([self.parenthesize(b, 100)] * int(x)) + ')'
+            if x.is_Integer and -4 <= int(x) <= -1:
+                return '((T)1 / (' + ' * '.join([self.parenthesize(b, 100)] * -int(x)) + '))'
+            raise NotImplementedError(f'link program: power {e}')
+    return P()
+
+
+def _program_code(exprs, nsyms):
+    """(temporaries, expressions) as C: ``const T lt_k = …;`` lines (common subexpressions) and one expression per
+    input, in the cell's own pdfs ``c0 … c{Q-1}``."""
+    pr = _c_printer()
+    tmp = sp.numbered_symbols('lt_')
+    reps, red = sp.cse([sp.sympify(e) for e in exprs], symbols=tmp)
+    lines = tuple(f'const T {pr.doprint(a)} = {pr.doprint(b)};' for a, b in reps)
+    return lines, tuple(pr.doprint(e) for e in red)
+
+
+def link_program(forward_bc, adjoint_bc, lb_method):
+    """Per direction ``d`` of the stencil, for a link that reads only the fluid cell's own pdfs: ``None`` (the rest
+    population) or ``(lines, value, jac)`` — C source of the forward link value ``f_{ī_d}(x + c_d) = L_d(pdf(x))``
+    (``lines``: temporaries, ``value``: an expression in ``c0 … c{Q-1}``, the cell's own pre-streaming pdfs) and of
+    the adjoint link's Jacobian row ``((k, lines_k, J_dk), …)`` read off the adjoint object's assignments
+    ``diffpdf(k) ← J_dk · diffpdf[c_d](ī_d)`` (J_dk may depend on the cell's pdfs; zero entries left out).
+    Raises ``NotImplementedError`` for a link that reads another cell or another field."""
+    from .. import ps
+    from .._adjoint_field import AdjointField
+    st = _directions(lb_method)
+    f = ps.fields(f'__pdf({st.Q}): [{st.D}D]')
+    g = AdjointField(f)
+    cs = sp.symbols(f'c0:{st.Q}')
+    own = {f(k): cs[k] for k in range(st.Q)}
+    # (a program reads only the cell's pdfs: the adjoint object's constant / time-constant fields change nothing)
+    derived = isinstance(adjoint_bc, AdjointBoundaryCondition) and adjoint_bc.forward_condition == forward_bc and \
+        type(adjoint_bc) is AdjointBoundaryCondition
+    if derived and callable(getattr(forward_bc, 'program', None)):
+        return forward_bc.program(lb_method)          # written out by the boundary (FixedDensity)
+    out = []
+    for d in range(st.Q):
+        c = st.directions[d]
+        if not any(c):
+            out.append(None)
+            continue
+        inv = st.inverse_direction_index(d)
+        fwd = list(forward_bc(f, d, lb_method))
+        if any(hasattr(a.lhs, 'field') and a.lhs != f[c](inv) for a in fwd):
+            raise NotImplementedError(f'{forward_bc!r}: a link writes one population of the wall cell, got {fwd}')
+        rhs = _inline(fwd, f[c](inv))
+        if rhs is None:
+            raise NotImplementedError(f'{forward_bc!r}: no link assignment to pdf[c_d](inv_d) in {fwd}')
+        rhs = sp.sympify(rhs)
+        bad = [a for a in rhs.atoms(ps.Field.Access) if a not in own]
+        if bad or (rhs.free_symbols - set(rhs.atoms(ps.Field.Access))):
+            raise NotImplementedError(f'{forward_bc!r}: the lattice kernels take links of the fluid cell\'s own pdfs '
+                                      f'and constants, got {rhs}')
+        value = rhs.xreplace(own)
+        lines, (val,) = _program_code([value], st.Q)
+        if derived:
+            # the adjoint object is the transposed derivative of this link (AdjointBoundaryCondition): its Jacobian
+            # row straight from the forward expression (what the transposed AD prints, without its cost per link)
+            rows = []
+            try:                                    # polynomial links (FixedDensity: quadratic): fast derivatives
+                poly = sp.Poly(value, *cs)
+                grads = [poly.diff(ck).as_expr() for ck in cs]
+            except sp.PolynomialError:
+                grads = [sp.diff(value, ck) for ck in cs]
+            pr = _c_printer()
+            for k, jk in enumerate(grads):
+                if jk != 0:
+                    rows.append((k, (), pr.doprint(jk)))
+            out.append((lines, val, tuple(rows)))
+            continue
+        bwd = adjoint_bc(g, d, lb_method)
+        allb = list(getattr(bwd, 'all_assignments', bwd))
+        if any(hasattr(a.lhs, 'field') and a.lhs not in [g(k) for k in range(st.Q)] for a in allb):
+            raise NotImplementedError(f'{adjoint_bc!r}: adjoint assignments beyond diffpdf(k) <- J_k * '
+                                      f'diffpdf[c_d](inv_d): {allb}')
+        jac = []
+        gv = sp.Symbol('__gv')
+        for k in range(st.Q):
+            r = _inline(allb, g(k))
+            if r is None:
+                continue
+            r = sp.expand(sp.sympify(r).xreplace({g[c](inv): gv}))
+            jk = sp.diff(r, gv)
+            if sp.expand(r - jk * gv) != 0:
+                raise NotImplementedError(f'{adjoint_bc!r}: adjoint link of pdf({k}) is not linear in '
+                                          f'diffpdf[c_d](inv_d): {r}')
+            if any(a not in own for a in jk.atoms(ps.Field.Access)):
+                raise NotImplementedError(f'{adjoint_bc!r}: adjoint coefficient of pdf({k}) reads {jk}')
+            jk = sp.expand(jk.xreplace(own))
+            if jk != 0:
+                jac.append((k, jk))
+        jrows = []
+        for k, jk in jac:
+            jl, (je,) = _program_code([jk], st.Q)
+            jrows.append((k, jl, je))
+        out.append((lines, val, tuple(jrows)))
+    return tuple(out)
+
+
+_FORMS = {}
+
+
+def link_form(forward_bc, adjoint_bc, lb_method):
+    """``('affine', link_coefficients(...))`` — the fused (α, β, γ, βρ, γρ) form — or ``('program',
+    link_program(...))``; raises ``NotImplementedError`` for a link neither takes. Memoised per (boundary pair,
+    stencil, compressibility): a D3Q19 ``FixedDensity`` program takes seconds of sympy."""
+    st = _directions(lb_method)
+    key = (forward_bc, adjoint_bc, type(adjoint_bc), getattr(st, 'name', None), st.Q,
+           getattr(lb_method, 'compressible', None))
+    try:
+        hit = _FORMS.get(key)
+    except TypeError:                       # an unhashable user boundary: no memo
+        key, hit = None, None
+    if hit is not None:
+        return hit
+    try:
+        res = 'affine', link_coefficients(forward_bc, adjoint_bc, lb_method)
+    except NotImplementedError:
+        res = 'program', link_program(forward_bc, adjoint_bc, lb_method)
+    if key is not None:
+        _FORMS[key] = res
+    return res
+
+
 class BoundaryHandling:
     """The wall flags of one lattice (``uint8``, one per cell: 0 = fluid, k ≥ 1 = the k-th boundary object set)
     and lbmpy's ``set_boundary`` surface over them. The forward and the adjoint kernels read the same flags, so the
@@ -348,18 +609,26 @@ class BoundaryHandling:
             self._on_change()
 
     def link_tables(self, lb_method):
-        """Per flag id ≥ 1: the ``link_coefficients`` of its (forward, adjoint) boundary pair, as a tuple, or None
-        when every id is a plain bounce-back (α = γ = 1, β = 0: the kernels' fast path, no id loads)."""
+        """``(tables, programs)``. ``tables``: per flag id ≥ 1 the ``link_coefficients`` of its (forward, adjoint)
+        boundary pair, or None when every id is a plain bounce-back (α = γ = 1, β = 0: the kernels' fast path, no id
+        loads). ``programs``: None, or per flag id the ``link_program`` of a boundary the fused form does not take
+        (None for the others; its table row is all zeros, so the fused path contributes nothing)."""
         objs = self.objects()
-        tables = [None]
+        st = _directions(lb_method)
+        zero = tuple((0.0, 0.0, 0.0, 0.0, 0.0) for _ in range(st.Q))
+        tables, programs = [None], [None]
         plain = True
         for k in range(1, len(objs)):
-            obj = objs[k]
-            t = link_coefficients(obj, self.adjoints[k], lb_method)
+            kind, t = link_form(objs[k], self.adjoints[k], lb_method)
+            if kind == 'program':
+                tables.append(zero)
+                programs.append(t)
+                plain = False
+                continue
             plain &= all(a == 1.0 and b == 0.0 and g == 1.0 and br == 0.0 and gr == 0.0 for a, b, g, br, gr in t)
             tables.append(t)
+            programs.append(None)
         if plain:
-            return None
-        st = _directions(lb_method)
+            return None, None
         tables[0] = tuple((1.0, 0.0, 1.0, 0.0, 0.0) for _ in range(st.Q))
-        return tuple(tables)
+        return tuple(tables), (tuple(programs) if any(p is not None for p in programs) else None)

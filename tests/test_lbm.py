@@ -472,10 +472,22 @@ def test_boundary_links_and_generic_adjoint():
                                   pdf_field(direction) - 0.1 * pdf_field(0))]
     with pytest.raises(NotImplementedError):
         lbm.link_coefficients(Skewed(), lbm.AdjointBoundaryCondition(Skewed()), st)
+    # ... it is a link program instead: the forward value and the Jacobian row of the cell's own pdfs
+    kind, prog = lbm.link_form(Skewed(), lbm.AdjointBoundaryCondition(Skewed()), st)
+    assert kind == 'program' and prog[0] is None
+    lines, val, jac = prog[6]
+    assert sorted(k for k, _, _ in jac) == [0, 6] and dict((k, e) for k, _, e in jac)[6] in ('(T)1', '(T)1.0')
+
+    class Remote(lbm.Boundary):
+        """Reads a population of another cell: neither form."""
+        def __call__(self, pdf_field, direction, lb_method, **kw):
+            c = st.directions[direction]
+            return [ps.Assignment(pdf_field[c](st.inverse_direction_index(direction)), pdf_field[-c[0], -c[1]](direction))]
     step = lbm.AutoDiffLatticeBoltzmannStep(lbm.create_lb_update_rule('D2Q9', compressible=True),
                                             domain_size=(6, 5), relaxation_rate=1.0, target='cpu')
     with pytest.raises(NotImplementedError):
-        step.set_boundary_including_adjoint(Skewed())
+        step.set_boundary_including_adjoint(Remote())
+    step.set_boundary_including_adjoint(Skewed(), lbm.make_slice[0, :])
 
 
 @pytest.mark.parametrize('adjoint', ['derived', 'noslip'])
@@ -997,3 +1009,159 @@ def test_lbm_density_weighted_ubb_gpu(compressible, trt):
     out.backward(torch.tensor(g, device='cuda'))
     assert float((out.detach().cpu() - ref.detach()).abs().max()) <= 1e-12 * np.abs(f0).max()
     assert float((x.grad.cpu() - gref).abs().max()) <= 1e-11 * float(gref.abs().max())
+
+
+# --- pressure boundaries (lbmpy FixedDensity) and other link programs ----------------------------------------
+RHO_IN, RHO_OUT = 1.02, 0.98
+
+
+def _pressure_channel(stencil, shape, compressible, target, trt=False, dtype='float64'):
+    """A channel along axis 0: no-slip walls on both ends of axis 1 (and axis 2), FixedDensity inlet / outlet
+    planes at the ends of axis 0 (lbmpy's pressure boundary, a link program of the lattice kernels)."""
+    kw = dict(method='trt') if trt else {}
+    rule = lbm.create_lb_update_rule(stencil, compressible=compressible, data_type=dtype, **kw)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.3, target=target)
+    D = len(shape)
+    wall = np.zeros(shape, bool)
+    for ax in range(1, D):
+        for end in (0, -1):
+            sl = [slice(None)] * D
+            sl[ax] = end
+            step.set_boundary_including_adjoint(lbm.NoSlip(), tuple(sl))
+            wall[tuple(sl)] = True
+    inner = tuple(slice(1, -1) for _ in range(1, D))
+    step.set_boundary_including_adjoint(lbm.FixedDensity(RHO_IN, name='inlet'), (0,) + inner)
+    step.set_boundary_including_adjoint(lbm.FixedDensity(RHO_OUT, name='outlet'), (-1,) + inner)
+    pressure = np.zeros(shape, bool)
+    pressure[(0,) + inner] = pressure[(-1,) + inner] = True
+    wall |= pressure
+    rho_w = np.ones(shape)
+    rho_w[(0,) + inner], rho_w[(-1,) + inner] = RHO_IN, RHO_OUT
+    assert np.array_equal(step.boundary_handling.flags != 0, wall)
+    K = step._lattice_kernels()
+    assert K.programs is not None and K.link_pass
+    return step, wall, pressure, rho_w, (OL.trt_odd_rate(1.3) if trt else None)
+
+
+def _pressure_ref(f0, step_args, stencil, compressible, T, g, device='cpu'):
+    import torch
+    _, wall, pressure, rho_w, w_odd = step_args
+    ft = torch.tensor(f0, requires_grad=True, device=device)
+    tw = [torch.tensor(a, device=device) for a in (wall, pressure, rho_w)]
+    ref = OL.run_pressure_walls(ft, 1.3, *tw, T, stencil, compressible, xp=torch, omega_odd=w_odd)
+    (gref,) = torch.autograd.grad(ref, ft, torch.tensor(g, device=device))
+    return ref.detach().cpu().numpy(), gref.cpu().numpy()
+
+
+PRESSURE_CASES = [('D2Q9', (16, 9), True, False), ('D2Q9', (15, 10), False, False), ('D2Q9', (12, 9), True, True),
+                  ('D3Q19', (9, 6, 5), True, False)]
+
+
+@pytest.mark.parametrize('stencil,shape,compressible,trt', PRESSURE_CASES)
+def test_lbm_pressure_channel_cpu(stencil, shape, compressible, trt):
+    """A pressure-driven channel (FixedDensity inlet / outlet, no-slip walls) on the C lattice kernels: T steps vs
+    the anti-bounce-back restatement (oracle/lbm.py ``run_pressure_walls``), the adjoint (link-program Jacobians
+    through the second pass) vs torch's reverse mode through it."""
+    T = 5
+    args = _pressure_channel(stencil, shape, compressible, 'cpu', trt)
+    step = args[0]
+    f0 = _init(stencil, shape, compressible, seed=31)
+    g = np.random.default_rng(32).standard_normal(f0.shape)
+    ref, gref = _pressure_ref(f0, args, stencil, compressible, T, g)
+    step.set_pdfs(f0)
+    step.run(T, record=True)
+    assert np.abs(step.pdf_array - ref).max() <= 1e-13 * np.abs(f0).max()
+    # the pressure links are in: the same walls bouncing back everywhere give another flow
+    import torch
+    still = OL.run_walls(torch.tensor(f0), 1.3, torch.tensor(args[1]), T, stencil, compressible, xp=torch,
+                         omega_odd=args[4]).numpy()
+    assert np.abs(ref - still).max() > 1e-4
+    step.set_adjoint_pdfs(g)
+    step.run_backward(T)
+    assert np.abs(step.adjoint_pdf_array - gref).max() <= 1e-12 * np.abs(gref).max()
+
+
+def test_lbm_pressure_drives_flow():
+    """Physics check of the pressure boundary: from rest, a density difference between inlet and outlet drives a
+    flow from high to low density along the channel (positive mean axis-0 velocity in the interior)."""
+    shape = (24, 11)
+    step, wall, *_ = _pressure_channel('D2Q9', shape, True, 'cpu')
+    f0 = OL.equilibrium(np.ones(shape), np.zeros(shape + (2,)), 'D2Q9', True)
+    step.set_pdfs(f0)
+    step.run(150)
+    f = step.pdf_array
+    dirs = OL.D2Q9[0]
+    rho = f.sum(-1)
+    ux = sum(c[0] * f[..., i] for i, c in enumerate(dirs)) / rho
+    interior = ux[2:-2, 2:-2]
+    assert interior.mean() > 1e-4
+    assert rho[1, 5] > rho[-2, 5]
+
+
+def test_lbm_link_program_paths_agree():
+    """The link program of FixedDensity three ways agree: written out by the boundary (``FixedDensity.program``,
+    what the kernels use), differentiated by sympy from the printed link (any ``AdjointBoundaryCondition``), and read
+    off the adjoint object's assignments (the transposed AD of the link, the general path)."""
+    st = lbm.LBStencil('D2Q9')
+    view = lbm.boundaries.LBMethodView(st, True)
+    fd = lbm.FixedDensity(1.03)
+    fast = lbm.link_program(fd, lbm.AdjointBoundaryCondition(fd), view)
+    # a subclass of the adjoint object: not taken as the plain derived adjoint, so its assignments are parsed
+
+    class Parsed(lbm.AdjointBoundaryCondition):
+        pass
+    slow = lbm.link_program(fd, Parsed(fd), view)
+
+    class NoProgram(lbm.FixedDensity):
+        program = None                                  # the derivative of the printed link by sympy
+    mid = lbm.link_program(NoProgram(1.03), lbm.AdjointBoundaryCondition(NoProgram(1.03)), view)
+    rng = np.random.default_rng(5)
+    env = {f'c{q}': v for q, v in enumerate(rng.uniform(0.05, 0.3, 9))}
+
+    def ev(lines, e):
+        loc = dict(env)
+        for ln in lines:
+            name, rhs = ln[len('const T '):].rstrip(';').split(' = ', 1)
+            loc[name] = eval(rhs.replace('(T)', ''), {}, loc)
+        return eval(e.replace('(T)', ''), {}, loc)
+    for a, b, m in zip(fast, slow, mid):
+        assert (a is None) == (b is None) == (m is None)
+        if a is not None:
+            assert ev(a[0], a[1]) == pytest.approx(ev(m[0], m[1]), rel=1e-13)
+            jm = {k: ev(l, e) for k, l, e in m[2]}
+            assert all(jm[k] == pytest.approx(ev(l, e), rel=1e-12, abs=1e-15) for k, l, e in a[2])
+        if a is None:
+            continue
+        assert ev(a[0], a[1]) == pytest.approx(ev(b[0], b[1]), rel=1e-13)
+        ja, jb = {k: ev(l, e) for k, l, e in a[2]}, {k: ev(l, e) for k, l, e in b[2]}
+        assert ja.keys() == jb.keys() and all(ja[k] == pytest.approx(jb[k], rel=1e-12, abs=1e-15) for k in ja)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('stencil,shape,compressible,trt,dtype', [('D2Q9', (70, 33), True, False, 'float64'),
+                                                                   ('D2Q9', (64, 40), False, True, 'float32'),
+                                                                   ('D3Q19', (20, 12, 10), True, False, 'float64')])
+def test_lbm_pressure_channel_gpu(stencil, shape, compressible, trt, dtype):
+    """The pressure-driven channel on the HIP lattice kernels (link programs compiled in, two adjoint passes),
+    through ``run`` / ``run_backward`` and the timestep op, vs the oracle and torch's reverse mode."""
+    import torch
+    T = 6
+    args = _pressure_channel(stencil, shape, compressible, 'gpu', trt, dtype)
+    step = args[0]
+    f0 = _init(stencil, shape, compressible, seed=33)
+    g = np.random.default_rng(34).standard_normal(f0.shape)
+    ref, gref = _pressure_ref(f0, args, stencil, compressible, T, g)
+    tdt = getattr(torch, dtype)
+    tol = 1e-12 if dtype == 'float64' else 2e-5
+    step.set_pdfs(torch.tensor(f0, dtype=tdt, device='cuda'))
+    step.run(T, record=True)
+    assert np.abs(step.pdf_array.double().cpu().numpy() - ref).max() <= tol * np.abs(f0).max()
+    step.set_adjoint_pdfs(torch.tensor(g, dtype=tdt, device='cuda'))
+    step.run_backward(T)
+    assert np.abs(step.adjoint_pdf_array.double().cpu().numpy() - gref).max() <= 10 * tol * np.abs(gref).max()
+    op = step.create_timestep_op(T)
+    x = torch.tensor(f0, dtype=tdt, device='cuda', requires_grad=True)
+    out = op.apply(x)
+    out.backward(torch.tensor(g, dtype=tdt, device='cuda'))
+    assert float((out.detach().double().cpu() - torch.tensor(ref)).abs().max()) <= tol * np.abs(f0).max()
+    assert float((x.grad.double().cpu() - torch.tensor(gref)).abs().max()) <= 10 * tol * np.abs(gref).max()
