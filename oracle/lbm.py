@@ -198,14 +198,16 @@ def run_moving_walls(f, omega, wall, wall_velocity, steps, stencil='D2Q9', compr
     return f
 
 
-def stream_pressure_walls(f, stencil, wall, pressure, rho_wall, compressible, xp, wall_velocity=None):
+def stream_pressure_walls(f, stencil, wall, pressure, rho_wall, compressible, xp, wall_velocity=None,
+                          density_weighted=False):
     """Pull streaming with bounce-back walls and pressure cells (lbmpy's ``FixedDensity`` [ext], anti-bounce-back):
     where ``x − c_i`` is a pressure cell of density ``ρ_w`` (``pressure``: bool over the domain, a subset of
     ``wall``; ``rho_wall``: per cell, read at pressure cells), with ``d = ī`` the direction that left ``x`` towards
     it, ``f_i(x) = 2 w_d ρ_w (1 + 4.5 (c_d·u)² − 1.5 u²) − f_d(x)`` (incompressible: ``2 w_d (ρ_w + 4.5 (c_d·u)² −
     1.5 u²) − f_d(x)``) with ``u = Σ_k c_k f_k(x) / ρ_w`` (incompressible: without the division) of the fluid cell's
     own pdfs — lbmpy prints the equilibrium's velocity subexpression with its density symbol replaced by ρ_w. Other
-    wall cells bounce back (moving with ``wall_velocity`` where given, as ``stream_moving_walls``)."""
+    wall cells bounce back (moving with ``wall_velocity`` where given, as ``stream_moving_walls``, its wall term
+    times the fluid cell's density with ``density_weighted``)."""
     dirs, w = SETS[stencil]
     inv = inverse(stencil)
     D = len(dirs[0])
@@ -222,8 +224,8 @@ def stream_pressure_walls(f, stencil, wall, pressure, rho_wall, compressible, xp
         rw = _roll_all(xp, rho_wall, c)
         bounced = f[..., d]
         if wall_velocity is not None:
-            bounced = bounced + 6 * float(w[i]) * sum(ca * _roll_all(xp, wall_velocity[..., a], c)
-                                                       for a, ca in enumerate(c) if ca)
+            cuw = sum(ca * _roll_all(xp, wall_velocity[..., a], c) for a, ca in enumerate(c) if ca)
+            bounced = bounced + 6 * float(w[i]) * (cuw * f.sum(-1) if density_weighted else cuw)
         u = [ma / rw if compressible else ma for ma in m]
         cu = sum(dirs[d][a] * u[a] for a in range(D) if dirs[d][a])
         usq = sum(ua * ua for ua in u)
@@ -234,13 +236,14 @@ def stream_pressure_walls(f, stencil, wall, pressure, rho_wall, compressible, xp
 
 
 def run_pressure_walls(f, omega, wall, pressure, rho_wall, steps, stencil='D2Q9', compressible=False, xp=None,
-                       omega_odd=None):
-    """``steps`` stream-pull-collide steps with no-slip walls and pressure cells; wall cells keep their state."""
+                       omega_odd=None, wall_velocity=None, density_weighted=False):
+    """``steps`` stream-pull-collide steps with (moving) bounce-back walls and pressure cells; wall cells keep their
+    state."""
     if xp is None:
         import numpy as xp
     keep = wall[..., None] if xp.__name__ != 'torch' else wall.unsqueeze(-1)
     for _ in range(steps):
-        new = collide(stream_pressure_walls(f, stencil, wall, pressure, rho_wall, compressible, xp), omega, stencil,
-                      compressible, xp, omega_odd=omega_odd)
+        new = collide(stream_pressure_walls(f, stencil, wall, pressure, rho_wall, compressible, xp, wall_velocity,
+                                            density_weighted), omega, stencil, compressible, xp, omega_odd=omega_odd)
         f = xp.where(keep, f, new)
     return f

@@ -36,7 +36,7 @@ import sympy as sp
 
 from .. import ps
 from ..autodiff import AutoDiffOp
-from ._lattice_kernels import LatticeKernels, neighbour_mask
+from ._lattice_kernels import LatticeKernels, fix_cells, neighbour_mask
 from ._method import LBStencil
 from .boundaries import (AdjointBoundaryCondition, AdjointNoSlip, Boundary, BoundaryHandling, LBMethodView,  # noqa: F401
                          NoSlip, link_form)
@@ -66,6 +66,7 @@ def _lattice_sweeps(step, which, launches, force=None, dforce=None):
     K = step._lattice_kernels()
     mask = step._flag_arg()
     ids = step._ids_arg()
+    cells = step._cells_arg()
     om = step._omega_of()
     mptr = (mask.data_ptr() if mask is not None else 0, ids.data_ptr() if ids is not None else 0)
     if force is not None:
@@ -81,9 +82,13 @@ def _lattice_sweeps(step, which, launches, force=None, dforce=None):
         if plan is None:
             plan = plans[sig] = K.plan(which, list(ts), mask, om, ids, force, dforce if which == 'adj' else None)
         plan(tuple(t.data_ptr() for t in ts) + mptr, stream, om)
+        # link-program walls (HIP): the fix-up kernels over the cells next to them
+        gs = K.fix_launch(which, list(ts), mask, om, ids, force, dforce if which == 'adj' else None, cells, stream)
         if rho is not None:
-            # the second pass of density-weighted walls / link programs, on this launch's output
-            K.rho_plan(ts[2], mask, rho)((ts[2].data_ptr(), mask.data_ptr(), rho.data_ptr()), stream)
+            # the second pass of density-weighted walls (and, on the CPU, link programs) on this launch's output
+            K.rho_pass(ts[2], mask, rho, ts[0], ids, stream)
+        if which == 'adj':
+            K.fix2_launch(ts[2], cells, gs, stream)
 
 
 def _plain_force_field(force, D):
@@ -392,11 +397,28 @@ class AutoDiffLatticeBoltzmannStep:
             if self._gpu:
                 torch = _torch()
                 dev = self._device or torch.device('cuda', torch.cuda.current_device())
+                fix = self._fix_mask()
                 self._flag_dev = neighbour_mask(torch.from_numpy(self._boundary.flags.copy()).to(dev), self.method,
-                                                torch)
+                                                torch, fix=fix)
+                self._cells_dev = None if fix is None else \
+                    torch.from_numpy(np.flatnonzero(fix.ravel()).astype(np.int32)).to(dev)
             else:
                 self._flag_dev = neighbour_mask(self._boundary.flags, self.method, np)
         return self._flag_dev
+
+    def _fix_mask(self):
+        """The fluid cells next to link-program walls (``FIX_BIT``: the HIP fix-up kernels' list), None if no
+        boundary is a link program."""
+        progs = self._programs()
+        if progs is None:
+            return None
+        return fix_cells(self._boundary.flags, self.method, [k for k, p in enumerate(progs) if p is not None])
+
+    def _cells_arg(self):
+        """The fix-up kernels' cell list (int32 on the device), None without link programs (or on the CPU)."""
+        if not self._gpu or self._flag_arg() is None:
+            return None
+        return getattr(self, '_cells_dev', None)
 
     def _links(self):
         """The wall kernels' link tables (None: every wall a plain bounce-back, or no walls), derived once per
@@ -448,7 +470,7 @@ class AutoDiffLatticeBoltzmannStep:
     def _fwd(self, src, dst, extra):
         if self._lattice is not None:
             return self._lattice_kernels().forward(src, dst, self._omega_of(), self._flag_arg(), ids=self._ids_arg(),
-                                                   force=self._force_arg(extra))
+                                                   force=self._force_arg(extra), cells=self._cells_arg())
         kf, _ = self._kernels()
         kf(**{self._pdf_arr_name: src, self._tmp_arr_name: dst}, **extra, **self.kernel_params)
 
@@ -471,7 +493,8 @@ class AutoDiffLatticeBoltzmannStep:
                     raise ValueError(f"the force field's adjoint '{name}' needs an array (extra_adj), accumulated into")
                 dforce = extra_adj[name]
             return self._lattice_kernels().adjoint(src, diffdst, diffsrc, self._omega_of(), self._flag_arg(),
-                                                   ids=self._ids_arg(), force=self._force_arg(extra), dforce=dforce)
+                                                   ids=self._ids_arg(), force=self._force_arg(extra), dforce=dforce,
+                                                   cells=self._cells_arg())
         _, kb = self._kernels()
         kb(**{self._pdf_arr_name: src, 'diff' + self._tmp_arr_name: diffdst, 'diff' + self._pdf_arr_name: diffsrc},
            **extra, **extra_adj, **self.kernel_params)

@@ -29,6 +29,7 @@ and a C loop nest (``use_cuda=False`` / ``target='cpu'``) compiled by gcc.
 """
 import ctypes
 import os
+import re
 import struct
 
 import numpy as np
@@ -42,10 +43,11 @@ def _c(v):
 
 
 SELF_BIT = 30      # bit of a cell's neighbour mask: the cell itself is an obstacle (bits 0..Q-1: x − c_i is one)
+FIX_BIT = 31       # ... the cell is a fluid cell next to a wall with a link program (the HIP fix-up kernels' cells)
 
 
 def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=None, force_model=None, force=None,
-          force_field=False, trt=None, programs=None):
+          force_field=False, trt=None, programs=None, mode='inline'):
     """Source of the forward (``lbm_fwd``) and adjoint (``lbm_adj``) kernels.
 
     ``addr='buf'`` (HIP): every pdf array is one buffer resource (its bytes below 2³²); a component's plane
@@ -73,8 +75,15 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     equilibrium sums over h_i = a g_i + b g_ī: ``v_j = (1 − a) g_j − b g_ĵ + A_h + Σ_a B_h,a ∂u_a/∂f_j``.
     ``programs``: per wall id None or the boundary's ``link_program`` (links of the cell's own pdfs the fused form does
     not take, ``boundaries.link_program``; their table rows are zeros): the forward evaluates the link from the
-    cell's own pdfs ``c0 … c{Q-1}``, the adjoint accumulates ``G_k = Σ_j J_jk v_j`` over the cell's program links and a
-    second pass (``lbm_adj_rho``, with the density term folded into ``G``) adds ``G_k`` to component k of the cell."""
+    cell's own pdfs ``c0 … c{Q-1}`` (loaded inside the link's branch), the adjoint's first pass stores ``v_j`` of each
+    program-linked component j to a per-cell scratch array and the second pass (``lbm_adj_rho``) adds
+    ``Σ_j J_jk(c) v_j`` to component k of the cell — the Jacobians are evaluated there, on the cells next to a wall,
+    not in the first pass, whose registers they would take on every cell (``mode='inline'``, the C target).
+    HIP (``mode='main'`` / ``'fix'``): the main kernels carry no program code and skip the cells marked ``FIX_BIT``
+    (fluid cells next to a program wall); list-driven fix-up kernels recompute exactly those cells with the
+    programs — forward (``lbm_fwd_fix``), adjoint with the regular scatter plus ``G_k = Σ_j J_jk v_j`` into a
+    per-listed-cell scratch (``lbm_adj_fix``), then ``out_k(x) += G_k`` (``lbm_adj_fix2``, after every other store of
+    the step) — so the lattice's bulk runs the plain wall kernels."""
     D, Q = stencil.D, stencil.Q
     dirs = [tuple(d) for d in stencil.directions]
     w = [float(x) for x in stencil.weights]
@@ -101,7 +110,11 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     # forward f_j += βρ·ρ(x); the adjoint adds Σ_j βρ_j v_j to every component of the cell in a second pass
     rho_links = links is not None and any(len(t) > 3 and t[3] != 0 for lk in links for t in lk)
     gen = links is not None and programs is not None and any(p is not None for p in programs)
-    two = rho_links or gen                  # the adjoint's second pass over a per-cell scratch array
+    fix = mode == 'fix'
+    if fix and not gen:
+        raise ValueError('fix-up kernels need link programs')
+    # the adjoint's second pass over a per-cell scratch array: density-weighted links (any mode), link programs inline
+    two = rho_links or (gen and mode == 'inline')
     if links is not None:
         # per (wall id, pulled component j): the link of direction d = ī_j (the population that left x towards the
         # wall cell x + c_d = x − c_j comes back as j)
@@ -218,6 +231,11 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             return []
         return [(wid, pg[inv[i]]) for wid, pg in enumerate(programs) if pg is not None and pg[inv[i]] is not None]
 
+    def own_loads(code, rd):
+        """Loads of the cell's own pdfs a program's code reads (``const T c<q> = …;``; ``rd(q)``: the load)."""
+        used = sorted({int(m) for m in re.findall(r'\bc(\d+)\b', code)})
+        return ' '.join(f'const {ct} c{q} = {rd(q)};' for q in used)
+
     def pull_loads(L, prefix, arr):
         for i in range(Q):
             k = key(dirs[i])
@@ -243,21 +261,15 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                         L.append(f'  if ((msk >> {i}) & 1u) switch (id{i}) {{')
                         for wid, pg in cases:
                             lines, val, _ = pg
-                            L.append(f'    case {wid}: {{ ' + ' '.join(lines) + f' f{i} = {val}; }} break;')
+                            body = ' '.join(lines) + f' f{i} = {val};'
+                            ld = own_loads(body, lambda q: load(prefix, arr, q, f'{prefix}o_{centre}'))
+                            L.append(f'    case {wid}: {{ {ld} {body} }} break;')
                         L.append('    default: break;\n  }')
             else:
                 L.append(f'  const {ct} f{i} = {load(prefix, arr, i, f"{prefix}o_{k}")};')
 
     def cell_density(L, prefix, arr):
-        """ρ(x) of the cell's own (pre-streaming) pdfs, for density-weighted links, on cells next to a wall (with
-        link programs: the cell's own pdfs c0 … c{Q-1} themselves, which the programs read)."""
-        if gen:
-            L.append(f'  {ct} ' + ', '.join(f'c{q} = 0' for q in range(Q)) + ';')
-            L.append(f'  if (msk & {low}) {{ ' + ' '.join(f'c{q} = {load(prefix, arr, q, f"{prefix}o_{centre}")};'
-                                                           for q in range(Q)) + ' }')
-            if rho_links:
-                L.append(f'  const {ct} rs = ' + ' + '.join(f'c{q}' for q in range(Q)) + ';')
-            return
+        """ρ(x) of the cell's own (pre-streaming) pdfs, for density-weighted links, on cells next to a wall."""
         if not rho_links:
             return
         L.append(f'  {ct} rs = 0;')
@@ -316,8 +328,13 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     else:
         fstr_unused = ''
     cell = '((IDX)z * Y + y) * X + x' if D == 3 else '(IDX)y * X + x'
+    ncells = '(IDX)Z * Y * X'
     sig_rho = ('T* __restrict__ out, const unsigned* __restrict__ nbmask, const T* __restrict__ rho_adj, const int Z, '
                'const int Y, const int X, const IDX o_q, const IDX o_z, const IDX o_y, const IDX o_x')
+    if gen and mode == 'inline':
+        # the programs' Jacobians read the cell's own pdfs and the neighbours' wall ids
+        sig_rho += (', const T* __restrict__ src, const unsigned char* __restrict__ wallid, '
+                    'const IDX s_q, const IDX s_z, const IDX s_y, const IDX s_x')
 
     # ---- forward
     L.append(f'{fn} void lbm_fwd_cell({sig_fwd}, const int z, const int y, const int x)\n{{')
@@ -332,10 +349,12 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     dcoff = 'dcb' if buf else 'dc'
     if walls:
         L.append(f'  const unsigned msk = nbmask[{cell}];')
-        L.append(f'  if (msk >> {SELF_BIT}) {{')
+        L.append(f'  if ((msk >> {SELF_BIT}) & 1u) {{')
         for i in range(Q):
             L.append('    ' + store('d', 'dst', i, dcoff, load('s', 'src', i, f'so_{centre}')))
         L.append('    return;\n  }')
+        if mode == 'main':
+            L.append(f'  if ((msk >> {FIX_BIT}) & 1u) return;      // next to a link-program wall: the fix-up kernel')
     force_loads(L)
     cell_density(L, 's', 'src')
     pull_loads(L, 's', 'src')
@@ -368,7 +387,8 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     L.append('}')
 
     # ---- adjoint (scatter to where the forward pulled from)
-    L.append(f'{fn} void lbm_adj_cell({sig_adj}, const int z, const int y, const int x)\n{{')
+    L.append(f'{fn} void lbm_adj_cell({sig_adj}, const int z, const int y, const int x'
+             + (f', {ct}* __restrict__ Gs, const int t' if fix else '') + ')\n{')
     L.append(f'  (void)Z; (void)s_bytes; (void)g_bytes; (void)o_bytes; (void)wallid; {fstr_unused}')
     rsrc(L, 's', 'src')
     rsrc(L, 'g', 'g')
@@ -382,10 +402,12 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     gcoff = 'gcb' if buf else 'gc'
     if walls:
         L.append(f'  const unsigned msk = nbmask[{cell}];')
-        L.append(f'  if (msk >> {SELF_BIT}) {{')
+        L.append(f'  if ((msk >> {SELF_BIT}) & 1u) {{')
         for i in range(Q):
             L.append('    ' + store('o', 'out', i, f'oo_{centre}', load('g', 'g', i, gcoff)))
         L.append('    return;\n  }')
+        if mode == 'main':
+            L.append(f'  if ((msk >> {FIX_BIT}) & 1u) return;')
     for i in range(Q):
         L.append(f'  const {ct} g{i} = {load("g", "g", i, gcoff)};')
     force_loads(L)
@@ -394,8 +416,10 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     moments(L)
     if rho_links:
         L.append(f'  {ct} Rr = 0;')             # Σ_j βρ_j v_j over the cell's density-weighted links
-    if gen:
-        L.append(f'  {ct} ' + ', '.join(f'G{q} = 0' for q in range(Q)) + ';')   # Σ_j J_jq v_j (link programs)
+    gq = sorted({q for pg in (programs or ()) if pg is not None for row in pg if row is not None
+                 for q, _, _ in row[2]}) if fix else []
+    if gq:
+        L.append(f'  {ct} ' + ', '.join(f'G{q} = 0' for q in gq) + ';')      # Σ_j J_jq v_j (link programs)
     L.append(f'  {ct} S = 0, A = 0;')
     for a in range(D):
         L.append(f'  {ct} B{a} = 0;')
@@ -468,11 +492,19 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             if rho_links:
                 L.append(f'    if ((msk >> {j}) & 1u) Rr += lk_gr[id{j} * {Q} + {j}] * v;')
             cases = program_cases(j)
-            if cases:
+            if cases and fix:
+                # a program-linked component: Σ_j J_jq(c) v_j (c: the cell's own pre-streaming pdfs)
                 L.append(f'    if ((msk >> {j}) & 1u) switch (id{j}) {{')
                 for wid, pg in cases:
                     rows = ' '.join('{ ' + ' '.join(jl) + f' G{q} += ({je}) * v; }}' for q, jl, je in pg[2])
-                    L.append(f'      case {wid}: {{ {rows} }} break;')
+                    ld = own_loads(rows, lambda q: load('s', 'src', q, f'so_{centre}'))
+                    L.append(f'      case {wid}: {{ {ld} {rows} }} break;')
+                L.append('      default: break;\n    }')
+            elif cases:
+                # a program-linked component: its v for the second pass (the Jacobian row is evaluated there)
+                L.append(f'    if ((msk >> {j}) & 1u) switch (id{j}) {{')
+                L.append('      ' + ' '.join(f'case {wid}:' for wid, _ in cases) +
+                         f' rho_adj[(IDX){j} * {ncells} + {cell}] = v; break;')
                 L.append('      default: break;\n    }')
             L.append(f'    if ((msk >> {j}) & 1u) v *= lk_g[id{j} * {Q} + {j}];')
         if walls and any(dirs[j]):
@@ -485,12 +517,12 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                          f'= (T)v; }}')
         else:
             L.append('    ' + store('o', 'out', j, f'oo_{k}', 'v') + ' }')
-    ncells = '(IDX)Z * Y * X'
-    if gen:
-        L.append(f'  if (msk & {low}) {{ ' + ' '.join(f'rho_adj[(IDX){q} * {ncells} + {cell}] = G{q}'
-                                                     + (' + Rr;' if rho_links else ';') for q in range(Q)) + ' }')
-    elif rho_links:
-        L.append(f'  if (msk & {low}) rho_adj[{cell}] = Rr;')
+    inl = gen and mode == 'inline'
+    if rho_links:
+        # the density term: slot Q of the scratch array with inline link programs, its only slot without
+        L.append(f'  if (msk & {low}) rho_adj[' + (f'(IDX){Q} * {ncells} + ' if inl else '') + f'{cell}] = Rr;')
+    if gq:
+        L.append('  ' + ' '.join(f'Gs[(IDX)t * {len(gq)} + {n}] = G{q};' for n, q in enumerate(gq)))
     L.append('}')
     if two:
         # second adjoint pass: the density term of the cell's links reaches every component of the cell, whose
@@ -498,26 +530,65 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         L.append(f'{fn} void lbm_adj_rho_cell({sig_rho}, const int z, const int y, const int x)\n{{')
         L.append('  (void)Z;')
         L.append(f'  const unsigned msk = nbmask[{cell}];')
-        L.append(f'  if ((msk >> {SELF_BIT}) || !(msk & {low})) return;')
+        L.append(f'  if (((msk >> {SELF_BIT}) & 1u) || !(msk & {low})) return;')
         L.append('  const IDX oc = ' + ' + '.join(f'(IDX){a} * o_{a}' for a in axes) + ';')
-        if gen:
-            for q in range(Q):
-                L.append(f'  out[(IDX){q} * o_q + oc] += rho_adj[(IDX){q} * {ncells} + {cell}];')
-        else:
-            L.append(f'  const {ct} R = rho_adj[{cell}];')
+        if rho_links:
+            L.append(f'  const {ct} R = rho_adj[' + (f'(IDX){Q} * {ncells} + ' if inl else '') + f'{cell}];')
             for q in range(Q):
                 L.append(f'  out[(IDX){q} * o_q + oc] += R;')
+        if inl:
+            # Σ_j J_jk(c) v_j over the cell's program-linked components (c: the cell's own pre-streaming pdfs)
+            wrap_lines(L)
+            L.append('  const IDX sc = ' + ' + '.join(f'(IDX){a} * s_{a}' for a in axes) + ';')
+            for j in range(Q):
+                cases = program_cases(j)
+                if not cases:
+                    continue
+                L.append(f'  if ((msk >> {j}) & 1u) {{')
+                L.append(f'    const {ct} v = rho_adj[(IDX){j} * {ncells} + {cell}];')
+                L.append(f'    switch (wallid[{ncell(key(dirs[j]))}]) {{')
+                for wid, pg in cases:
+                    rows = ' '.join('{ ' + ' '.join(jl) + f' out[(IDX){q} * o_q + oc] += ({je}) * v; }}'
+                                    for q, jl, je in pg[2])
+                    ld = own_loads(rows, lambda q: f'({ct})src[(IDX){q} * s_q + sc]')
+                    L.append(f'      case {wid}: {{ {ld} {rows} }} break;')
+                L.append('      default: break;\n    }\n  }')
         L.append('}')
 
     # ---- entry points
     fa_f, fa_a, fs = (', force', ', force, dforce', 'f_c, f_z, f_y, f_x, ') if ff else ('', '', '')
     fa_a += ', rho_adj' if two else ''
-    args_r = 'out, nbmask, rho_adj, Z, Y, X, o_q, o_z, o_y, o_x'
+    args_r = 'out, nbmask, rho_adj, Z, Y, X, o_q, o_z, o_y, o_x' + \
+        (', src, wallid, s_q, s_z, s_y, s_x' if gen and mode == 'inline' else '')
     args_f = (f'src, dst, nbmask, wallid{fa_f}, Z, Y, X, s_q, s_z, s_y, s_x, d_q, d_z, d_y, d_x, {fs}s_bytes, d_bytes, '
               'omega')
     args_a = (f'src, g, out, nbmask, wallid{fa_a}, Z, Y, X, s_q, s_z, s_y, s_x, g_q, g_z, g_y, g_x, o_q, o_z, o_y, o_x, '
               f'{fs}s_bytes, g_bytes, o_bytes, omega')
-    if hip:
+    if hip and fix:
+        # the fix-up kernels: one thread per listed cell (the fluid cells next to a link-program wall)
+        gcols = len(gq)
+        sig_fix2 = (f'T* __restrict__ out, const {ct}* __restrict__ Gs, const int Z, const int Y, const int X, '
+                    'const IDX o_q, const IDX o_z, const IDX o_y, const IDX o_x')
+        for nm, sig, call in (('lbm_fwd_fix', sig_fwd, f'lbm_fwd_cell({args_f}, z, y, x);'),
+                              ('lbm_adj_fix', sig_adj + f', {ct}* __restrict__ Gs',
+                               f'lbm_adj_cell({args_a}, z, y, x, Gs, t);'),
+                              ('lbm_adj_fix2', sig_fix2, None)):
+            L.append(f'extern "C" __global__ void __launch_bounds__(256) {nm}({sig}, const int* __restrict__ cells, '
+                     'const int ncell)\n{')
+            L.append('  const int t = (int)(blockIdx.x * 256u + threadIdx.x);')
+            L.append('  if (t >= ncell) return;')
+            L.append('  const unsigned cell = (unsigned)cells[t];')
+            L.append('  const unsigned r = cell / (unsigned)X;')
+            L.append('  const int x = (int)(cell - r * (unsigned)X);')
+            L.append('  const int z = (int)(r / (unsigned)Y), y = (int)(r - (unsigned)z * Y);')
+            if call is not None:
+                L.append(f'  {call}\n}}')
+            else:
+                L.append('  const IDX oc = ' + ' + '.join(f'(IDX){a} * o_{a}' for a in axes) + ';')
+                for n, q in enumerate(gq):
+                    L.append(f'  out[(IDX){q} * o_q + oc] += Gs[(IDX)t * {gcols} + {n}];')
+                L.append('}')
+    elif hip:
         # a block = 256 consecutive cells of the lattice in C order (rows of x), and consecutive blocks on one XCD
         # (bijective remap of the round-robin dispatch): a lattice row's x-shifted loads and the adjoint's
         # x-shifted stores cover cache lines that the neighbouring wave also touches — in one block, or in a
@@ -575,10 +646,28 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     return '\n'.join(L) + '\n'
 
 
-def neighbour_mask(flags, stencil, xp):
+def fix_cells(flags, stencil, program_ids):
+    """Bool over the domain: fluid cells with a neighbour ``x − c_i`` (periodic) among the walls of ``program_ids``
+    (the flag ids whose boundary is a link program) — the cells the HIP fix-up kernels recompute."""
+    f = np.asarray(flags)
+    prog = np.isin(f, np.asarray(sorted(program_ids), dtype=f.dtype))
+    near = np.zeros(f.shape, bool)
+    for c in stencil.directions:
+        if any(c):
+            near |= np.roll(prog, tuple(int(v) for v in c), axis=tuple(range(len(c))))
+    return near & (f == 0)
+
+
+def neighbour_mask(flags, stencil, xp, fix=None):
     """``uint32`` per cell: bit i set where ``x − c_i`` is a wall cell (periodic), bit ``SELF_BIT`` where ``x`` is
-    one (``flags``: wall ids over the domain, 0 = fluid, numpy or torch)."""
+    one (``flags``: wall ids over the domain, 0 = fluid, numpy or torch); bit ``FIX_BIT`` where ``fix`` (a numpy
+    bool array, ``fix_cells``) is set — then computed on the host, and a torch result comes back as the uint32
+    bits in an int32 tensor on ``flags``' device."""
     is_torch = xp.__name__ == 'torch'
+    if fix is not None:
+        m = neighbour_mask(flags.cpu().numpy() if is_torch else flags, stencil, np)
+        m = m | (np.asarray(fix, bool).astype(np.uint32) << np.uint32(FIX_BIT))
+        return xp.from_numpy(np.ascontiguousarray(m).view(np.int32)).to(flags.device) if is_torch else m
     f = (flags != 0).to(xp.int32) if is_torch else (np.asarray(flags) != 0).astype(np.int64)
     m = f * 0
     for i, c in enumerate(stencil.directions):
@@ -634,21 +723,30 @@ class LatticeKernels:
         self.links = links if walls else None
         # density-weighted links: the adjoint takes a second pass (lbm_adj_rho) over a per-cell scratch array
         self.rho_links = self.links is not None and any(len(t) > 3 and t[3] != 0 for lk in self.links for t in lk)
-        # link programs (boundaries.link_program): a Q-component scratch array per cell, the same second pass
+        # link programs (boundaries.link_program). C: inline, a Q-component scratch array per cell and the second
+        # pass; HIP: the main kernels skip the FIX_BIT cells, the fix-up kernels (a module of their own) redo them
         self.programs = programs if self.links is not None and programs is not None and \
             any(p is not None for p in programs) else None
-        self.link_pass = self.rho_links or self.programs is not None
+        self.link_pass = self.rho_links or (self.programs is not None and target != 'gpu')
+        self.program_ids = tuple(k for k, p in enumerate(self.programs or ()) if p is not None)
+        self._gs = {}
         self._rho_bufs = {}
         self.target = target
         self._fns = {}
         self._plans = {}
 
-    def source(self, idx='int', addr='buf'):
+    def source(self, idx='int', addr='buf', fix=False):
+        """The C source (inline link programs), or a HIP module: the main kernels, or (``fix``) the fix-up kernels
+        of the cells next to link-program walls."""
         if self.target != 'gpu':
             return _emit(self.stencil, self.compressible, self.ct, self.walls, 'c', 'i64', 'ptr', self.links,
                          self.force_model, self.force, self.force_field, self.trt, self.programs)
+        if fix:
+            return _emit(self.stencil, self.compressible, self.ct, self.walls, 'hip', idx, addr, self.links,
+                         self.force_model, self.force, self.force_field, self.trt, self.programs, mode='fix')
         return _emit(self.stencil, self.compressible, self.ct, self.walls, 'hip', idx, addr, self.links,
-                     self.force_model, self.force, self.force_field, self.trt, self.programs)
+                     self.force_model, self.force, self.force_field, self.trt, None,
+                     mode='main' if self.programs is not None else 'inline')
 
     # -- GPU ---------------------------------------------------------------------------------------
     def _gpu_fn(self, which, idx, addr, device):
@@ -656,14 +754,15 @@ class LatticeKernels:
         fn = self._fns.get(key)
         if fn is None:
             from ..backends import hip_runtime as rt
-            code = rt.compile_hip(self.source(idx, addr), name='psad_lbm.hip')
+            code = rt.compile_hip(self.source(idx, addr, fix=which.endswith(('fix', 'fix2'))), name='psad_lbm.hip')
             fn = self._fns[key] = rt.load_function(code, f'lbm_{which}', device)
         return fn
 
     def build(self):
         from ..backends import hip_runtime as rt
         if self.target == 'gpu':
-            return [rt.compile_hip(self.source('int', a), name='psad_lbm.hip') for a in ('buf', 'ptr')]
+            return [rt.compile_hip(self.source('int', a, f), name='psad_lbm.hip') for a in ('buf', 'ptr')
+                    for f in ((False, True) if self.programs is not None else (False,))]
         return self._cpu_fn('fwd')
 
     def _check(self, tensors, mask, ids=None):
@@ -729,14 +828,17 @@ class LatticeKernels:
                 tuple(force.stride() if xp_tensor else force.strides):
             raise ValueError('the force adjoint must have the strides of the force')
 
-    def plan(self, which, tensors, mask, omega, ids=None, force=None, dforce=None):
+    def plan(self, which, tensors, mask, omega, ids=None, force=None, dforce=None, fix=None):
         """The launch of ``which`` ('fwd' / 'adj') on tensors of these shapes, strides, dtype and device (with or
         without walls): a ``LaunchPlan`` whose pointer slots and relaxation rate are patched per launch — the
         time-step op launches T of them per apply. ω is not part of the key (a trained or scheduled rate reuses the
-        plan); the plan is built with the first ω it sees."""
+        plan); the plan is built with the first ω it sees. ``fix``: (cells, scratch) — the fix-up kernel of
+        ``which`` over the listed cells (int32 cell indices; the adjoint's per-listed-cell G scratch)."""
         key = (which, mask is not None) + tuple((tuple(t.shape), tuple(t.stride()), t.dtype, t.device)
                                                 for t in tensors) + \
-            ((tuple(force.shape), tuple(force.stride())) if force is not None else ())
+            ((tuple(force.shape), tuple(force.stride())) if force is not None else ()) + \
+            ((fix[0].data_ptr(), int(fix[0].numel()), fix[1].data_ptr() if fix[1] is not None else 0)
+             if fix is not None else ())
         plan = self._plans.get(key)
         if plan is not None:
             return plan
@@ -748,10 +850,10 @@ class LatticeKernels:
                 idx = 'long long'
             strides += list(lattice_strides(force, self.stencil.D))
         dev = tensors[0].device.index
-        fn = self._gpu_fn(which, idx, addr, dev)
+        fn = self._gpu_fn(which + ('_fix' if fix is not None else ''), idx, addr, dev)
         Z, Y, X = self._extent(tensors[0])
         code = 'i' if idx == 'int' else 'q'
-        nblocks = self._blocks(X, Y, Z)
+        nblocks = self._blocks(X, Y, Z) if fix is None else -(-int(fix[0].numel()) // 256)
         reach = [self._reach(t) * t.element_size() for t in tensors]
         ptrs = [t.data_ptr() for t in tensors] + [mask.data_ptr() if mask is not None else 0,
                                                   ids.data_ptr() if ids is not None else 0]
@@ -761,9 +863,63 @@ class LatticeKernels:
             ptrs += [0]                                  # the second pass's scratch array (patched per launch)
         fmt = 'Q' * len(ptrs) + 'iii' + code * len(strides) + 'q' * len(tensors) + \
             ('d' if self.ct == 'double' else 'f')
-        args = _pack(fmt, *ptrs, Z, Y, X, *strides, *reach, float(omega))
-        plan = self._plans[key] = LaunchPlan(fn, nblocks, args, len(ptrs), dev, _offset(fmt, len(fmt) - 1), fmt[-1])
+        vals = [*ptrs, Z, Y, X, *strides, *reach, float(omega)]
+        om_i = len(fmt) - 1
+        if fix is not None:
+            # the fix-up kernel: (+ the G scratch,) the cell list and its length after the main kernel's arguments
+            extra = ([fix[1].data_ptr()] if which == 'adj' else []) + [fix[0].data_ptr(), int(fix[0].numel())]
+            fmt += 'Q' * (len(extra) - 1) + 'i'
+            vals += extra
+        args = _pack(fmt, *vals)
+        plan = self._plans[key] = LaunchPlan(fn, nblocks, args, len(ptrs), dev, _offset(fmt, om_i), fmt[om_i])
         return plan
+
+    def fix2_plan(self, out, cells, gs):
+        """The last fix-up launch of the adjoint (``lbm_adj_fix2``: out_k(x) += G_k at the listed cells)."""
+        key = ('fix2', tuple(out.shape), tuple(out.stride()), out.dtype, out.device, cells.data_ptr(),
+               int(cells.numel()), gs.data_ptr())
+        plan = self._plans.get(key)
+        if plan is not None:
+            return plan
+        idx, addr = self._mode([out])
+        dev = out.device.index
+        fn = self._gpu_fn('adj_fix2', idx, addr, dev)
+        Z, Y, X = self._extent(out)
+        code = 'i' if idx == 'int' else 'q'
+        fmt = 'QQ' + 'iii' + code * 4 + 'Qi'
+        args = _pack(fmt, out.data_ptr(), gs.data_ptr(), Z, Y, X, *lattice_strides(out, self.stencil.D),
+                     cells.data_ptr(), int(cells.numel()))
+        plan = self._plans[key] = LaunchPlan(fn, -(-int(cells.numel()) // 256), args, 1, dev, None, None)
+        return plan
+
+    def gs_buffer(self, cells, t):
+        """The fix-up adjoint's scratch: the G columns per listed cell (one per domain list and device, reused)."""
+        import torch
+        ncol = len({q for k in self.program_ids for row in self.programs[k] if row is not None for q, _, _ in row[2]})
+        key = (cells.data_ptr(), int(cells.numel()), t.device, t.dtype)
+        b = self._gs.get(key)
+        if b is None:
+            b = self._gs[key] = torch.empty((max(1, int(cells.numel())), ncol), dtype=t.dtype, device=t.device)
+        return b
+
+    def fix_launch(self, which, tensors, mask, omega, ids, force, dforce, cells, stream):
+        """The fix-up launches after a main ``which`` launch on ``tensors`` (HIP with link programs; nothing when
+        no cell is listed). The adjoint's ``fix2`` runs later: ``fix2_launch`` (after the density pass)."""
+        if self.programs is None or self.target != 'gpu' or cells is None or int(cells.numel()) == 0:
+            return None
+        gs = self.gs_buffer(cells, tensors[0]) if which == 'adj' else None
+        plan = self.plan(which, tensors, mask, omega, ids, force, dforce, fix=(cells, gs))
+        ptrs = tuple(t.data_ptr() for t in tensors) + (mask.data_ptr(), ids.data_ptr())
+        if force is not None:
+            ptrs += (force.data_ptr(),) + ((dforce.data_ptr(),) if which == 'adj' else ())
+        if which == 'adj' and self.link_pass:
+            ptrs += (self.rho_buffer(tensors[0]).data_ptr(),)
+        plan(ptrs, stream, omega)
+        return gs
+
+    def fix2_launch(self, out, cells, gs, stream):
+        if gs is not None:
+            self.fix2_plan(out, cells, gs)((out.data_ptr(),), stream)
 
     def rho_buffer(self, t):
         """The per-cell scratch array of the second adjoint pass (one per domain and device, reused: stream-ordered):
@@ -772,39 +928,57 @@ class LatticeKernels:
         key = (tuple(int(n) for n in t.shape[:self.stencil.D]), t.device, t.dtype)
         b = self._rho_bufs.get(key)
         if b is None:
-            shape = ((self.stencil.Q,) if self.programs is not None else ()) + key[0]
+            # (HIP: link programs run in the fix-up kernels, so the density pass alone uses it — one slot)
+            shape = ((self.stencil.Q + int(self.rho_links),) if self.programs is not None and self.target != 'gpu'
+                     else ()) + key[0]
             b = self._rho_bufs[key] = torch.empty(shape, dtype=t.dtype, device=t.device)
         return b
 
-    def rho_plan(self, out, mask, rho):
-        """The density pass of the adjoint (``lbm_adj_rho``: every component of a cell next to a density-weighted
-        wall gets the cell's Σ_j βρ_j v_j added) on ``out``'s shape and strides."""
-        key = ('rho', tuple(out.shape), tuple(out.stride()), out.dtype, out.device)
+    def rho_plan(self, out, mask, rho, src=None, ids=None):
+        """The second pass of the adjoint (``lbm_adj_rho``: every component of a cell next to a density-weighted
+        wall gets the cell's Σ_j βρ_j v_j added; with link programs, component k of a cell next to a program wall
+        gets Σ_j J_jk v_j, the Jacobians evaluated at the cell's own pdfs in ``src``) on ``out``'s shape and strides.
+        The plan's pointer slots: out, mask, scratch (+ src, ids with link programs)."""
+        key = ('rho', tuple(out.shape), tuple(out.stride()), out.dtype, out.device) + \
+            ((tuple(src.stride()),) if self.programs is not None else ())
         plan = self._plans.get(key)
         if plan is not None:
             return plan
-        idx, addr = self._mode([out])
+        tensors = [out] + ([src] if self.programs is not None else [])
+        idx, addr = self._mode(tensors)
         dev = out.device.index
         fn = self._gpu_fn('adj_rho', idx, addr, dev)
         Z, Y, X = self._extent(out)
         code = 'i' if idx == 'int' else 'q'
-        fmt = 'QQQ' + 'iii' + code * 4
-        args = _pack(fmt, out.data_ptr(), mask.data_ptr(), rho.data_ptr(), Z, Y, X,
-                     *lattice_strides(out, self.stencil.D))
-        plan = self._plans[key] = LaunchPlan(fn, self._blocks(X, Y, Z), args, 3, dev, None, None)
+        if self.programs is None:
+            fmt = 'QQQ' + 'iii' + code * 4
+            args = _pack(fmt, out.data_ptr(), mask.data_ptr(), rho.data_ptr(), Z, Y, X,
+                         *lattice_strides(out, self.stencil.D))
+            nptr = 3
+        else:
+            fmt = 'QQQ' + 'iii' + code * 4 + 'QQ' + code * 4
+            args = _pack(fmt, out.data_ptr(), mask.data_ptr(), rho.data_ptr(), Z, Y, X,
+                         *lattice_strides(out, self.stencil.D), src.data_ptr(), ids.data_ptr(),
+                         *lattice_strides(src, self.stencil.D))
+            nptr = 3
+        plan = self._plans[key] = LaunchPlan(fn, self._blocks(X, Y, Z), args, nptr, dev, None, None)
+        if self.programs is not None:
+            plan.extra = _offset(fmt, 3 + 3 + 4)          # the src / ids slots, patched per launch
         return plan
 
-    def forward(self, src, dst, omega, mask=None, stream=None, ids=None, force=None):
+    def forward(self, src, dst, omega, mask=None, stream=None, ids=None, force=None, cells=None):
         """``dst = stream-pull-collide(src)`` (torch tensors ``[*domain, q]``, any strides; ``force``: the per-cell
         force ``[*domain, D]`` of force-field kernels)."""
         if self.target != 'gpu':
             return self._cpu('fwd', [src, dst], omega, mask, ids, force)
+        st = _stream(stream, src)
         self.plan('fwd', [src, dst], mask, omega, ids, force)(
             (src.data_ptr(), dst.data_ptr(), mask.data_ptr() if mask is not None else 0,
              ids.data_ptr() if ids is not None else 0) + ((force.data_ptr(),) if force is not None else ()),
-            _stream(stream, src), omega)
+            st, omega)
+        self.fix_launch('fwd', [src, dst], mask, omega, ids, force, None, cells, st)
 
-    def adjoint(self, src, g, out, omega, mask=None, stream=None, ids=None, force=None, dforce=None):
+    def adjoint(self, src, g, out, omega, mask=None, stream=None, ids=None, force=None, dforce=None, cells=None):
         """``out = (∂ step / ∂ src)ᵀ g`` at the state ``src``; force-field kernels also ADD ``(∂ step / ∂ F)ᵀ g`` to
         ``dforce``."""
         if self.target != 'gpu':
@@ -816,8 +990,16 @@ class LatticeKernels:
              ids.data_ptr() if ids is not None else 0) +
             ((force.data_ptr(), dforce.data_ptr()) if force is not None else ()) +
             ((rho.data_ptr(),) if rho is not None else ()), st, omega)
+        gs = self.fix_launch('adj', [src, g, out], mask, omega, ids, force, dforce, cells, st)
         if rho is not None:
-            self.rho_plan(out, mask, rho)((out.data_ptr(), mask.data_ptr(), rho.data_ptr()), st)
+            self.rho_pass(out, mask, rho, src, ids, st)
+        self.fix2_launch(out, cells, gs, st)
+
+    def rho_pass(self, out, mask, rho, src, ids, stream):
+        """Launch the adjoint's second pass (``rho_plan``) for this launch's ``out`` / ``src``."""
+        plan = self.rho_plan(out, mask, rho, src, ids)
+        plan((out.data_ptr(), mask.data_ptr(), rho.data_ptr()), stream,
+             extra=(src.data_ptr(), ids.data_ptr()) if self.programs is not None else None)
 
     def _extent(self, t):
         shape = [int(n) for n in t.shape[:self.stencil.D]]
@@ -875,7 +1057,8 @@ class LatticeKernels:
         rho = None
         if which == 'adj' and self.link_pass:
             # the second pass's scratch (both passes in one call)
-            rho = np.empty(((self.stencil.Q,) if self.programs is not None else ()) + shape[:D], self.dtype)
+            rho = np.empty(((self.stencil.Q + int(self.rho_links),) if self.programs is not None else ()) + shape[:D],
+                           self.dtype)
             ptrs += [rho.ctypes.data]
         ext = list(shape[:D]) if D == 3 else [1] + list(shape[:D])
         P = (ctypes.c_void_p * len(ptrs))(*ptrs)
@@ -890,16 +1073,19 @@ class LaunchPlan:
     """One lattice kernel launch with its argument buffer; ``plan(ptrs, stream, omega)`` patches the leading pointer
     slots (the pdf arrays, then the neighbour mask) and the relaxation rate, and launches on the plan's device
     (made current for the launch when it is not: the function handle belongs to that device's module)."""
-    __slots__ = ('fn', 'nblocks', 'template', 'fmt', 'device', 'om_off', 'om_fmt')
+    __slots__ = ('fn', 'nblocks', 'template', 'fmt', 'device', 'om_off', 'om_fmt', 'extra')
 
     def __init__(self, fn, nblocks, template, nptr, device, om_off, om_code):
         self.fn, self.nblocks, self.template, self.fmt = fn, nblocks, template, f'<{nptr}Q'
         self.device, self.om_off, self.om_fmt = device, om_off, None if om_code is None else '<' + om_code
+        self.extra = None              # byte offset of two more pointer slots patched per launch (second pass)
 
-    def __call__(self, ptrs, stream, omega=None):
+    def __call__(self, ptrs, stream, omega=None, extra=None):
         from ..backends import hip_runtime as rt
         buf = bytearray(self.template)
         struct.pack_into(self.fmt, buf, 0, *ptrs)
+        if extra is not None:
+            struct.pack_into('<2Q', buf, self.extra, *extra)
         if omega is not None and self.om_off is not None:
             struct.pack_into(self.om_fmt, buf, self.om_off, float(omega))
         import torch

@@ -248,6 +248,10 @@ def run_lbm(name, stencil, shape, dtype, T=10, reps=5, compressible=False, walls
         # a channel: no-slip walls on the first and last rows of axis 1
         step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[:, 0])
         step.set_boundary_including_adjoint(lbm.NoSlip(), lbm.make_slice[:, -1])
+    if walls == 'pressure':
+        # ... driven by FixedDensity inlet / outlet planes at the ends of axis 0 (link programs)
+        step.set_boundary_including_adjoint(lbm.FixedDensity(1.01, name='inlet'), lbm.make_slice[0, 1:-1])
+        step.set_boundary_including_adjoint(lbm.FixedDensity(0.99, name='outlet'), lbm.make_slice[-1, 1:-1])
     Op = step.create_timestep_op(T)
     q = rule.stencil.Q
     g = torch.Generator(device='cuda').manual_seed(0)
@@ -293,7 +297,8 @@ def run_lbm(name, stencil, shape, dtype, T=10, reps=5, compressible=False, walls
     es = torch.tensor([], dtype=dtype).element_size()
     f_ms, b_ms = sorted(fw)[len(fw) // 2], sorted(bw)[len(bw) // 2]
     res = {'config': name, 'shape': list(shape), 'dtype': str(dtype).replace('torch.', ''), 'time_steps': T,
-           'schedule': 'lattice' if step._lattice is not None else 'autodiffop', 'walls': bool(walls),
+           'schedule': 'lattice' if step._lattice is not None else 'autodiffop',
+           'walls': walls if isinstance(walls, str) else bool(walls),
            'fwd_mlups': round(cells * T / (f_ms * 1e-3) / 1e6, 1), 'bwd_mlups': round(cells * T / (b_ms * 1e-3) / 1e6, 1),
            'fwd_ms': round(f_ms, 4), 'bwd_ms': round(b_ms, 4),
            'fwd_GBps': round((2 * q + (D if force_field else 0)) * es * cells * T / (f_ms * 1e-3) / 1e9, 1),
@@ -379,7 +384,9 @@ def main():
     lbms = [('lbm_d2q9_f32_2048^2', 'D2Q9', (2048, 2048), torch.float32, False),
             ('lbm_d3q19_f32_192^3', 'D3Q19', (192, 192, 192), torch.float32, False),
             ('lbm_d2q9_f32_2048^2_channel', 'D2Q9', (2048, 2048), torch.float32, True),
-            ('lbm_d3q19_f32_192^3_channel', 'D3Q19', (192, 192, 192), torch.float32, True)]
+            ('lbm_d3q19_f32_192^3_channel', 'D3Q19', (192, 192, 192), torch.float32, True),
+            ('lbm_d2q9_f32_2048^2_pressure', 'D2Q9', (2048, 2048), torch.float32, 'pressure'),
+            ('lbm_d3q19_f32_192^3_pressure', 'D3Q19', (192, 192, 192), torch.float32, 'pressure')]
     for name, stencil, shape, dt, walls in lbms:
         if only and name not in only:
             continue
