@@ -79,11 +79,11 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     program-linked component j to a per-cell scratch array and the second pass (``lbm_adj_rho``) adds
     ``Σ_j J_jk(c) v_j`` to component k of the cell — the Jacobians are evaluated there, on the cells next to a wall,
     not in the first pass, whose registers they would take on every cell (``mode='inline'``, the C target).
-    HIP (``mode='main'`` / ``'fix'``): the main kernels carry no program code and skip the cells marked ``FIX_BIT``
-    (fluid cells next to a program wall); list-driven fix-up kernels recompute exactly those cells with the
-    programs — forward (``lbm_fwd_fix``), adjoint with the regular scatter plus ``G_k = Σ_j J_jk v_j`` into a
-    per-listed-cell scratch (``lbm_adj_fix``), then ``out_k(x) += G_k`` (``lbm_adj_fix2``, after every other store of
-    the step) — so the lattice's bulk runs the plain wall kernels."""
+    HIP (``mode='main'`` / ``'fix'``): the forward evaluates the programs inline as above; the main adjoint carries
+    no program code and skips the cells marked ``FIX_BIT`` (fluid cells next to a program wall), and list-driven
+    fix-up kernels redo exactly those cells — the regular scatter plus ``G_k = Σ_j J_jk v_j`` into a per-listed-cell
+    scratch (``lbm_adj_fix``), then ``out_k(x) += G_k`` (``lbm_adj_fix2``, after every other store of the step) — so
+    the lattice's bulk runs the plain adjoint (measured: profiles/r05_lbm_pressure.jsonl)."""
     D, Q = stencil.D, stencil.Q
     dirs = [tuple(d) for d in stencil.directions]
     w = [float(x) for x in stencil.weights]
@@ -236,7 +236,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         used = sorted({int(m) for m in re.findall(r'\bc(\d+)\b', code)})
         return ' '.join(f'const {ct} c{q} = {rd(q)};' for q in used)
 
-    def pull_loads(L, prefix, arr):
+    def pull_loads(L, prefix, arr, progs=True):
         for i in range(Q):
             k = key(dirs[i])
             cq = '' if links is not None and walls and any(dirs[i]) else 'const '
@@ -256,7 +256,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                     L.append(f'  unsigned id{i} = 0;')
                     L.append(f'  if ((msk >> {i}) & 1u) {{ id{i} = wallid[{ncell(k)}]; '
                              f'f{i} = lk_a[id{i} * {Q} + {i}] * f{i} + lk_b[id{i} * {Q} + {i}]{rterm}; }}')
-                    cases = program_cases(i)
+                    cases = program_cases(i) if progs else []
                     if cases:
                         L.append(f'  if ((msk >> {i}) & 1u) switch (id{i}) {{')
                         for wid, pg in cases:
@@ -353,8 +353,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         for i in range(Q):
             L.append('    ' + store('d', 'dst', i, dcoff, load('s', 'src', i, f'so_{centre}')))
         L.append('    return;\n  }')
-        if mode == 'main':
-            L.append(f'  if ((msk >> {FIX_BIT}) & 1u) return;      // next to a link-program wall: the fix-up kernel')
+
     force_loads(L)
     cell_density(L, 's', 'src')
     pull_loads(L, 's', 'src')
@@ -412,7 +411,8 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         L.append(f'  const {ct} g{i} = {load("g", "g", i, gcoff)};')
     force_loads(L)
     cell_density(L, 's', 'src')
-    pull_loads(L, 's', 'src')
+    adj_progs = gen and mode != 'main'          # the main HIP adjoint leaves the program cells to the fix-up kernels
+    pull_loads(L, 's', 'src', adj_progs)
     moments(L)
     if rho_links:
         L.append(f'  {ct} Rr = 0;')             # Σ_j βρ_j v_j over the cell's density-weighted links
@@ -491,7 +491,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         if walls and any(dirs[j]) and links is not None:
             if rho_links:
                 L.append(f'    if ((msk >> {j}) & 1u) Rr += lk_gr[id{j} * {Q} + {j}] * v;')
-            cases = program_cases(j)
+            cases = program_cases(j) if adj_progs else []
             if cases and fix:
                 # a program-linked component: Σ_j J_jq(c) v_j (c: the cell's own pre-streaming pdfs)
                 L.append(f'    if ((msk >> {j}) & 1u) switch (id{j}) {{')
@@ -569,8 +569,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         gcols = len(gq)
         sig_fix2 = (f'T* __restrict__ out, const {ct}* __restrict__ Gs, const int Z, const int Y, const int X, '
                     'const IDX o_q, const IDX o_z, const IDX o_y, const IDX o_x')
-        for nm, sig, call in (('lbm_fwd_fix', sig_fwd, f'lbm_fwd_cell({args_f}, z, y, x);'),
-                              ('lbm_adj_fix', sig_adj + f', {ct}* __restrict__ Gs',
+        for nm, sig, call in (('lbm_adj_fix', sig_adj + f', {ct}* __restrict__ Gs',
                                f'lbm_adj_cell({args_a}, z, y, x, Gs, t);'),
                               ('lbm_adj_fix2', sig_fix2, None)):
             L.append(f'extern "C" __global__ void __launch_bounds__(256) {nm}({sig}, const int* __restrict__ cells, '
@@ -745,7 +744,7 @@ class LatticeKernels:
             return _emit(self.stencil, self.compressible, self.ct, self.walls, 'hip', idx, addr, self.links,
                          self.force_model, self.force, self.force_field, self.trt, self.programs, mode='fix')
         return _emit(self.stencil, self.compressible, self.ct, self.walls, 'hip', idx, addr, self.links,
-                     self.force_model, self.force, self.force_field, self.trt, None,
+                     self.force_model, self.force, self.force_field, self.trt, self.programs,
                      mode='main' if self.programs is not None else 'inline')
 
     # -- GPU ---------------------------------------------------------------------------------------
@@ -903,9 +902,11 @@ class LatticeKernels:
         return b
 
     def fix_launch(self, which, tensors, mask, omega, ids, force, dforce, cells, stream):
-        """The fix-up launches after a main ``which`` launch on ``tensors`` (HIP with link programs; nothing when
-        no cell is listed). The adjoint's ``fix2`` runs later: ``fix2_launch`` (after the density pass)."""
-        if self.programs is None or self.target != 'gpu' or cells is None or int(cells.numel()) == 0:
+        """The fix-up launch after a main adjoint launch on ``tensors`` (HIP with link programs; nothing for the
+        forward, which runs them inline, or when no cell is listed). ``fix2`` runs later: ``fix2_launch`` (after the
+        density pass)."""
+        if which != 'adj' or self.programs is None or self.target != 'gpu' or cells is None or \
+                int(cells.numel()) == 0:
             return None
         gs = self.gs_buffer(cells, tensors[0]) if which == 'adj' else None
         plan = self.plan(which, tensors, mask, omega, ids, force, dforce, fix=(cells, gs))
@@ -976,7 +977,6 @@ class LatticeKernels:
             (src.data_ptr(), dst.data_ptr(), mask.data_ptr() if mask is not None else 0,
              ids.data_ptr() if ids is not None else 0) + ((force.data_ptr(),) if force is not None else ()),
             st, omega)
-        self.fix_launch('fwd', [src, dst], mask, omega, ids, force, None, cells, st)
 
     def adjoint(self, src, g, out, omega, mask=None, stream=None, ids=None, force=None, dforce=None, cells=None):
         """``out = (∂ step / ∂ src)ᵀ g`` at the state ``src``; force-field kernels also ADD ``(∂ step / ∂ F)ᵀ g`` to
