@@ -49,10 +49,47 @@ def trt_odd_rate(omega, magic=3.0 / 16.0):
     return 1.0 / (magic / (1.0 / omega - 0.5) + 0.5)
 
 
-def collide(f, omega, stencil, compressible, xp, force_model=None, force=None, omega_odd=None):
+# MRT moments (lbmpy's weighted-orthogonal MRT groups, restated): monomials c_x^a c_y^b (c_z^c) with integer
+# coefficients, Gram–Schmidt-orthogonalised under the lattice weights in this order
+MRT_BASIS = {
+    2: [('cons', {(0, 0): 1}), ('cons', {(1, 0): 1}), ('cons', {(0, 1): 1}), ('bulk', {(2, 0): 1, (0, 2): 1}),
+        ('shear', {(2, 0): 1, (0, 2): -1}), ('shear', {(1, 1): 1}), ('third', {(2, 1): 1}), ('third', {(1, 2): 1}),
+        ('fourth', {(2, 2): 1})],
+    3: [('cons', {(0, 0, 0): 1}), ('cons', {(1, 0, 0): 1}), ('cons', {(0, 1, 0): 1}), ('cons', {(0, 0, 1): 1}),
+        ('bulk', {(2, 0, 0): 1, (0, 2, 0): 1, (0, 0, 2): 1}),
+        ('shear', {(2, 0, 0): 2, (0, 2, 0): -1, (0, 0, 2): -1}), ('shear', {(0, 2, 0): 1, (0, 0, 2): -1}),
+        ('shear', {(1, 1, 0): 1}), ('shear', {(1, 0, 1): 1}), ('shear', {(0, 1, 1): 1}),
+        ('third', {(2, 1, 0): 1}), ('third', {(2, 0, 1): 1}), ('third', {(1, 2, 0): 1}), ('third', {(0, 2, 1): 1}),
+        ('third', {(1, 0, 2): 1}), ('third', {(0, 1, 2): 1}),
+        ('fourth', {(2, 2, 0): 1}), ('fourth', {(2, 0, 2): 1}), ('fourth', {(0, 2, 2): 1})],
+}
+
+
+def mrt_matrix(stencil, rates):
+    """The MRT collision matrix ``M⁻¹ S M`` (numpy float64, Q×Q) for group rates ``rates`` = {'shear', 'bulk',
+    'third', 'fourth'} (the conserved moments relax with 0): ``dst = f − (M⁻¹ S M)(f − feq)``."""
+    import numpy as np
+    dirs, w = SETS[stencil]
+    D = len(dirs[0])
+    W = np.array([float(x) for x in w])
+    rows, groups = [], []
+    for grp, poly in MRT_BASIS[D]:
+        v = np.array([sum(cf * np.prod([c[a] ** e[a] for a in range(D)]) for e, cf in poly.items()) for c in dirs],
+                     dtype=np.float64)
+        for r in rows:
+            v = v - (W * v * r).sum() / (W * r * r).sum() * r
+        rows.append(v)
+        groups.append(grp)
+    M = np.array(rows)
+    S = np.diag([0.0 if g == 'cons' else float(rates[g]) for g in groups])
+    return np.linalg.inv(M) @ S @ M
+
+
+def collide(f, omega, stencil, compressible, xp, force_model=None, force=None, omega_odd=None, mrt=None):
     """SRT collision, or TRT with ``omega_odd`` (the antisymmetric part of each population pair (f_i − f_ī)/2
-    relaxes with ω₋, the symmetric part with ω); ``force_model`` 'simple' (+3 w_i c_i·F) or 'guo' (velocity shifted
-    by F/2, + w_i (1 − ω/2) (3 (c_i − u)·F + 9 (c_i·u)(c_i·F))) with a body force ``force`` (lbmpy's published force
+    relaxes with ω₋, the symmetric part with ω), or MRT with ``mrt`` (a Q×Q collision matrix, ``mrt_matrix``:
+    dst = f − A (f − feq)); ``force_model`` 'simple' (+3 w_i c_i·F) or 'guo' (velocity shifted by F/2,
+    + w_i (1 − ω/2) (3 (c_i − u)·F + 9 (c_i·u)(c_i·F))) with a body force ``force`` (lbmpy's published force
     models)."""
     dirs, w = SETS[stencil]
     D = len(dirs[0])
@@ -74,7 +111,9 @@ def collide(f, omega, stencil, compressible, xp, force_model=None, force=None, o
     for i, c in enumerate(dirs):
         cu = sum(ca * ua for ca, ua in zip(c, u) if ca)
         feq = feqs[i]
-        if omega_odd is None:
+        if mrt is not None:
+            g = f[..., i] - sum(float(mrt[i][k]) * (f[..., k] - feqs[k]) for k in range(len(dirs)) if mrt[i][k] != 0)
+        elif omega_odd is None:
             g = f[..., i] + omega * (feq - f[..., i])
         else:
             j = opp[i]
@@ -92,16 +131,18 @@ def collide(f, omega, stencil, compressible, xp, force_model=None, force=None, o
     return xp.stack(out, -1) if xp.__name__ != 'torch' else xp.stack(out, dim=-1)
 
 
-def step(f, omega, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None, omega_odd=None):
+def step(f, omega, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None, omega_odd=None,
+         mrt=None):
     """One stream-pull-collide time step on a periodic domain (``f``: ``[*spatial, q]``)."""
     if xp is None:
         import numpy as xp
-    return collide(stream(f, stencil, xp), omega, stencil, compressible, xp, force_model, force, omega_odd)
+    return collide(stream(f, stencil, xp), omega, stencil, compressible, xp, force_model, force, omega_odd, mrt)
 
 
-def run(f, omega, steps, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None, omega_odd=None):
+def run(f, omega, steps, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None, omega_odd=None,
+        mrt=None):
     for _ in range(steps):
-        f = step(f, omega, stencil, compressible, xp, force_model, force, omega_odd)
+        f = step(f, omega, stencil, compressible, xp, force_model, force, omega_odd, mrt)
     return f
 
 
@@ -147,20 +188,21 @@ def stream_walls(f, stencil, wall, xp):
 
 
 def step_walls(f, omega, wall, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None,
-               omega_odd=None):
+               omega_odd=None, mrt=None):
     """One stream-pull-collide step with no-slip obstacles (and optionally a body force on the fluid cells, as
     ``collide``); obstacle cells keep their state."""
     if xp is None:
         import numpy as xp
-    new = collide(stream_walls(f, stencil, wall, xp), omega, stencil, compressible, xp, force_model, force, omega_odd)
+    new = collide(stream_walls(f, stencil, wall, xp), omega, stencil, compressible, xp, force_model, force, omega_odd,
+                  mrt)
     keep = wall[..., None] if xp.__name__ != 'torch' else wall.unsqueeze(-1)
     return xp.where(keep, f, new)
 
 
 def run_walls(f, omega, wall, steps, stencil='D2Q9', compressible=False, xp=None, force_model=None, force=None,
-              omega_odd=None):
+              omega_odd=None, mrt=None):
     for _ in range(steps):
-        f = step_walls(f, omega, wall, stencil, compressible, xp, force_model, force, omega_odd)
+        f = step_walls(f, omega, wall, stencil, compressible, xp, force_model, force, omega_odd, mrt)
     return f
 
 

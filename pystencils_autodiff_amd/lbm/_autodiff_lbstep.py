@@ -232,6 +232,29 @@ class AutoDiffLatticeBoltzmannStep:
                 self._lattice_trt = ('rate', float(update_rule.relaxation_rate_odd))
             else:
                 trt_ok = False                      # a symbolic odd rate: the AutoDiffOp kernels
+        # MRT: the relaxation matrix A = ω P_ω + C (groups relaxing with the rule's ω / with constant rates)
+        self._lattice_mrt = None
+        if getattr(update_rule, 'method', 'srt') == 'mrt':
+            from ._method import MRT_GROUPS, mrt_relaxation_matrices
+            P = mrt_relaxation_matrices(update_rule.stencil)
+            Qn = update_rule.stencil.Q
+            Pw = [[0.0] * Qn for _ in range(Qn)]
+            Cm = [[0.0] * Qn for _ in range(Qn)]
+            om = sp.sympify(update_rule.relaxation_rate)
+            for grp in MRT_GROUPS:
+                r = sp.sympify(update_rule.mrt_rates[grp])
+                if r == om:
+                    tgt, scale = Pw, 1.0
+                elif r.is_number:
+                    tgt, scale = Cm, float(r)
+                else:
+                    trt_ok = False                  # a symbolic rate other than ω: the AutoDiffOp kernels
+                    break
+                for i in range(Qn):
+                    for k in range(Qn):
+                        tgt[i][k] += scale * float(P[grp][i][k])
+            else:
+                self._lattice_mrt = (Pw, Cm)
         self._lattice = {} if (getattr(update_rule, 'stencil', None) is not None and not time_constant_fields
                                and self._lattice_force is not None
                                and os.environ.get('PSAD_LBM_LATTICE', '1') != '0'
@@ -457,7 +480,7 @@ class AutoDiffLatticeBoltzmannStep:
             k = self._lattice[(walls, links, programs)] = LatticeKernels(
                 self.method, getattr(self._update_rule, 'compressible', False), self.pdf_field.dtype.numpy_dtype,
                 walls, self._target, links, *self._lattice_force, force_field=self._force_field is not None,
-                trt=self._lattice_trt, programs=programs)
+                trt=self._lattice_trt, programs=programs, mrt=self._lattice_mrt)
         return k
 
     # -- kernels -----------------------------------------------------------------------------------

@@ -47,7 +47,7 @@ FIX_BIT = 31       # ... the cell is a fluid cell next to a wall with a link pro
 
 
 def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=None, force_model=None, force=None,
-          force_field=False, trt=None, programs=None, mode='inline'):
+          force_field=False, trt=None, programs=None, mode='inline', mrt=None):
     """Source of the forward (``lbm_fwd``) and adjoint (``lbm_adj``) kernels.
 
     ``addr='buf'`` (HIP): every pdf array is one buffer resource (its bytes below 2³²); a component's plane
@@ -73,6 +73,10 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     magic number, computed per launch from the ω argument) or ``('rate', ω₋)`` (a constant). With a = (ω₊ + ω₋)/2,
     b = (ω₊ − ω₋)/2 the collision is ``dst_i = (1 − a) f_i − b f_ī + a feq_i + b feq_ī`` and the adjoint takes the
     equilibrium sums over h_i = a g_i + b g_ī: ``v_j = (1 − a) g_j − b g_ĵ + A_h + Σ_a B_h,a ∂u_a/∂f_j``.
+    ``mrt``: the MRT method's relaxation matrix ``A = ω P_ω + C`` (``(P_ω, C)``, Q×Q numbers, ``_method.
+    mrt_relaxation_matrices`` summed over the groups relaxing with the ω argument / with constant rates):
+    ``dst = f − A (f − feq)``; the adjoint takes the equilibrium sums over h = Aᵀ g: ``v_j = g_j − h_j + A_h + Σ_a B_h,a
+    ∂u_a/∂f_j``.
     ``programs``: per wall id None or the boundary's ``link_program`` (links of the cell's own pdfs the fused form does
     not take, ``boundaries.link_program``; their table rows are zeros): the forward evaluates the link from the
     cell's own pdfs ``c0 … c{Q-1}`` (loaded inside the link's branch), the adjoint's first pass stores ``v_j`` of each
@@ -92,6 +96,8 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     F = [float(v) for v in force] if fm and not ff else None
     cF = [sum(c * f for c, f in zip(d, F)) for d in dirs] if fm and not ff else None
     inv = [stencil.inverse_direction_index(i) for i in range(Q)]
+    if mrt is not None and (trt is not None or fm == 'guo'):
+        raise NotImplementedError('MRT lattice kernels with TRT or the Guo force model')
     if trt is not None and fm == 'guo':
         raise NotImplementedError('TRT lattice kernels with the Guo force model')
     axes = ['z', 'y', 'x'][3 - D:]          # spatial axes, axis 0 slowest; x fastest
@@ -129,6 +135,17 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
 
     def c_(v):
         return f'({ct}){_c(v)}'
+
+    def mat_terms(M, vec, transpose=False):
+        """Σ_k M[i][k] vec_k (or M[k][i]) as C, zero entries left out (None when the row is all zeros)."""
+        def row(i):
+            t = []
+            for k in range(Q):
+                v = float(M[k][i] if transpose else M[i][k])
+                if v != 0.0:
+                    t.append(f'{c_(v)} * {vec}{k}')
+            return ' + '.join(t) if t else None
+        return row
 
     def Fa(a):
         """Force component a: a constant, or the cell's value (``force_field``)."""
@@ -358,14 +375,16 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     cell_density(L, 's', 'src')
     pull_loads(L, 's', 'src')
     moments(L)
-    if trt is not None:
-        # TRT: every population's equilibrium first (the collision of i reads feq of ī too)
+    if trt is not None or mrt is not None:
+        # TRT / MRT: every population's equilibrium first (the collision of i reads feq of other populations too)
         for i in range(Q):
             L.append(f'  {ct} fe{i};')
             L.append(f'  {{ const {ct} cu = {cu_expr(i)};')
             L.append(f'    const {ct} poly = cu * (({ct})3 + ({ct})4.5 * cu) - ({ct})1.5 * usq;')
             L.append(f'    fe{i} = ' + (f'{c_(w[i])} * rho * (({ct})1 + poly);' if compressible
                                         else f'{c_(w[i])} * (rho + poly);') + ' }')
+        if mrt is not None:
+            L.append(f'  const {ct} ' + ', '.join(f'nq{k} = f{k} - fe{k}' for k in range(Q)) + ';')   # f − feq
     for i in range(Q):
         L.append(f'  {{ const {ct} cu = {cu_expr(i)};')
         L.append(f'    const {ct} poly = cu * (({ct})3 + ({ct})4.5 * cu) - ({ct})1.5 * usq;')
@@ -380,6 +399,9 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             j = inv[i]
             val = (f'(({ct})1 - ta) * f{i} - tb * f{j} + ta * fe{i} + tb * fe{j}{term}' if j != i else
                    f'f{i} + omega * (fe{i} - f{i}){term}')
+        elif mrt is not None:
+            pw, cc = mat_terms(mrt[0], 'nq')(i), mat_terms(mrt[1], 'nq')(i)
+            val = f'f{i}' + (f' - omega * ({pw})' if pw else '') + (f' - ({cc})' if cc else '') + term
         else:
             val = f'f{i} + omega * ({feq} - f{i}){term}'
         L.append('    ' + store('d', 'dst', i, dcoff, val) + ' }')
@@ -420,6 +442,12 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                  for q, _, _ in row[2]}) if fix else []
     if gq:
         L.append(f'  {ct} ' + ', '.join(f'G{q} = 0' for q in gq) + ';')      # Σ_j J_jq v_j (link programs)
+    if mrt is not None:
+        # h = Aᵀ g
+        for i in range(Q):
+            pw, cc = mat_terms(mrt[0], 'g', True)(i), mat_terms(mrt[1], 'g', True)(i)
+            hv = ' + '.join(t for t in ((f'omega * ({pw})' if pw else None), (f'({cc})' if cc else None)) if t)
+            L.append(f'  const {ct} h{i} = {hv or c_(0)};')
     L.append(f'  {ct} S = 0, A = 0;')
     for a in range(D):
         L.append(f'  {ct} B{a} = 0;')
@@ -433,6 +461,8 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             # the equilibrium sums over h_i = a g_i + b g_ī (rest population: ω g_0)
             hi = f'(ta * g{i} + tb * g{inv[i]})' if inv[i] != i else f'omega * g{i}'
             L.append(f'    const {ct} gw = {hi} * {c_(w[i])};')
+        elif mrt is not None:
+            L.append(f'    const {ct} gw = h{i} * {c_(w[i])};')
         else:
             L.append(f'    const {ct} gw = g{i} * {c_(w[i])};')
         L.append('    S += gw;')
@@ -449,7 +479,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                     if dirs[i][a]:
                         L.append(f'    E{a} {"+" if dirs[i][a] > 0 else "-"}= tf;')
             if ff and fm == 'simple':
-                gwm = f'(g{i} * {c_(w[i])})' if trt is not None else 'gw'
+                gwm = f'(g{i} * {c_(w[i])})' if trt is not None or mrt is not None else 'gw'
                 for a in range(D):
                     if dirs[i][a]:
                         L.append(f'    M{a} {"+" if dirs[i][a] > 0 else "-"}= {gwm};')
@@ -485,6 +515,8 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             L.append(f'  {{ {vq}{ct} v = (({ct})1 - ta) * g{j} - tb * g{inv[j]} + (A + {du});')
         elif trt is not None:
             L.append(f'  {{ {vq}{ct} v = (({ct})1 - omega) * g{j} + (A + {du});')
+        elif mrt is not None:
+            L.append(f'  {{ {vq}{ct} v = g{j} - h{j} + (A + {du});')
         else:
             L.append(f'  {{ {vq}{ct} v = (({ct})1 - omega) * g{j} + omega * (A + {du});')
         k = key(dirs[j])
@@ -707,8 +739,10 @@ class LatticeKernels:
     bounce-back)."""
 
     def __init__(self, stencil, compressible, dtype, walls, target, links=None, force_model=None, force=None,
-                 force_field=False, trt=None, programs=None):
+                 force_field=False, trt=None, programs=None, mrt=None):
         self.stencil = stencil
+        # MRT: (P_ω, C) relaxation matrices as float tuples (``_method.mrt_relaxation_matrices``)
+        self.mrt = None if mrt is None else tuple(tuple(tuple(float(v) for v in row) for row in M) for M in mrt)
         self.trt = None if trt is None else (str(trt[0]), float(trt[1]))
         self.force_model = force_model
         self.force_field = bool(force_model) and bool(force_field)
@@ -739,13 +773,14 @@ class LatticeKernels:
         of the cells next to link-program walls."""
         if self.target != 'gpu':
             return _emit(self.stencil, self.compressible, self.ct, self.walls, 'c', 'i64', 'ptr', self.links,
-                         self.force_model, self.force, self.force_field, self.trt, self.programs)
+                         self.force_model, self.force, self.force_field, self.trt, self.programs, mrt=self.mrt)
         if fix:
             return _emit(self.stencil, self.compressible, self.ct, self.walls, 'hip', idx, addr, self.links,
-                         self.force_model, self.force, self.force_field, self.trt, self.programs, mode='fix')
+                         self.force_model, self.force, self.force_field, self.trt, self.programs, mode='fix',
+                         mrt=self.mrt)
         return _emit(self.stencil, self.compressible, self.ct, self.walls, 'hip', idx, addr, self.links,
                      self.force_model, self.force, self.force_field, self.trt, self.programs,
-                     mode='main' if self.programs is not None else 'inline')
+                     mode='main' if self.programs is not None else 'inline', mrt=self.mrt)
 
     # -- GPU ---------------------------------------------------------------------------------------
     def _gpu_fn(self, which, idx, addr, device):

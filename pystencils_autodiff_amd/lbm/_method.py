@@ -26,7 +26,7 @@ import sympy as sp
 from .. import ps
 
 __all__ = ['LBStencil', 'create_lb_update_rule', 'create_lb_adjoint_rule', 'macroscopic_getter',
-           'equilibrium_setter', 'relaxation_rate_from_magic_number']
+           'equilibrium_setter', 'relaxation_rate_from_magic_number', 'mrt_moments', 'mrt_relaxation_matrices']
 
 
 class LBStencil:
@@ -144,7 +144,67 @@ def relaxation_rate_from_magic_number(relaxation_rate, magic_number=sp.Rational(
     return (4 - 2 * w) / (4 * lam * w + 2 - w)
 
 
-METHODS = ('srt', 'trt')
+METHODS = ('srt', 'trt', 'mrt')
+
+# MRT moment polynomials (exponents per axis), grouped by relaxation rate: lbmpy's weighted-orthogonal MRT groups
+# (shear, bulk, third order, fourth order) [ext]; conserved moments (density, momentum) first
+_MRT_POLYS = {
+    2: [('conserved', [(0, 0)]), ('conserved', [(1, 0)]), ('conserved', [(0, 1)]),
+        ('bulk', [(2, 0), (0, 2)]), ('shear', [(2, 0), (0, 2, -1)]), ('shear', [(1, 1)]),
+        ('third', [(2, 1)]), ('third', [(1, 2)]), ('fourth', [(2, 2)])],
+    3: [('conserved', [(0, 0, 0)]), ('conserved', [(1, 0, 0)]), ('conserved', [(0, 1, 0)]), ('conserved', [(0, 0, 1)]),
+        ('bulk', [(2, 0, 0), (0, 2, 0), (0, 0, 2)]),
+        ('shear', [(2, 0, 0, 2), (0, 2, 0, -1), (0, 0, 2, -1)]), ('shear', [(0, 2, 0), (0, 0, 2, -1)]),
+        ('shear', [(1, 1, 0)]), ('shear', [(1, 0, 1)]), ('shear', [(0, 1, 1)]),
+        ('third', [(2, 1, 0)]), ('third', [(2, 0, 1)]), ('third', [(1, 2, 0)]), ('third', [(0, 2, 1)]),
+        ('third', [(1, 0, 2)]), ('third', [(0, 1, 2)]),
+        ('fourth', [(2, 2, 0)]), ('fourth', [(2, 0, 2)]), ('fourth', [(0, 2, 2)])],
+}
+MRT_GROUPS = ('shear', 'bulk', 'third', 'fourth')
+
+
+def mrt_moments(stencil):
+    """The MRT moment basis of a D2Q9 / D3Q19 stencil: ``[(group, row)]`` — each row the moment's values per
+    direction (exact rationals), made orthogonal under the lattice weights (Σ_i w_i m_i n_i = 0) by Gram–Schmidt in
+    the listed order (conserved → second order (bulk = |c|², shear = the traceless and off-diagonal parts) → third →
+    fourth order). A polynomial is a list of monomial exponent tuples, an optional last entry the coefficient."""
+    st = stencil if isinstance(stencil, LBStencil) else LBStencil(stencil)
+    if (st.D, st.Q) not in ((2, 9), (3, 19)):
+        raise NotImplementedError(f'MRT moments for {st.name}: D2Q9 and D3Q19 are restated')
+    w = st.weights
+    rows = []
+    for group, terms in _MRT_POLYS[st.D]:
+        vec = [sp.Integer(0)] * st.Q
+        for t in terms:
+            e, coef = t[:st.D], (sp.Integer(t[st.D]) if len(t) > st.D else sp.Integer(1))
+            for i, c in enumerate(st.directions):
+                m = sp.Integer(1)
+                for a in range(st.D):
+                    m *= sp.Integer(c[a]) ** e[a]
+                vec[i] += coef * m
+        for _, r in rows:
+            proj = sum(wi * a * b for wi, a, b in zip(w, vec, r)) / sum(wi * b * b for wi, b in zip(w, r))
+            vec = [a - proj * b for a, b in zip(vec, r)]
+        if all(v == 0 for v in vec):
+            raise AssertionError(f'MRT moment basis of {st.name} is degenerate')
+        rows.append((group, vec))
+    return rows
+
+
+def mrt_relaxation_matrices(stencil):
+    """Per group: the projector ``P_g = M⁻¹ E_g M`` (E_g selects the group's moments) as exact rationals, ``P_g[i][k]``
+    — the collision's relaxation matrix is ``Σ_g s_g P_g`` (the conserved group relaxes with 0). With the weighted-
+    orthogonal rows m_k: ``P_g = Σ_{k∈g} W m_k m_kᵀ / (m_kᵀ W m_k)``."""
+    st = stencil if isinstance(stencil, LBStencil) else LBStencil(stencil)
+    w = st.weights
+    out = {}
+    for group, m in mrt_moments(st):
+        nrm = sum(wi * a * a for wi, a in zip(w, m))
+        P = out.setdefault(group, [[sp.Integer(0)] * st.Q for _ in range(st.Q)])
+        for i in range(st.Q):
+            for k in range(st.Q):
+                P[i][k] += w[i] * m[i] * m[k] / nrm
+    return out
 
 
 def create_lb_update_rule(stencil='D2Q9', relaxation_rate=None, compressible=False, src_field=None, dst_field=None,
@@ -158,6 +218,14 @@ def create_lb_update_rule(stencil='D2Q9', relaxation_rate=None, compressible=Fal
     (``relaxation_rate_from_magic_number``, lbmpy's default 3/16):
 
         dst_i = f_i − ω₊ (f_i⁺ − feq_i⁺) − ω₋ (f_i⁻ − feq_i⁻),   x_i^± = (x_i ± x_ī) / 2.
+
+    MRT (D2Q9, D3Q19) relaxes the weighted-orthogonal moments (``mrt_moments``) group by group —
+    ``relaxation_rates=[shear, bulk, third, fourth]`` (lbmpy's order; missing entries default to ω, the first to ω):
+
+        dst = f − Σ_g s_g P_g (f − feq),   P_g = M⁻¹ E_g M   (``mrt_relaxation_matrices``)
+
+    — all rates ω is SRT, ``[ω, ω, ω₋, ω]`` is TRT (the odd non-conserved moments are the third-order ones). The
+    rule keeps ``ac.mrt_rates`` (per group) for the lattice kernels.
 
     Fields: ``src(q)``/``dst(q)`` vector fields in ``layout`` (``'fzyx'``: components slowest, lbmpy's default)
     unless given. ``force_model`` ('simple' or 'guo'; TRT: 'simple') with ``force``: a body force — constant (numbers
@@ -173,19 +241,33 @@ def create_lb_update_rule(stencil='D2Q9', relaxation_rate=None, compressible=Fal
     if src_field is None or dst_field is None:
         src_field, dst_field = ps.fields(f"src({st.Q}), dst({st.Q}): {data_type}[{st.D}D]", layout=layout)
     if relaxation_rates is not None:
-        if method != 'trt' or len(relaxation_rates) != 2:
+        if method == 'trt' and len(relaxation_rates) != 2:
             raise ValueError('relaxation_rates: [even, odd] for the TRT method')
+        if method == 'mrt' and not 1 <= len(relaxation_rates) <= 4:
+            raise ValueError('relaxation_rates: [shear, bulk, third, fourth] for the MRT method')
+        if method == 'srt':
+            raise ValueError('relaxation_rates: for the TRT / MRT methods (SRT: relaxation_rate)')
         relaxation_rate = relaxation_rates[0]
     omega = sp.Symbol('omega') if relaxation_rate is None else sp.sympify(relaxation_rate)
     f = [src_field[tuple(-c for c in st.directions[i])](i) for i in range(st.Q)]
-    if method == 'trt' and force_model is not None and str(force_model).lower() != 'simple':
-        raise NotImplementedError("TRT with force_model 'guo' (its prefactor per moment) is not restated: 'simple'")
+    if method in ('trt', 'mrt') and force_model is not None and str(force_model).lower() != 'simple':
+        raise NotImplementedError(f"{method.upper()} with force_model 'guo' (its prefactor per moment) is not "
+                                  "restated: 'simple'")
     shift, term = _force(force_model, force, st)
     rho, us, subs = _moments(st, f, compressible, shift)
     feq = [_feq(st, i, rho, us, compressible) for i in range(st.Q)]
+    mrt_rates = None
     if method == 'srt':
         omega_odd = None
         coll = [f[i] + omega * (feq[i] - f[i]) for i in range(st.Q)]
+    elif method == 'mrt':
+        omega_odd = None
+        given = list(relaxation_rates or [])
+        mrt_rates = {g: (sp.sympify(given[n]) if n < len(given) else omega) for n, g in enumerate(MRT_GROUPS)}
+        P = mrt_relaxation_matrices(st)
+        neq = [f[k] - feq[k] for k in range(st.Q)]
+        coll = [f[i] - sum(mrt_rates[g] * sum(P[g][i][k] * neq[k] for k in range(st.Q) if P[g][i][k] != 0)
+                           for g in MRT_GROUPS) for i in range(st.Q)]
     else:
         omega_odd = sp.sympify(relaxation_rates[1]) if relaxation_rates is not None else \
             relaxation_rate_from_magic_number(omega, magic_number)
@@ -200,6 +282,7 @@ def create_lb_update_rule(stencil='D2Q9', relaxation_rate=None, compressible=Fal
     ac.method = method
     ac.relaxation_rate_odd = omega_odd
     ac.magic_number = sp.sympify(magic_number) if method == 'trt' and relaxation_rates is None else None
+    ac.mrt_rates = mrt_rates
     ac.force_model = None if force_model is None else str(force_model).lower()
     ac.force = None if force is None else tuple(force_components(force, st.D))
     return ac
@@ -222,6 +305,7 @@ def create_lb_adjoint_rule(update_rule, diff_fields_prefix='diff'):
     comp = update_rule.compressible
     omega = update_rule.relaxation_rate
     trt = getattr(update_rule, 'method', 'srt') == 'trt'
+    mrt = getattr(update_rule, 'method', 'srt') == 'mrt'
     src = update_rule.free_fields
     dst = update_rule.bound_fields
     (src,), (dst,) = tuple(src), tuple(dst)
@@ -239,6 +323,15 @@ def create_lb_adjoint_rule(update_rule, diff_fields_prefix='diff'):
         subs += [ps.Assignment(ka, (omega + update_rule.relaxation_rate_odd) / 2),
                  ps.Assignment(kb, (omega - update_rule.relaxation_rate_odd) / 2)]
         h = [ka * g[i] + kb * g[opp[i]] for i in range(st.Q)]
+    elif mrt:
+        # h = Aᵀ g, A = Σ_g s_g P_g: dst = f − A (f − feq)  ⇒  v_j = g_j − h_j + (Jfeqᵀ h)_j
+        P = mrt_relaxation_matrices(st)
+        hs = sp.symbols(f'mrt_h_:{st.Q}')
+        for i in range(st.Q):
+            subs.append(ps.Assignment(hs[i], sum(update_rule.mrt_rates[gr] * sum(P[gr][k][i] * g[k] for k in range(st.Q)
+                                                                                if P[gr][k][i] != 0)
+                                                 for gr in MRT_GROUPS)))
+        h = list(hs)
     else:
         h = g
     subs.append(ps.Assignment(A, sum(gi * sp.diff(fe, rho) for gi, fe in zip(h, feq))))
@@ -253,6 +346,8 @@ def create_lb_adjoint_rule(update_rule, diff_fields_prefix='diff'):
         eq = A + sum(B[a] * du[a] for a in range(st.D) if du[a] != 0)
         if trt:
             rhs = (1 - ka) * g[j] - kb * g[opp[j]] + eq
+        elif mrt:
+            rhs = g[j] - h[j] + eq
         else:
             rhs = (1 - omega) * g[j] + omega * eq
         main.append(ps.Assignment(dsrc[tuple(-ci for ci in c)](j), rhs))

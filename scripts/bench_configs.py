@@ -225,13 +225,14 @@ def run_slab(name, builder, shape, dtype, full_cells, steps=20, warmup=3):
 
 
 def run_lbm(name, stencil, shape, dtype, T=10, reps=5, compressible=False, walls=False, force_model=None,
-            force_field=False):
+            force_field=False, method='srt'):
     """Lattice Boltzmann time-step op (lbm.AutoDiffLatticeBoltzmannStep.create_timestep_op): T forward steps
     and the T adjoint steps, HIP events around Op.apply and backward (back-to-back applies). MLUPS = cells · T / time; algorithmic
     bytes per cell and step: forward 2q·s (read src, write dst), adjoint 3q·s (read diffdst and the recorded
     src, write diffsrc), s = element size; the ghost sync, state records and adjoint border fills are extra.
     ``force_field``: a per-cell force (a D-component fzyx field, an input of the op): + D·s per cell and step forward
     (the force read), + 3·D·s adjoint (the force read, its accumulated adjoint read and written)."""
+    import sympy as sp
     import torch
 
     from pystencils_autodiff_amd import lbm
@@ -241,8 +242,9 @@ def run_lbm(name, stencil, shape, dtype, T=10, reps=5, compressible=False, walls
     force = (1e-5, -2e-5, 5e-6)[:D] if force_model else None
     if force_model and force_field:
         force = ps.fields(f"F({D}): {dts}[{D}D]", layout='fzyx')
+    mk = dict(method='mrt', relaxation_rates=[sp.Symbol('omega'), 1.1, 0.9, 1.2]) if method == 'mrt' else {}
     rule = lbm.create_lb_update_rule(stencil, compressible=compressible, data_type=dts, force_model=force_model,
-                                     force=force)
+                                     force=force, **mk)
     step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.5, target='gpu')
     if walls:
         # a channel: no-slip walls on the first and last rows of axis 1
@@ -303,7 +305,8 @@ def run_lbm(name, stencil, shape, dtype, T=10, reps=5, compressible=False, walls
            'fwd_ms': round(f_ms, 4), 'bwd_ms': round(b_ms, 4),
            'fwd_GBps': round((2 * q + (D if force_field else 0)) * es * cells * T / (f_ms * 1e-3) / 1e9, 1),
            'bwd_GBps': round((3 * q + (3 * D if force_field else 0)) * es * cells * T / (b_ms * 1e-3) / 1e9, 1),
-           'force': (f'{force_model}, per-cell field' if force_field else force_model) if force_model else None}
+           'force': (f'{force_model}, per-cell field' if force_field else force_model) if force_model else None,
+           'method': method}
     res['fwd_frac'] = round(res['fwd_GBps'] / PEAK, 4)
     res['bwd_frac'] = round(res['bwd_GBps'] / PEAK, 4)
     print(json.dumps(res))
@@ -386,11 +389,13 @@ def main():
             ('lbm_d2q9_f32_2048^2_channel', 'D2Q9', (2048, 2048), torch.float32, True),
             ('lbm_d3q19_f32_192^3_channel', 'D3Q19', (192, 192, 192), torch.float32, True),
             ('lbm_d2q9_f32_2048^2_pressure', 'D2Q9', (2048, 2048), torch.float32, 'pressure'),
-            ('lbm_d3q19_f32_192^3_pressure', 'D3Q19', (192, 192, 192), torch.float32, 'pressure')]
-    for name, stencil, shape, dt, walls in lbms:
+            ('lbm_d3q19_f32_192^3_pressure', 'D3Q19', (192, 192, 192), torch.float32, 'pressure'),
+            ('lbm_d2q9_f32_2048^2_mrt', 'D2Q9', (2048, 2048), torch.float32, False, 'mrt'),
+            ('lbm_d3q19_f32_192^3_mrt', 'D3Q19', (192, 192, 192), torch.float32, False, 'mrt')]
+    for name, stencil, shape, dt, walls, *method in lbms:
         if only and name not in only:
             continue
-        run_lbm(name, stencil, shape, dt, walls=walls)
+        run_lbm(name, stencil, shape, dt, walls=walls, method=method[0] if method else 'srt')
 
 
 if __name__ == '__main__':

@@ -1206,3 +1206,109 @@ def test_lbm_pressure_with_density_weighted_lid(target):
     step.run_backward(T)
     adj = step.adjoint_pdf_array.cpu().numpy() if target == 'gpu' else step.adjoint_pdf_array
     assert np.abs(adj - gref).max() <= 1e-11 * np.abs(gref).max()
+
+
+# --- MRT (lbmpy's weighted-orthogonal moment groups, restated) --------------------------------------------------
+MRT_RATES = dict(shear=1.3, bulk=1.1, third=0.9, fourth=1.2)
+
+
+def _mrt_case(stencil, shape, compressible, target, walls, dtype='float64', force=None):
+    kw = dict(force_model='simple', force=force) if force is not None else {}
+    rule = lbm.create_lb_update_rule(stencil, compressible=compressible, method='mrt', data_type=dtype,
+                                     relaxation_rates=[sp_omega(), MRT_RATES['bulk'], MRT_RATES['third'],
+                                                       MRT_RATES['fourth']], **kw)
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=MRT_RATES['shear'], target=target)
+    wall = np.zeros(shape, bool)
+    if walls:
+        for end in (0, -1):
+            sl = [slice(None)] * len(shape)
+            sl[1] = end
+            step.set_boundary_including_adjoint(lbm.NoSlip(), tuple(sl))
+            wall[tuple(sl)] = True
+    assert step._lattice is not None and step._lattice_mrt is not None
+    return step, wall, OL.mrt_matrix(stencil, MRT_RATES)
+
+
+def sp_omega():
+    import sympy as sp
+    return sp.Symbol('omega')
+
+
+MRT_CASES = [('D2Q9', (10, 7), True, False), ('D2Q9', (9, 12), False, True), ('D3Q19', (6, 5, 4), True, True),
+             ('D3Q19', (5, 6, 4), False, False)]
+
+
+@pytest.mark.parametrize('stencil,shape,compressible,walls', MRT_CASES)
+def test_lbm_mrt_cpu_vs_oracle(stencil, shape, compressible, walls):
+    """MRT on the C lattice kernels (relaxation matrix ω P_ω + C compiled in): T steps vs the oracle's moment-space
+    collision (its own Gram–Schmidt basis, ``M⁻¹ S M`` by numpy), the adjoint (h = Aᵀ g) vs torch's reverse mode."""
+    import torch
+    T = 4
+    step, wall, A = _mrt_case(stencil, shape, compressible, 'cpu', walls)
+    f0 = _init(stencil, shape, compressible, seed=51)
+    g = np.random.default_rng(52).standard_normal(f0.shape)
+    ft = torch.tensor(f0, requires_grad=True)
+    ref = OL.run_walls(ft, None, torch.tensor(wall), T, stencil, compressible, xp=torch, mrt=A)
+    (gref,) = torch.autograd.grad(ref, ft, torch.tensor(g))
+    srt = OL.run_walls(torch.tensor(f0), MRT_RATES['shear'], torch.tensor(wall), T, stencil, compressible, xp=torch)
+    assert float((ref.detach() - srt).abs().max()) > 1e-6          # the other rates are in
+    step.set_pdfs(f0)
+    step.run(T, record=True)
+    assert np.abs(step.pdf_array - ref.detach().numpy()).max() <= 1e-13 * np.abs(f0).max()
+    step.set_adjoint_pdfs(g)
+    step.run_backward(T)
+    assert np.abs(step.adjoint_pdf_array - gref.numpy()).max() <= 1e-12 * np.abs(gref.numpy()).max()
+
+
+def test_lbm_mrt_special_cases_and_generic_schedule():
+    """MRT with every rate ω is SRT and with [ω, ω, ω₋, ω] TRT (the only odd non-conserved moments are the third-order
+    ones); a rate that is another symbol runs on the rule's AutoDiffOp kernels and matches the lattice kernels."""
+    import sympy as sp
+    shape = (9, 8)
+    f0 = _init('D2Q9', shape, True, seed=53)
+    res = {}
+    for name, kw in (('srt', {}), ('mrt_all', dict(method='mrt')),
+                     ('trt', dict(method='trt', relaxation_rates=[sp.Symbol('omega'), 0.8])),
+                     ('mrt_trt', dict(method='mrt', relaxation_rates=[sp.Symbol('omega'), sp.Symbol('omega'), 0.8]))):
+        step = lbm.AutoDiffLatticeBoltzmannStep(lbm.create_lb_update_rule('D2Q9', compressible=True, **kw),
+                                                domain_size=shape, relaxation_rate=1.3, target='cpu')
+        step.set_pdfs(f0)
+        step.run(3)
+        res[name] = step.pdf_array.copy()
+    assert np.abs(res['srt'] - res['mrt_all']).max() <= 1e-14
+    assert np.abs(res['trt'] - res['mrt_trt']).max() <= 1e-14
+    sb = sp.Symbol('s_bulk')
+    rule = lbm.create_lb_update_rule('D2Q9', compressible=True, method='mrt',
+                                     relaxation_rates=[sp.Symbol('omega'), sb, 0.9, 1.2])
+    generic = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.3, target='cpu',
+                                               kernel_params={'s_bulk': 1.1})
+    assert generic._lattice is None                   # a rate that is neither ω nor a number: the AutoDiffOp kernels
+    lattice, _, _ = _mrt_case('D2Q9', shape, True, 'cpu', False)
+    for st in (generic, lattice):
+        st.set_pdfs(f0)
+        st.run(3)
+    assert np.abs(generic.pdf_array - lattice.pdf_array).max() <= 1e-13
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('stencil,shape,compressible,walls,dtype', [('D2Q9', (66, 40), True, True, 'float64'),
+                                                                     ('D3Q19', (20, 12, 10), False, False, 'float64'),
+                                                                     ('D3Q19', (16, 12, 10), True, True, 'float32')])
+def test_lbm_mrt_gpu_vs_oracle(stencil, shape, compressible, walls, dtype):
+    """MRT on the HIP lattice kernels through the timestep op vs the oracle and torch's reverse mode."""
+    import torch
+    T = 5
+    step, wall, A = _mrt_case(stencil, shape, compressible, 'gpu', walls, dtype)
+    f0 = _init(stencil, shape, compressible, seed=54)
+    g = np.random.default_rng(55).standard_normal(f0.shape)
+    ft = torch.tensor(f0, requires_grad=True)
+    ref = OL.run_walls(ft, None, torch.tensor(wall), T, stencil, compressible, xp=torch, mrt=A)
+    (gref,) = torch.autograd.grad(ref, ft, torch.tensor(g))
+    tdt = getattr(torch, dtype)
+    tol = 1e-12 if dtype == 'float64' else 2e-5
+    op = step.create_timestep_op(T)
+    x = torch.tensor(f0, dtype=tdt, device='cuda', requires_grad=True)
+    out = op.apply(x)
+    out.backward(torch.tensor(g, dtype=tdt, device='cuda'))
+    assert float((out.detach().double().cpu() - ref.detach()).abs().max()) <= tol * np.abs(f0).max()
+    assert float((x.grad.double().cpu() - gref).abs().max()) <= 10 * tol * float(gref.abs().max())
