@@ -888,9 +888,12 @@ def test_lbm_trt_rule_api():
                                             target='cpu')
     assert step._lattice is None
     with pytest.raises(NotImplementedError):
-        lbm.create_lb_update_rule('D2Q9', method='mrt')
+        lbm.create_lb_update_rule('D2Q9', method='cumulant')
     with pytest.raises(NotImplementedError):
-        lbm.create_lb_update_rule('D2Q9', method='trt', force_model='guo', force=(1e-3, 0))
+        lbm.create_lb_update_rule('D3Q27', method='mrt')          # MRT moments: D2Q9 and D3Q19
+    for m in ('trt', 'mrt'):
+        with pytest.raises(NotImplementedError):
+            lbm.create_lb_update_rule('D2Q9', method=m, force_model='guo', force=(1e-3, 0))
     with pytest.raises(ValueError):
         lbm.create_lb_update_rule('D2Q9', relaxation_rates=[1.2, 1.1])
 
