@@ -70,7 +70,7 @@ BAND_F32_IDLE_MAX_X = 1024
 # keys are this layer's tile parameters; an unknown one is a typo and raises.
 TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
              'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE', 'BLDR', 'BLAUX', 'BPAD', 'BZF', 'BREG', 'BMBR', 'BNT', 'BPE', 'BSI',
-             'BPRIO', 'BABL', 'BLW', 'BTB', 'BSHIFT', 'BDEAD')
+             'BPRIO', 'BABL', 'BLW', 'BTB', 'BSHIFT', 'BDEAD', 'BFM')
 
 
 def _band_config(ir, ve, shape, over):
@@ -160,7 +160,8 @@ def _band_config(ir, ve, shape, over):
                        BMBR=int(over.get('BMBR', 0)), BNT=int(over.get('BNT', 2)), BPE=int(over.get('BPE', 0)),
                        BSI=int(over.get('BSI', 0)), BPRIO=int(over.get('BPRIO', 0)), BABL=int(over.get('BABL', 0)),
                        BLW=int(over.get('BLW', 1)), BTB=int(over.get('BTB', 0)),
-                       BSHIFT=int(over.get('BSHIFT', 0)), BDEAD=int(over.get('BDEAD', 0)))
+                       BSHIFT=int(over.get('BSHIFT', 0)), BDEAD=int(over.get('BDEAD', 0)),
+                       BFM=int(over.get('BFM', 0)))
 
 
 def default_march_config(ir, ve, shape=None, tuning=None, band=True):
@@ -778,7 +779,7 @@ class HipStencilKernel:
             # unmasked stores when every band row lies in [ylo, yhi) and the x range is whole rows
             g0 = self.march_launch_geometry(shape, cfg, z_range, z_limits=z_limits)
             if not (g0['ylo'] == 0 and g0['yhi'] == g0['nty'] * cfg.BTY and g0['xlo'] == 0 and g0['xhi'] == g0['X']) or \
-                    g0['X'] % (16 // esize):                          # a partial last chunk per row
+                    g0['X'] % (16 // esize) or cfg.BFM:               # a partial last chunk per row (BFM: probe)
                 cfg = MarchConfig(**{**cfg.__dict__, 'BMASK': True,
                                      'BXW': g0['xlo'] == 0 and g0['xhi'] == g0['X'] and not cfg.XB})
         variant = ('march', cfg)
