@@ -278,7 +278,7 @@ def stream_pressure_walls(f, stencil, wall, pressure, rho_wall, compressible, xp
 
 
 def run_pressure_walls(f, omega, wall, pressure, rho_wall, steps, stencil='D2Q9', compressible=False, xp=None,
-                       omega_odd=None, wall_velocity=None, density_weighted=False):
+                       omega_odd=None, wall_velocity=None, density_weighted=False, mrt=None):
     """``steps`` stream-pull-collide steps with (moving) bounce-back walls and pressure cells; wall cells keep their
     state."""
     if xp is None:
@@ -286,6 +286,7 @@ def run_pressure_walls(f, omega, wall, pressure, rho_wall, steps, stencil='D2Q9'
     keep = wall[..., None] if xp.__name__ != 'torch' else wall.unsqueeze(-1)
     for _ in range(steps):
         new = collide(stream_pressure_walls(f, stencil, wall, pressure, rho_wall, compressible, xp, wall_velocity,
-                                            density_weighted), omega, stencil, compressible, xp, omega_odd=omega_odd)
+                                            density_weighted), omega, stencil, compressible, xp, omega_odd=omega_odd,
+                      mrt=mrt)
         f = xp.where(keep, f, new)
     return f

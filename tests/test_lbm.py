@@ -1315,3 +1315,46 @@ def test_lbm_mrt_gpu_vs_oracle(stencil, shape, compressible, walls, dtype):
     out.backward(torch.tensor(g, dtype=tdt, device='cuda'))
     assert float((out.detach().double().cpu() - ref.detach()).abs().max()) <= tol * np.abs(f0).max()
     assert float((x.grad.double().cpu() - gref).abs().max()) <= 10 * tol * float(gref.abs().max())
+
+
+@pytest.mark.parametrize('target', ['cpu', pytest.param('gpu', marks=pytest.mark.gpu)])
+def test_lbm_mrt_pressure_channel(target):
+    """MRT with link-program walls: a D3Q19 pressure-driven channel (FixedDensity inlet / outlet, no-slip walls) on
+    the MRT lattice kernels — on the GPU through the fix-up kernels — vs the oracle and torch's reverse mode."""
+    import sympy as sp
+    import torch
+    stencil, shape, T = 'D3Q19', (10, 7, 6), 4
+    rule = lbm.create_lb_update_rule(stencil, compressible=True, method='mrt',
+                                     relaxation_rates=[sp.Symbol('omega'), MRT_RATES['bulk'], MRT_RATES['third'],
+                                                       MRT_RATES['fourth']])
+    step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=MRT_RATES['shear'], target=target)
+    wall = np.zeros(shape, bool)
+    for ax in (1, 2):
+        for end in (0, -1):
+            sl = [slice(None)] * 3
+            sl[ax] = end
+            step.set_boundary_including_adjoint(lbm.NoSlip(), tuple(sl))
+            wall[tuple(sl)] = True
+    step.set_boundary_including_adjoint(lbm.FixedDensity(RHO_IN), (0, slice(1, -1), slice(1, -1)))
+    step.set_boundary_including_adjoint(lbm.FixedDensity(RHO_OUT), (-1, slice(1, -1), slice(1, -1)))
+    pressure = np.zeros(shape, bool)
+    pressure[0, 1:-1, 1:-1] = pressure[-1, 1:-1, 1:-1] = True
+    wall |= pressure
+    rho_w = np.where(pressure, np.where(np.arange(shape[0])[:, None, None] == 0, RHO_IN, RHO_OUT), 1.0)
+    K = step._lattice_kernels()
+    assert K.programs is not None and K.mrt is not None
+    f0 = _init(stencil, shape, True, seed=61)
+    g = np.random.default_rng(62).standard_normal(f0.shape)
+    ft = torch.tensor(f0, requires_grad=True)
+    ref = OL.run_pressure_walls(ft, None, torch.tensor(wall), torch.tensor(pressure), torch.tensor(rho_w), T, stencil,
+                                True, xp=torch, mrt=OL.mrt_matrix(stencil, MRT_RATES))
+    (gref,) = torch.autograd.grad(ref, ft, torch.tensor(g))
+    ref, gref = ref.detach().numpy(), gref.numpy()
+    dev = (lambda a: torch.tensor(a, device='cuda')) if target == 'gpu' else (lambda a: a)
+    host = (lambda a: a.cpu().numpy()) if target == 'gpu' else (lambda a: a)
+    step.set_pdfs(dev(f0))
+    step.run(T, record=True)
+    assert np.abs(host(step.pdf_array) - ref).max() <= 1e-12 * np.abs(f0).max()
+    step.set_adjoint_pdfs(dev(g))
+    step.run_backward(T)
+    assert np.abs(host(step.adjoint_pdf_array) - gref).max() <= 1e-11 * np.abs(gref).max()
