@@ -442,6 +442,11 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                  for q, _, _ in row[2]}) if fix else []
     if gq:
         L.append(f'  {ct} ' + ', '.join(f'G{q} = 0' for q in gq) + ';')      # Σ_j J_jq v_j (link programs)
+        # the cell's own pdfs, once: every listed cell has a program link (not per link and row)
+        used = sorted({int(m) for pg in programs if pg is not None for row in pg if row is not None
+                       for _, jl, je in row[2] for m in re.findall(r'\bc(\d+)\b', ' '.join(jl) + ' ' + je)})
+        if used:
+            L.append('  ' + ' '.join(f'const {ct} c{q} = {load("s", "src", q, f"so_{centre}")};' for q in used))
     if mrt is not None:
         # h = Aᵀ g
         for i in range(Q):
@@ -528,9 +533,12 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                 # a program-linked component: Σ_j J_jq(c) v_j (c: the cell's own pre-streaming pdfs)
                 L.append(f'    if ((msk >> {j}) & 1u) switch (id{j}) {{')
                 for wid, pg in cases:
-                    rows = ' '.join('{ ' + ' '.join(jl) + f' G{q} += ({je}) * v; }}' for q, jl, je in pg[2])
-                    ld = own_loads(rows, lambda q: load('s', 'src', q, f'so_{centre}'))
-                    L.append(f'      case {wid}: {{ {ld} {rows} }} break;')
+                    if len({jl for _, jl, _ in pg[2]}) == 1:
+                        # one set of temporaries for the whole row (FixedDensity.program): emitted once
+                        rows = ' '.join(pg[2][0][1]) + ' ' + ' '.join(f'G{q} += ({je}) * v;' for q, _, je in pg[2])
+                    else:
+                        rows = ' '.join('{ ' + ' '.join(jl) + f' G{q} += ({je}) * v; }}' for q, jl, je in pg[2])
+                    L.append(f'      case {wid}: {{ {rows} }} break;')
                 L.append('      default: break;\n    }')
             elif cases:
                 # a program-linked component: its v for the second pass (the Jacobian row is evaluated there)
