@@ -410,7 +410,7 @@ def _c_printer():
     return P()
 
 
-def _program_code(exprs, nsyms):
+def _program_code(exprs):
     """(temporaries, expressions) as C: ``const T lt_k = …;`` lines (common subexpressions) and one expression per
     input, in the cell's own pdfs ``c0 … c{Q-1}``."""
     pr = _c_printer()
@@ -458,7 +458,7 @@ def link_program(forward_bc, adjoint_bc, lb_method):
             raise NotImplementedError(f'{forward_bc!r}: the lattice kernels take links of the fluid cell\'s own pdfs '
                                       f'and constants, got {rhs}')
         value = rhs.xreplace(own)
-        lines, (val,) = _program_code([value], st.Q)
+        lines, (val,) = _program_code([value])
         if derived:
             # the adjoint object is the transposed derivative of this link (AdjointBoundaryCondition): its Jacobian
             # row straight from the forward expression (what the transposed AD prints, without its cost per link)
@@ -497,7 +497,7 @@ def link_program(forward_bc, adjoint_bc, lb_method):
                 jac.append((k, jk))
         jrows = []
         for k, jk in jac:
-            jl, (je,) = _program_code([jk], st.Q)
+            jl, (je,) = _program_code([jk])
             jrows.append((k, jl, je))
         out.append((lines, val, tuple(jrows)))
     return tuple(out)
