@@ -21,7 +21,10 @@ D3Q19 = ([(0, 0, 0), (0, 1, 0), (0, -1, 0), (-1, 0, 0), (1, 0, 0), (0, 0, 1), (0
           (-1, -1, 0), (1, -1, 0), (0, 1, 1), (0, -1, 1), (-1, 0, 1), (1, 0, 1), (0, 1, -1), (0, -1, -1),
           (-1, 0, -1), (1, 0, -1)],
          [Fraction(1, 3)] + [Fraction(1, 18)] * 6 + [Fraction(1, 36)] * 12)
-SETS = {'D2Q9': D2Q9, 'D3Q19': D3Q19}
+D3Q27 = (D3Q19[0] + [(1, 1, 1), (-1, 1, 1), (1, -1, 1), (-1, -1, 1), (1, 1, -1), (-1, 1, -1), (1, -1, -1),
+                     (-1, -1, -1)],
+         [Fraction(8, 27)] + [Fraction(2, 27)] * 6 + [Fraction(1, 54)] * 12 + [Fraction(1, 216)] * 8)
+SETS = {'D2Q9': D2Q9, 'D3Q19': D3Q19, 'D3Q27': D3Q27}
 
 
 def _roll(xp, a, shift, axis):
@@ -52,10 +55,10 @@ def trt_odd_rate(omega, magic=3.0 / 16.0):
 # MRT moments (lbmpy's weighted-orthogonal MRT groups, restated): monomials c_x^a c_y^b (c_z^c) with integer
 # coefficients, Gram–Schmidt-orthogonalised under the lattice weights in this order
 MRT_BASIS = {
-    2: [('cons', {(0, 0): 1}), ('cons', {(1, 0): 1}), ('cons', {(0, 1): 1}), ('bulk', {(2, 0): 1, (0, 2): 1}),
+    9: [('cons', {(0, 0): 1}), ('cons', {(1, 0): 1}), ('cons', {(0, 1): 1}), ('bulk', {(2, 0): 1, (0, 2): 1}),
         ('shear', {(2, 0): 1, (0, 2): -1}), ('shear', {(1, 1): 1}), ('third', {(2, 1): 1}), ('third', {(1, 2): 1}),
         ('fourth', {(2, 2): 1})],
-    3: [('cons', {(0, 0, 0): 1}), ('cons', {(1, 0, 0): 1}), ('cons', {(0, 1, 0): 1}), ('cons', {(0, 0, 1): 1}),
+    19: [('cons', {(0, 0, 0): 1}), ('cons', {(1, 0, 0): 1}), ('cons', {(0, 1, 0): 1}), ('cons', {(0, 0, 1): 1}),
         ('bulk', {(2, 0, 0): 1, (0, 2, 0): 1, (0, 0, 2): 1}),
         ('shear', {(2, 0, 0): 2, (0, 2, 0): -1, (0, 0, 2): -1}), ('shear', {(0, 2, 0): 1, (0, 0, 2): -1}),
         ('shear', {(1, 1, 0): 1}), ('shear', {(1, 0, 1): 1}), ('shear', {(0, 1, 1): 1}),
@@ -63,6 +66,9 @@ MRT_BASIS = {
         ('third', {(1, 0, 2): 1}), ('third', {(0, 1, 2): 1}),
         ('fourth', {(2, 2, 0): 1}), ('fourth', {(2, 0, 2): 1}), ('fourth', {(0, 2, 2): 1})],
 }
+# D3Q27: + c_x c_y c_z (third order) and the fourth- to sixth-order monomials (relaxed with the fourth-order rate)
+MRT_BASIS[27] = MRT_BASIS[19][:16] + [('third', {(1, 1, 1): 1})] + MRT_BASIS[19][16:] + \
+    [('fourth', {e: 1}) for e in ((2, 1, 1), (1, 2, 1), (1, 1, 2), (2, 2, 1), (2, 1, 2), (1, 2, 2), (2, 2, 2))]
 
 
 def mrt_matrix(stencil, rates):
@@ -73,7 +79,7 @@ def mrt_matrix(stencil, rates):
     D = len(dirs[0])
     W = np.array([float(x) for x in w])
     rows, groups = [], []
-    for grp, poly in MRT_BASIS[D]:
+    for grp, poly in MRT_BASIS[len(dirs)]:
         v = np.array([sum(cf * np.prod([c[a] ** e[a] for a in range(D)]) for e, cf in poly.items()) for c in dirs],
                      dtype=np.float64)
         for r in rows:

@@ -149,10 +149,10 @@ METHODS = ('srt', 'trt', 'mrt')
 # MRT moment polynomials (exponents per axis), grouped by relaxation rate: lbmpy's weighted-orthogonal MRT groups
 # (shear, bulk, third order, fourth order) [ext]; conserved moments (density, momentum) first
 _MRT_POLYS = {
-    2: [('conserved', [(0, 0)]), ('conserved', [(1, 0)]), ('conserved', [(0, 1)]),
+    (2, 9): [('conserved', [(0, 0)]), ('conserved', [(1, 0)]), ('conserved', [(0, 1)]),
         ('bulk', [(2, 0), (0, 2)]), ('shear', [(2, 0), (0, 2, -1)]), ('shear', [(1, 1)]),
         ('third', [(2, 1)]), ('third', [(1, 2)]), ('fourth', [(2, 2)])],
-    3: [('conserved', [(0, 0, 0)]), ('conserved', [(1, 0, 0)]), ('conserved', [(0, 1, 0)]), ('conserved', [(0, 0, 1)]),
+    (3, 19): [('conserved', [(0, 0, 0)]), ('conserved', [(1, 0, 0)]), ('conserved', [(0, 1, 0)]), ('conserved', [(0, 0, 1)]),
         ('bulk', [(2, 0, 0), (0, 2, 0), (0, 0, 2)]),
         ('shear', [(2, 0, 0, 2), (0, 2, 0, -1), (0, 0, 2, -1)]), ('shear', [(0, 2, 0), (0, 0, 2, -1)]),
         ('shear', [(1, 1, 0)]), ('shear', [(1, 0, 1)]), ('shear', [(0, 1, 1)]),
@@ -160,20 +160,25 @@ _MRT_POLYS = {
         ('third', [(1, 0, 2)]), ('third', [(0, 1, 2)]),
         ('fourth', [(2, 2, 0)]), ('fourth', [(2, 0, 2)]), ('fourth', [(0, 2, 2)])],
 }
+# D3Q27: the D3Q19 moments plus xyz (third order) and the fourth- to sixth-order ones (all relaxing with the last rate)
+_MRT_POLYS[(3, 27)] = _MRT_POLYS[(3, 19)][:16] + [('third', [(1, 1, 1)])] + _MRT_POLYS[(3, 19)][16:] + \
+    [('fourth', [(2, 1, 1)]), ('fourth', [(1, 2, 1)]), ('fourth', [(1, 1, 2)]), ('fourth', [(2, 2, 1)]),
+     ('fourth', [(2, 1, 2)]), ('fourth', [(1, 2, 2)]), ('fourth', [(2, 2, 2)])]
 MRT_GROUPS = ('shear', 'bulk', 'third', 'fourth')
 
 
 def mrt_moments(stencil):
-    """The MRT moment basis of a D2Q9 / D3Q19 stencil: ``[(group, row)]`` — each row the moment's values per
+    """The MRT moment basis of a D2Q9 / D3Q19 / D3Q27 stencil: ``[(group, row)]`` — each row the moment's values per
     direction (exact rationals), made orthogonal under the lattice weights (Σ_i w_i m_i n_i = 0) by Gram–Schmidt in
     the listed order (conserved → second order (bulk = |c|², shear = the traceless and off-diagonal parts) → third →
-    fourth order). A polynomial is a list of monomial exponent tuples, an optional last entry the coefficient."""
+    fourth order; D3Q27's fifth- and sixth-order moments relax with the fourth-order rate). A polynomial is a list of
+    monomial exponent tuples, an optional last entry the coefficient."""
     st = stencil if isinstance(stencil, LBStencil) else LBStencil(stencil)
-    if (st.D, st.Q) not in ((2, 9), (3, 19)):
-        raise NotImplementedError(f'MRT moments for {st.name}: D2Q9 and D3Q19 are restated')
+    if (st.D, st.Q) not in _MRT_POLYS:
+        raise NotImplementedError(f'MRT moments for {st.name}: D2Q9, D3Q19 and D3Q27 are restated')
     w = st.weights
     rows = []
-    for group, terms in _MRT_POLYS[st.D]:
+    for group, terms in _MRT_POLYS[(st.D, st.Q)]:
         vec = [sp.Integer(0)] * st.Q
         for t in terms:
             e, coef = t[:st.D], (sp.Integer(t[st.D]) if len(t) > st.D else sp.Integer(1))
@@ -219,7 +224,7 @@ def create_lb_update_rule(stencil='D2Q9', relaxation_rate=None, compressible=Fal
 
         dst_i = f_i − ω₊ (f_i⁺ − feq_i⁺) − ω₋ (f_i⁻ − feq_i⁻),   x_i^± = (x_i ± x_ī) / 2.
 
-    MRT (D2Q9, D3Q19) relaxes the weighted-orthogonal moments (``mrt_moments``) group by group —
+    MRT (D2Q9, D3Q19, D3Q27) relaxes the weighted-orthogonal moments (``mrt_moments``) group by group —
     ``relaxation_rates=[shear, bulk, third, fourth]`` (lbmpy's order; missing entries default to ω, the first to ω):
 
         dst = f − Σ_g s_g P_g (f − feq),   P_g = M⁻¹ E_g M   (``mrt_relaxation_matrices``)

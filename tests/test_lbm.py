@@ -12,7 +12,7 @@ from pystencils_autodiff_amd import lbm, ps
 def _init(stencil, shape, compressible, seed=0):
     rng = np.random.default_rng(seed)
     D = len(shape)
-    Q = {'D2Q9': 9, 'D3Q19': 19}[stencil]
+    Q = {'D2Q9': 9, 'D3Q19': 19, 'D3Q27': 27}[stencil]
     rho = 1 + 0.05 * rng.standard_normal(shape)
     u = 0.04 * rng.standard_normal(shape + (D,))
     return OL.equilibrium(rho, u, stencil, compressible) + 0.01 * rng.standard_normal(shape + (Q,))
@@ -889,8 +889,6 @@ def test_lbm_trt_rule_api():
     assert step._lattice is None
     with pytest.raises(NotImplementedError):
         lbm.create_lb_update_rule('D2Q9', method='cumulant')
-    with pytest.raises(NotImplementedError):
-        lbm.create_lb_update_rule('D3Q27', method='mrt')          # MRT moments: D2Q9 and D3Q19
     for m in ('trt', 'mrt'):
         with pytest.raises(NotImplementedError):
             lbm.create_lb_update_rule('D2Q9', method=m, force_model='guo', force=(1e-3, 0))
@@ -1238,7 +1236,7 @@ def sp_omega():
 
 
 MRT_CASES = [('D2Q9', (10, 7), True, False), ('D2Q9', (9, 12), False, True), ('D3Q19', (6, 5, 4), True, True),
-             ('D3Q19', (5, 6, 4), False, False)]
+             ('D3Q19', (5, 6, 4), False, False), ('D3Q27', (5, 6, 4), True, True)]
 
 
 @pytest.mark.parametrize('stencil,shape,compressible,walls', MRT_CASES)
@@ -1296,7 +1294,8 @@ def test_lbm_mrt_special_cases_and_generic_schedule():
 @pytest.mark.gpu
 @pytest.mark.parametrize('stencil,shape,compressible,walls,dtype', [('D2Q9', (66, 40), True, True, 'float64'),
                                                                      ('D3Q19', (20, 12, 10), False, False, 'float64'),
-                                                                     ('D3Q19', (16, 12, 10), True, True, 'float32')])
+                                                                     ('D3Q19', (16, 12, 10), True, True, 'float32'),
+                                                                     ('D3Q27', (12, 10, 8), True, True, 'float64')])
 def test_lbm_mrt_gpu_vs_oracle(stencil, shape, compressible, walls, dtype):
     """MRT on the HIP lattice kernels through the timestep op vs the oracle and torch's reverse mode."""
     import torch
