@@ -96,10 +96,11 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     F = [float(v) for v in force] if fm and not ff else None
     cF = [sum(c * f for c, f in zip(d, F)) for d in dirs] if fm and not ff else None
     inv = [stencil.inverse_direction_index(i) for i in range(Q)]
-    if mrt is not None and (trt is not None or fm == 'guo'):
-        raise NotImplementedError('MRT lattice kernels with TRT or the Guo force model')
-    if trt is not None and fm == 'guo':
-        raise NotImplementedError('TRT lattice kernels with the Guo force model')
+    if mrt is not None and trt is not None:
+        raise NotImplementedError('MRT and TRT lattice kernels at once')
+    # Guo with TRT / MRT: the force term (prefactor 1 − ω/2 with the shear rate ω, as lbmpy's Guo model) is not
+    # relaxed by the collision matrix, so its adjoint sums run over g while the equilibrium's run over h
+    gsplit = fm == 'guo' and (trt is not None or mrt is not None)
     axes = ['z', 'y', 'x'][3 - D:]          # spatial axes, axis 0 slowest; x fastest
     ct = ctype
     hip = target == 'hip'
@@ -454,8 +455,12 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             hv = ' + '.join(t for t in ((f'omega * ({pw})' if pw else None), (f'({cc})' if cc else None)) if t)
             L.append(f'  const {ct} h{i} = {hv or c_(0)};')
     L.append(f'  {ct} S = 0, A = 0;')
+    if gsplit:
+        L.append(f'  {ct} Sg = 0;')                   # Σ_i g_i w_i (the force term's sums run over g)
     for a in range(D):
         L.append(f'  {ct} B{a} = 0;')
+        if gsplit:
+            L.append(f'  {ct} Bg{a} = 0;')            # Σ_i g_i w_i (3 + 9 c_i·u) c_ia
         if fm == 'guo':
             L.append(f'  {ct} E{a} = 0;')           # Σ_i g_i w_i c_ia (c_i·F)
         if ff and fm == 'simple':
@@ -471,6 +476,9 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         else:
             L.append(f'    const {ct} gw = g{i} * {c_(w[i])};')
         L.append('    S += gw;')
+        if gsplit:
+            L.append(f'    const {ct} gwg = g{i} * {c_(w[i])};')
+            L.append('    Sg += gwg;')
         if compressible:
             L.append(f'    A += gw * (({ct})1 + cu * (({ct})3 + ({ct})4.5 * cu) - ({ct})1.5 * usq);')
         if any(dirs[i]):
@@ -478,8 +486,13 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             for a in range(D):
                 if dirs[i][a]:
                     L.append(f'    B{a} {"+" if dirs[i][a] > 0 else "-"}= t;')
+            if gsplit:
+                L.append(f'    const {ct} tg = gwg * (({ct})3 + ({ct})9 * cu);')
+                for a in range(D):
+                    if dirs[i][a]:
+                        L.append(f'    Bg{a} {"+" if dirs[i][a] > 0 else "-"}= tg;')
             if fm == 'guo' and cFi(i):
-                L.append(f'    const {ct} tf = gw * {cFi(i)};')
+                L.append(f'    const {ct} tf = {"gwg" if gsplit else "gw"} * {cFi(i)};')
                 for a in range(D):
                     if dirs[i][a]:
                         L.append(f'    E{a} {"+" if dirs[i][a] > 0 else "-"}= tf;')
@@ -494,10 +507,14 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     for a in range(D):
         L.append(f'  B{a} -= ({ct})3 * u{a} * S;')
         if ff and fm == 'guo':
-            L.append(f'  const {ct} Bf{a} = B{a};')
+            # the explicit force term's F-derivative sums (over g: Bg for TRT / MRT, = B before the ρ scaling for SRT)
+            L.append(f'  const {ct} Bf{a} = ' + (f'Bg{a} - ({ct})3 * u{a} * Sg;' if gsplit else f'B{a};'))
         if compressible:
             L.append(f'  B{a} *= rho;')
-        if fm == 'guo':
+        if gsplit:
+            # the force term's derivative through u (TRT / MRT: v = g − h + A_h + Σ B_a ∂u_a/∂f_j, no ω factor)
+            L.append(f'  B{a} += kg * (({ct})9 * E{a} - ({ct})3 * {Fa(a)} * Sg);')
+        elif fm == 'guo':
             # the force term's derivative through u, scaled into B (v = … + ω (A + Σ B_a ∂u_a/∂f_j))
             L.append(f'  B{a} += kg * (({ct})9 * E{a} - ({ct})3 * {Fa(a)} * S) / omega;')
     if ff:
@@ -506,7 +523,10 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             if fm == 'simple':
                 val = f'({ct})3 * M{a}'
             else:
-                val = f'kg * Bf{a} + ({ct})0.5 * omega * B{a}' + (' * irho' if compressible else '')
+                # through the explicit term, and through the velocity shift ∂u_a/∂F_a = 1/2 (/ρ): Σ_i g_i ∂dst_i/∂u_a,
+                # which is ω B_a for SRT (B carries 1/ω) and B_a for TRT / MRT
+                sc = '' if gsplit else 'omega * '
+                val = f'kg * Bf{a} + ({ct})0.5 * {sc}B{a}' + (' * irho' if compressible else '')
             L.append(f'  dforce[(IDX){a} * f_c + fc] += {val};')
     if compressible:
         L.append(f'  const {ct} Bu = ' + ' + '.join(f'B{a} * u{a}' for a in range(D)) + ';')

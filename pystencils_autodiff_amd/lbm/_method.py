@@ -255,9 +255,8 @@ def create_lb_update_rule(stencil='D2Q9', relaxation_rate=None, compressible=Fal
         relaxation_rate = relaxation_rates[0]
     omega = sp.Symbol('omega') if relaxation_rate is None else sp.sympify(relaxation_rate)
     f = [src_field[tuple(-c for c in st.directions[i])](i) for i in range(st.Q)]
-    if method in ('trt', 'mrt') and force_model is not None and str(force_model).lower() != 'simple':
-        raise NotImplementedError(f"{method.upper()} with force_model 'guo' (its prefactor per moment) is not "
-                                  "restated: 'simple'")
+    # Guo with TRT / MRT: lbmpy's Guo model scales the force term by 1 − ω/2 with the shear rate ω [ext] (not by
+    # moment group); the velocity shift F/2 as for SRT
     shift, term = _force(force_model, force, st)
     rho, us, subs = _moments(st, f, compressible, shift)
     feq = [_feq(st, i, rho, us, compressible) for i in range(st.Q)]

@@ -889,9 +889,8 @@ def test_lbm_trt_rule_api():
     assert step._lattice is None
     with pytest.raises(NotImplementedError):
         lbm.create_lb_update_rule('D2Q9', method='cumulant')
-    for m in ('trt', 'mrt'):
-        with pytest.raises(NotImplementedError):
-            lbm.create_lb_update_rule('D2Q9', method=m, force_model='guo', force=(1e-3, 0))
+    for m in ('trt', 'mrt'):                      # Guo with TRT / MRT: lbmpy's shear-rate prefactor (tested below)
+        assert lbm.create_lb_update_rule('D2Q9', method=m, force_model='guo', force=(1e-3, 0)).force_model == 'guo'
     with pytest.raises(ValueError):
         lbm.create_lb_update_rule('D2Q9', relaxation_rates=[1.2, 1.1])
 
@@ -1357,3 +1356,81 @@ def test_lbm_mrt_pressure_channel(target):
     step.set_adjoint_pdfs(dev(g))
     step.run_backward(T)
     assert np.abs(host(step.adjoint_pdf_array) - gref).max() <= 1e-11 * np.abs(gref).max()
+
+
+# --- Guo forcing with TRT / MRT (lbmpy's Guo model: prefactor 1 − ω/2 with the shear rate, velocity shift F/2) --------
+GUO_METHOD_CASES = [('D2Q9', (9, 7), True, 'trt', 'const', 'lattice'), ('D2Q9', (8, 9), False, 'mrt', 'const', 'lattice'),
+                    ('D2Q9', (7, 8), True, 'mrt', 'field', 'lattice'), ('D3Q19', (5, 4, 6), True, 'trt', 'field', 'lattice'),
+                    ('D3Q19', (4, 5, 4), False, 'mrt', 'field', 'lattice'),
+                    ('D2Q9', (6, 7), True, 'mrt', 'field', 'autodiffop'), ('D2Q9', (7, 6), False, 'trt', 'const', 'autodiffop')]
+
+
+def _guo_method_case(stencil, shape, compressible, method, force_kind, schedule, target, T=3):
+    import os
+    import sympy as sp
+    import torch
+    D = len(shape)
+    w = sp.Symbol('omega')
+    if method == 'trt':
+        kw = dict(method='trt', relaxation_rates=[w, 0.9])
+        okw = dict(omega_odd=0.9)
+    else:
+        kw = dict(method='mrt', relaxation_rates=[w, MRT_RATES['bulk'], MRT_RATES['third'], MRT_RATES['fourth']])
+        okw = dict(mrt=OL.mrt_matrix(stencil, dict(MRT_RATES, shear=1.4)))
+    F = ps.fields(f"F({D}): float64[{D}D]", layout='fzyx') if force_kind == 'field' else (1e-3, -2e-3, 5e-4)[:D]
+    rule = lbm.create_lb_update_rule(stencil, compressible=compressible, force_model='guo', force=F, **kw)
+    old = os.environ.get('PSAD_LBM_LATTICE')
+    os.environ['PSAD_LBM_LATTICE'] = '1' if schedule == 'lattice' else '0'
+    try:
+        step = lbm.AutoDiffLatticeBoltzmannStep(rule, domain_size=shape, relaxation_rate=1.4, target=target)
+    finally:
+        if old is None:
+            os.environ.pop('PSAD_LBM_LATTICE')
+        else:
+            os.environ['PSAD_LBM_LATTICE'] = old
+    assert (step._lattice is not None) == (schedule == 'lattice')
+    op = step.create_timestep_op(T)
+    rng = np.random.default_rng(sum(shape) + 7)
+    f0 = _init(stencil, shape, compressible, seed=71)
+    dev = 'cuda' if target == 'gpu' else 'cpu'
+    x = torch.tensor(f0, device=dev, requires_grad=True)
+    ft = torch.tensor(f0, requires_grad=True)
+    g = torch.tensor(rng.standard_normal(f0.shape))
+    if force_kind == 'field':
+        Fv = 1e-3 * rng.standard_normal(shape + (D,))
+        Ft, Fr = torch.tensor(Fv, device=dev, requires_grad=True), torch.tensor(Fv, requires_grad=True)
+        out = op.apply(x, Ft)
+        ref = OL.run(ft, 1.4, T, stencil, compressible, xp=torch, force_model='guo',
+                     force=tuple(Fr[..., a] for a in range(D)), **okw)
+        out.backward(g.to(dev))
+        gx, gF = torch.autograd.grad(ref, (ft, Fr), g)
+        return out.detach().cpu(), ref.detach(), x.grad.cpu(), gx, Ft.grad.cpu(), gF
+    out = op.apply(x)
+    ref = OL.run(ft, 1.4, T, stencil, compressible, xp=torch, force_model='guo', force=F, **okw)
+    out.backward(g.to(dev))
+    (gx,) = torch.autograd.grad(ref, ft, g)
+    return out.detach().cpu(), ref.detach(), x.grad.cpu(), gx, None, None
+
+
+def _check_guo(res, tol):
+    out, ref, gx, gxr, gF, gFr = res
+    assert float((out - ref).abs().max()) <= tol * float(ref.abs().max())
+    assert float((gx - gxr).abs().max()) <= 10 * tol * float(gxr.abs().max())
+    if gF is not None:
+        assert float((gF - gFr).abs().max()) <= 10 * tol * float(gFr.abs().max())
+
+
+@pytest.mark.parametrize('stencil,shape,compressible,method,force_kind,schedule', GUO_METHOD_CASES)
+def test_lbm_guo_trt_mrt_cpu(stencil, shape, compressible, method, force_kind, schedule):
+    """Guo forcing with the TRT and MRT collisions (constant and per-cell forces) on the C kernels — the lattice kernels
+    (the force term's adjoint sums over g beside the equilibrium's over h) and the rule's AutoDiffOp kernels — vs the
+    oracle's collisions with Guo's term and torch's reverse mode (parity unpinned vs lbmpy)."""
+    _check_guo(_guo_method_case(stencil, shape, compressible, method, force_kind, schedule, 'cpu'), 1e-13)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('stencil,shape,compressible,method,force_kind,schedule',
+                         [c for c in GUO_METHOD_CASES if c[-1] == 'lattice'])
+def test_lbm_guo_trt_mrt_gpu(stencil, shape, compressible, method, force_kind, schedule):
+    """The same on the HIP lattice kernels."""
+    _check_guo(_guo_method_case(stencil, shape, compressible, method, force_kind, schedule, 'gpu'), 1e-12)
