@@ -64,6 +64,10 @@ BAND_REG_STAR_ODD = 1
 # row length (7-point 512²×520 0.389 vs 0.632 ms on zsum, profiles/r04_op_band_idle.log)
 BAND_F32_IDLE_MAX_X = 1024
 
+# (CX, NR) candidates of the LDS-DMA plane ring for stencils that are not linear off the centre plane
+# (hip_emitter._ring_ws_geometry), widest first: the first whose ring fits the LDS
+RING_WS_TILES = ((4, 4), (4, 2), (2, 4), (2, 2), (1, 4), (1, 2), (1, 1))
+
 # gpu_indexing_params keys of pystencils' own GPU indexing (``block_size``, ``maximum_block_size``, …, e.g.
 # ``gpu_indexing_params={'block_size': (8, 4, 2)}`` in the reference's tests/test_graph_datahandling.py:70): they
 # describe a one-thread-per-cell launch these schedules do not have, so they are accepted and ignored. Upper-case
@@ -214,6 +218,17 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             # profiles/r02_tune_small_*.log)
             cfg.update(WS=True, CX=4, NR=8 if ws0['kind'] == 'h' else 4, D=4, ZMIN=8, ZMAX=128, BLK=256)
             star_ws = True
+    ring_ws = False
+    if ir.ndim == 3 and not zsum_ok and not ir.has_index_dims:
+        # stencils not linear off the centre plane (products / functions of neighbour taps): the plane ring fed by
+        # an LDS-DMA loader wave, 2 planes in flight, the widest tile whose ring fits the LDS
+        for cx, nr in RING_WS_TILES:
+            c = {**cfg, 'CX': cx, 'NR': nr, 'WS': True, 'D': 2, 'ZMIN': 8, 'ZMAX': 128, 'BLK': 256}
+            w = ws_geometry(ir, MarchConfig(VE=ve, **c))
+            if w is not None and w['lds_bytes'] <= 160 * 1024:
+                cfg.update(c)
+                ring_ws = True
+                break
     if ir.ndim == 2:
         cfg.update(CX=4, WX=1, NR=4, VIEW2D='yx', NT_STORE=False)   # 256×16 tiles (4096²: 0.024 ms, 5.6 TB/s)
     if ir.has_index_dims:
@@ -236,6 +251,8 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
         for kv in env.split(','):
             k, v = kv.split('=')
             over[k.strip()] = v.strip() if k.strip() == 'VIEW2D' else int(v)
+    if ring_ws and any(k in over for k in ('CX', 'WX', 'NR', 'NW')) and 'WS' not in over:
+        cfg.update(WS=False, D=3)           # a tile override on the ring: the register-prefetch form it was sized for
     for k, v in over.items():
         if k not in TILE_KEYS:
             raise ValueError(f"unknown tile parameter '{k}' (gpu_indexing_params / PSAD_MARCH)")
@@ -727,7 +744,7 @@ class HipStencilKernel:
             # ring still takes 16-byte pieces (dword-aligned; the image in LDS keeps its layout) and zero-fills
             # past each row end (XM) — where the WS schedule applies
             probe = self._march_cfg(ve, shape, band=False)
-            xm = bool(probe.WS) and ws_geometry(ir, probe) is not None
+            xm = bool(probe.WS) and probe.ZSUM and ws_geometry(ir, probe) is not None
         xo = False
         if not xm and not fits(ve) and esize == 2 and not ir.has_index_dims and os.environ.get('PSAD_XO', '1') != '0' and \
                 all(np.dtype(f.dtype.numpy_dtype).itemsize == 2 for f in ir.fields) and \

@@ -11,6 +11,7 @@ import sympy as sp
 from . import ps
 
 __all__ = ['diffusion_7pt', 'laplace_5pt', 'stencil_27pt', 'readme_op', 'asym_7pt', 'vector_laplace_7pt',
+           'varcoef_diffusion_7pt',
            'WEIGHTS_27PT', 'ALPHA']
 
 ALPHA = 0.1
@@ -66,3 +67,14 @@ def vector_laplace_7pt(shape=None, dtype='float32', ncomp=3, layout='numpy'):
     nb = [(1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)]
     return ps.AssignmentCollection({out.center(c): sp.Add(*[u[o](c) for o in nb]) - 6 * u.center(c)
                                     for c in range(ncomp)})
+
+
+def varcoef_diffusion_7pt(shape=None, dtype='float32', alpha=ALPHA):
+    """3-D 7-point diffusion with a conductivity field ``k`` (face value = mean of the two cells):
+    ``out = u + α Σ₆ ½(k + k[nb])(u[nb] − u)`` — the learn-the-coefficient problem of differentiable PDE
+    solvers; its adjoint has two outputs (``diffu``, ``diffk``) from three inputs."""
+    u, k, out = _fields('u, k, out', dtype, 3, shape)
+    nb = [(1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)]
+    half = sp.Rational(1, 2)
+    return ps.AssignmentCollection({out.center: u.center + alpha * sp.Add(
+        *[half * (k.center + k[o]) * (u[o] - u.center) for o in nb])})

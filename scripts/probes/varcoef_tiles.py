@@ -1,0 +1,69 @@
+"""Tile sweep of the variable-coefficient diffusion (workloads.varcoef_diffusion_7pt) on the schedules a nonlinear
+multi-field stencil can take, forward and TF-MAD adjoint kernels timed alone with HIP events (median of 20 after
+warm-up), fraction of 8 TB/s from the algorithmic bytes (fwd 12, bwd 20 B/cell fp32). Timing only (parity:
+tests/test_varcoef.py).  python scripts/probes/varcoef_tiles.py [n=512] [tiles=all]"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', '..'))
+import pystencils_autodiff_amd as pa  # noqa: E402
+from pystencils_autodiff_amd import workloads as W  # noqa: E402
+from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel  # noqa: E402
+
+TILES = {
+    'default': {},
+    'reg': dict(CX=4, NR=4), 'reg_cx2nr2': dict(CX=2, NR=2), 'reg_cx1wx4nr4': dict(CX=1, WX=4, NR=4),
+    'ws_cx4nr4': dict(WS=1, CX=4, NR=4, D=2), 'ws_cx4nr2': dict(WS=1, CX=4, NR=2, D=2),
+    'ws_cx4nr2d3': dict(WS=1, CX=4, NR=2, D=3), 'ws_cx2nr4': dict(WS=1, CX=2, NR=4, D=2),
+    'ws_cx2nr4d3': dict(WS=1, CX=2, NR=4, D=3), 'ws_cx2nr2d3': dict(WS=1, CX=2, NR=2, D=3),
+    'ws_cx2nr2d4': dict(WS=1, CX=2, NR=2, D=4), 'ws_cx1nr4d3': dict(WS=1, CX=1, NR=4, D=3),
+    'ws_cx2wx2nr2': dict(WS=1, CX=2, WX=2, NR=2, D=3), 'ws_cx4nr1d3': dict(WS=1, CX=4, NR=1, D=3),
+    'ws_cx2nr2': dict(WS=1, CX=2, NR=2, D=2), 'ws_cx1nr4': dict(WS=1, CX=1, NR=4, D=2),
+    'ws_cx1nr2': dict(WS=1, CX=1, NR=2, D=2), 'ws_cx2nr1': dict(WS=1, CX=2, NR=1, D=2),
+    'ws_cx4nr1': dict(WS=1, CX=4, NR=1, D=2), 'ws_cx2nr2d1': dict(WS=1, CX=2, NR=2, D=1),
+}
+
+
+def timed(fn, reps=20):
+    for _ in range(5):
+        fn()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+    names = sys.argv[2].split(',') if len(sys.argv) > 2 else list(TILES)
+    op = pa.AutoDiffOp(W.varcoef_diffusion_7pt(), boundary_handling='zeros')
+    shape = (n, n, n)
+    u, k, d = (torch.rand(shape, device='cuda') for _ in range(3))
+    out, du, dk = (torch.empty(shape, device='cuda') for _ in range(3))
+    cells = n ** 3
+    for name in names:
+        p = TILES[name]
+        fk = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='vcf', target='gpu',
+                           gpu_indexing_params=p or None).compile()
+        bk = StencilKernel(op.backward_assignments, boundary_handling='zeros', function_name='vcb', target='gpu',
+                           gpu_indexing_params=p or None).compile()
+        tf = timed(lambda: fk(u=u, k=k, out=out))
+        tb = timed(lambda: bk(u=u, k=k, diffout=d, diffu=du, diffk=dk))
+        v = fk.last_variant[1] if len(fk.last_variant) > 1 else None
+        bv = bk.last_variant[1] if len(bk.last_variant) > 1 else None
+        print(f'varcoef {n}^3 {name:10s} fwd {tf:.4f} ms ({12 * cells / tf / 1e6 / 8000:.3f})  bwd {tb:.4f} ms '
+              f'({20 * cells / tb / 1e6 / 8000:.3f})  fwd CX={getattr(v, "CX", "-")} NR={getattr(v, "NR", "-")} '
+              f'WS={getattr(v, "WS", "-")} D={getattr(v, "D", "-")} | bwd CX={getattr(bv, "CX", "-")} NR={getattr(bv, "NR", "-")} '
+              f'WS={getattr(bv, "WS", "-")} D={getattr(bv, "D", "-")}', flush=True)
+
+
+if __name__ == '__main__':
+    main()
