@@ -262,6 +262,8 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
         elif k == 'VIEW2D':
             cfg[k] = str(v)
+        elif k == 'BABL' and ring_ws:
+            cfg[k] = int(v)                 # (timing probe of the march ring, as on the band: 3 = no plane loads)
     bc = _band_config(ir, ve, shape, over) if band else None
     if bc is not None:
         return bc

@@ -23,6 +23,14 @@ TILES = {
     'ws_cx2nr2': dict(WS=1, CX=2, NR=2, D=2), 'ws_cx1nr4': dict(WS=1, CX=1, NR=4, D=2),
     'ws_cx1nr2': dict(WS=1, CX=1, NR=2, D=2), 'ws_cx2nr1': dict(WS=1, CX=2, NR=1, D=2),
     'ws_cx4nr1': dict(WS=1, CX=4, NR=1, D=2), 'ws_cx2nr2d1': dict(WS=1, CX=2, NR=2, D=1),
+    'ws8_cx4nr1': dict(WS=1, NW=8, CX=4, NR=1, D=2), 'ws8_cx4nr2': dict(WS=1, NW=8, CX=4, NR=2, D=2),
+    'ws8_cx2nr2': dict(WS=1, NW=8, CX=2, NR=2, D=2), 'ws8_cx2nr1': dict(WS=1, NW=8, CX=2, NR=1, D=2),
+    'ws8_cx2wx2nr1': dict(WS=1, NW=8, WX=2, CX=2, NR=1, D=2), 'ws8_cx2nr4': dict(WS=1, NW=8, CX=2, NR=4, D=2),
+    'ws_cx4nr1d4': dict(WS=1, CX=4, NR=1, D=4), 'ws8_cx4nr1d3': dict(WS=1, NW=8, CX=4, NR=1, D=3),
+    'ws8_cx4nr1d4': dict(WS=1, NW=8, CX=4, NR=1, D=4), 'ws_cx2nr2d4': dict(WS=1, CX=2, NR=2, D=4),
+    'ws8_cx2nr2d3': dict(WS=1, NW=8, CX=2, NR=2, D=3),
+    # timing only (wrong results): the default ring with no plane loads — the compute waves' time alone
+    'abl_noload': dict(BABL=3), 'abl_noload_ws8': dict(WS=1, NW=8, CX=4, NR=1, D=2, BABL=3),
 }
 
 

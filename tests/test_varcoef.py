@@ -161,3 +161,29 @@ def test_varcoef_schedules_gpu(sched):
 def test_varcoef_full_size_gpu():
     """160³ fp32 on the default schedule, every cell against the oracle."""
     _run((160, 160, 160), torch.float32, 'cuda', seed=5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('params', [dict(WS=1, NW=8, CX=4, NR=1, D=2), dict(WS=1, NW=8, CX=2, NR=2, D=3),
+                                    dict(WS=1, CX=2, NR=2, D=1), dict(WS=1, CX=1, WX=4, NR=4, D=2),
+                                    dict(WS=0, CX=2, NR=2)], ids=str)
+def test_varcoef_ring_tilings_gpu(params):
+    """The plane ring's tilings (8 compute waves, ring depths, register-prefetch form) on a box of ragged tiles and
+    chunks, every cell against the oracle."""
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    op = _op()
+    shape = (19, 37, 200)
+    u, k, d = _inputs(shape, torch.float32, 'cuda', seed=7)
+    fk = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='vct_f', target='gpu',
+                       gpu_indexing_params=params).compile()
+    bk = StencilKernel(op.backward_assignments, boundary_handling='zeros', function_name='vct_b', target='gpu',
+                       gpu_indexing_params=params).compile()
+    out, du, dk = (torch.zeros_like(u) for _ in range(3))
+    fk(u=u, k=k, out=out)
+    bk(u=u, k=k, diffout=d, diffu=du, diffk=dk)
+    torch.cuda.synchronize()
+    assert fk.last_variant[1].WS == bool(params['WS']) and bk.last_variant[1].WS == bool(params['WS'])
+    ref, ab = oracle(op, *(x.double().cpu().numpy() for x in (u, k, d)))
+    check(out, ref['out'], ab['out'], False, f'{params} out')
+    check(du, ref['diffu'], ab['diffu'], False, f'{params} diffu')
+    check(dk, ref['diffk'], ab['diffk'], False, f'{params} diffk')
