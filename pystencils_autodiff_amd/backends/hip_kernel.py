@@ -74,7 +74,7 @@ RING_WS_TILES = ((4, 4), (4, 2), (2, 4), (2, 2), (1, 4), (1, 2), (1, 1))
 # keys are this layer's tile parameters; an unknown one is a typo and raises.
 TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
              'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE', 'BLDR', 'BLAUX', 'BPAD', 'BZF', 'BREG', 'BMBR', 'BNT', 'BPE', 'BSI',
-             'BPRIO', 'BABL', 'BLW', 'BTB', 'BSHIFT', 'BDEAD', 'BFM')
+             'BPRIO', 'BABL', 'BLW', 'BTB', 'BSHIFT', 'BDEAD', 'BFM', 'SFAST')
 
 
 def _band_config(ir, ve, shape, over):
@@ -262,6 +262,8 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
         elif k == 'VIEW2D':
             cfg[k] = str(v)
+        elif k == 'SFAST':
+            cfg[k] = int(v)
         elif k == 'BABL' and ring_ws:
             cfg[k] = int(v)                 # (timing probe of the march ring, as on the band: 3 = no plane loads)
     bc = _band_config(ir, ve, shape, over) if band else None
