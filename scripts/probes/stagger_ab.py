@@ -3,7 +3,8 @@ its five arrays start relative to each other: one allocation each (the caching a
 equal strides apart), and views into padded blocks with array i shifted by i × a stagger. Interleaved rounds in one
 process, HIP events, median of 20. Timing only (the default schedule's kernel, same code for every layout).
 
-python scripts/probes/stagger_ab.py [n=512] [rounds=3]"""
+python scripts/probes/stagger_ab.py [n=512] [rounds=3]
+python scripts/probes/stagger_ab.py 1024 3 diffusion7     (the headline's forward: u read, out written)"""
 import os
 import sys
 
@@ -13,7 +14,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'
 import pystencils_autodiff_amd as pa  # noqa: E402
 from pystencils_autodiff_amd import workloads as W  # noqa: E402
 
-STAGGERS = [0, 4096, 65536 + 256, 1 << 20, (1 << 20) + 4096 * 3]
+STAGGERS = [0, 4096, 65536 + 256, 1 << 20, (1 << 20) + 4096 * 3, 256, 2048]
 
 
 def timed(fn, reps=20):
@@ -31,10 +32,28 @@ def timed(fn, reps=20):
     return ts[len(ts) // 2]
 
 
-def arrays(shape, stagger, keep):
+HEADLINE_STAGGERS = [0, 1024, 2048, 4096, 8192, 12288, 16384, 32768, 65536, 131072, 262144, 524288, 1 << 20,
+                     (1 << 20) + 4096]
+
+
+def headline(shape, rounds):
+    op = pa.AutoDiffOp(W.diffusion_7pt(), boundary_handling='zeros')
+    fk = op.forward_ast_gpu.compile()
+    layouts = {}
+    for s in HEADLINE_STAGGERS:
+        keep = []
+        layouts[s] = (arrays(shape, s, keep, 2), keep)
+    for r in range(rounds):
+        line = []
+        for s, ((u, o), _) in layouts.items():
+            line.append(f'{s:>8d}: {timed(lambda: fk(u=u, out=o)):.4f}')
+        print(f'diffusion7 {shape[0]}^3 forward round {r} (stagger bytes: ms) ' + ' | '.join(line), flush=True)
+
+
+def arrays(shape, stagger, keep, count=5):
     n = shape[0] * shape[1] * shape[2]
     out = []
-    for i in range(5):
+    for i in range(count):
         pad = (i * stagger) // 4
         blk = torch.rand(n + pad + 64, device='cuda')
         keep.append(blk)
@@ -46,6 +65,8 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     shape = (n, n, n)
+    if len(sys.argv) > 3 and sys.argv[3] == 'diffusion7':
+        return headline(shape, rounds)
     op = pa.AutoDiffOp(W.varcoef_diffusion_7pt(), boundary_handling='zeros')
     fk, bk = op.forward_ast_gpu.compile(), op.backward_ast_gpu.compile()
     layouts = {}
