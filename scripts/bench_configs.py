@@ -363,6 +363,8 @@ def main():
         # variable-coefficient diffusion (two inputs; the adjoint reads three fields and writes two)
         ('varcoef7_f32_768^3', lambda: W.varcoef_diffusion_7pt(), (768, 768, 768), torch.float32, 'zeros', 2, 12, 20),
         ('varcoef7_f32_512^3', lambda: W.varcoef_diffusion_7pt(), (512, 512, 512), torch.float32, 'zeros', 2, 12, 20),
+        ('varcoef7_f16_768^3', lambda: W.varcoef_diffusion_7pt(dtype='float16'), (768, 768, 768), torch.float16, 'zeros',
+         2, 6, 10),
         ('veclaplace7_f32_384^3x3', lambda: W.vector_laplace_7pt(), (384, 384, 384, 3), torch.float32, 'zeros', 1,
          24, 24),
     ]

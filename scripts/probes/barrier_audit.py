@@ -25,7 +25,8 @@ def disassemble(workload, shape, tun, which):
     from pystencils_autodiff_amd.backends.hip_kernel import HipStencilKernel, default_march_config
     from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
     wl = {'stencil27': W.stencil_27pt, 'diffusion7': W.diffusion_7pt,
-          'diffusion7_f16': lambda: W.diffusion_7pt(dtype='float16'), 'varcoef': W.varcoef_diffusion_7pt}[workload]
+          'diffusion7_f16': lambda: W.diffusion_7pt(dtype='float16'), 'varcoef': W.varcoef_diffusion_7pt,
+          'varcoef_f16': lambda: W.varcoef_diffusion_7pt(dtype='float16')}[workload]
     op = AutoDiffOp(wl(), boundary_handling='zeros')
     asg = op.forward_assignments if which == 'forward' else op.backward_assignments
     k = StencilKernel(asg, boundary_handling='zeros', function_name='audit', target='gpu', gpu_indexing_params=tun)

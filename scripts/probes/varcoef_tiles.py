@@ -1,7 +1,7 @@
 """Tile sweep of the variable-coefficient diffusion (workloads.varcoef_diffusion_7pt) on the schedules a nonlinear
 multi-field stencil can take, forward and TF-MAD adjoint kernels timed alone with HIP events (median of 20 after
 warm-up), fraction of 8 TB/s from the algorithmic bytes (fwd 12, bwd 20 B/cell fp32). Timing only (parity:
-tests/test_varcoef.py).  python scripts/probes/varcoef_tiles.py [n=512] [tiles=all]"""
+tests/test_varcoef.py).  python scripts/probes/varcoef_tiles.py [n=512] [tiles=all] [f16]"""
 import os
 import sys
 
@@ -52,10 +52,12 @@ def timed(fn, reps=20):
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
     names = sys.argv[2].split(',') if len(sys.argv) > 2 else list(TILES)
-    op = pa.AutoDiffOp(W.varcoef_diffusion_7pt(), boundary_handling='zeros')
+    f16 = len(sys.argv) > 3 and sys.argv[3] == 'f16'
+    dt, es = (torch.float16, 2) if f16 else (torch.float32, 4)
+    op = pa.AutoDiffOp(W.varcoef_diffusion_7pt(dtype='float16' if f16 else 'float32'), boundary_handling='zeros')
     shape = (n, n, n)
-    u, k, d = (torch.rand(shape, device='cuda') for _ in range(3))
-    out, du, dk = (torch.empty(shape, device='cuda') for _ in range(3))
+    u, k, d = (torch.rand(shape, device='cuda').to(dt) for _ in range(3))
+    out, du, dk = (torch.empty(shape, device='cuda', dtype=dt) for _ in range(3))
     cells = n ** 3
     for name in names:
         p = TILES[name]
@@ -67,8 +69,8 @@ def main():
         tb = timed(lambda: bk(u=u, k=k, diffout=d, diffu=du, diffk=dk))
         v = fk.last_variant[1] if len(fk.last_variant) > 1 else None
         bv = bk.last_variant[1] if len(bk.last_variant) > 1 else None
-        print(f'varcoef {n}^3 {name:10s} fwd {tf:.4f} ms ({12 * cells / tf / 1e6 / 8000:.3f})  bwd {tb:.4f} ms '
-              f'({20 * cells / tb / 1e6 / 8000:.3f})  fwd CX={getattr(v, "CX", "-")} NR={getattr(v, "NR", "-")} '
+        print(f'varcoef {n}^3 {name:10s} fwd {tf:.4f} ms ({3 * es * cells / tf / 1e6 / 8000:.3f})  bwd {tb:.4f} ms '
+              f'({5 * es * cells / tb / 1e6 / 8000:.3f})  fwd CX={getattr(v, "CX", "-")} NR={getattr(v, "NR", "-")} '
               f'WS={getattr(v, "WS", "-")} D={getattr(v, "D", "-")} | bwd CX={getattr(bv, "CX", "-")} NR={getattr(bv, "NR", "-")} '
               f'WS={getattr(bv, "WS", "-")} D={getattr(bv, "D", "-")}', flush=True)
 

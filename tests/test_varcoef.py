@@ -17,6 +17,7 @@ import pystencils_autodiff_amd as pa
 from oracle import evaluate as OE
 from pystencils_autodiff_amd import ps
 from pystencils_autodiff_amd import workloads as W
+from tests.conftest import fp16_ulp
 
 torch = pytest.importorskip('torch')
 
@@ -69,9 +70,12 @@ def oracle(op, u, k, d):
     return ref, ab
 
 
-def check(got, ref, absterms, fp64, what):
+def check(got, ref, absterms, fp64, what, fp16=False):
+    """fp16 storage: the fp32 bound plus half an fp16 ulp of the stored result (conftest.assert_cells' form)."""
     got = got.detach().double().cpu().numpy() if hasattr(got, 'detach') else np.asarray(got, np.float64)
     bound = 1e-12 * (np.abs(ref) + absterms) if fp64 else 1e-6 * np.abs(ref) + 32 * 2.0 ** -24 * absterms
+    if fp16:
+        bound = bound + 0.5 * fp16_ulp(np.abs(ref) + bound)
     err = np.abs(got - ref)
     bad = err > bound
     assert not bad.any(), f'{what}: {int(bad.sum())} of {bad.size} cells outside the bound, worst err {err.max():.3e}'
@@ -96,17 +100,17 @@ def _apply(op, u, k, d, device):
 
 
 def _run(shape, dtype, device, seed=0):
-    fp64 = dtype == torch.float64
-    op = _op('float64' if fp64 else 'float32')
+    fp64, fp16 = dtype == torch.float64, dtype == torch.float16
+    op = _op({torch.float64: 'float64', torch.float16: 'float16'}.get(dtype, 'float32'))
     u, k, d = _inputs(shape, dtype, device, seed)
     out, gu, gk = _apply(op, u, k, d, device)
     ref, ab = oracle(op, *(x.double().cpu().numpy() for x in (u, k, d)))
-    check(out, ref['out'], ab['out'], fp64, 'out')
-    check(gu, ref['diffu'], ab['diffu'], fp64, 'diffu')
-    check(gk, ref['diffk'], ab['diffk'], fp64, 'diffk')
+    check(out, ref['out'], ab['out'], fp64, 'out', fp16)
+    check(gu, ref['diffu'], ab['diffu'], fp64, 'diffu', fp16)
+    check(gk, ref['diffk'], ab['diffk'], fp64, 'diffk', fp16)
     # the forward against an independent restatement
     ro = torch_varcoef(u.double().cpu(), k.double().cpu()).numpy()
-    check(out, ro, ab['out'], fp64, 'out vs torch')
+    check(out, ro, ab['out'], fp64, 'out vs torch', fp16)
 
 
 def test_varcoef_cpu_backend_vs_oracle():
@@ -133,7 +137,7 @@ def test_varcoef_tfmad_is_reverse_mode_for_uniform_k():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('shape', [(17, 33, 45), (9, 20, 128), (5, 7, 3), (40, 64, 256), (33, 50, 130)])
-@pytest.mark.parametrize('dtype', [torch.float32, torch.float64], ids=['f32', 'f64'])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64, torch.float16], ids=['f32', 'f64', 'f16'])
 def test_varcoef_gpu_vs_oracle(shape, dtype):
     _run(shape, dtype, 'cuda')
 
