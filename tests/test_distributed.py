@@ -624,3 +624,65 @@ def test_zslab_native_node_loopback(builder_name, shape, monkeypatch):
         assert_close_rel(res[0][1].cpu().numpy(), periodic(d, S.flip(taps)), tol, 'diffu')
     finally:
         z.close()
+
+
+def _worker_varcoef(rank, world, port, shape, use_cuda, result_dir):
+    """Two input fields and a nonlinear stencil on z-slabs: the halos of u and k (forward) and of u, k and diffout
+    (adjoint) exchanged; this rank's slabs of out / diffu / diffk saved."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import pystencils_autodiff_amd as pa
+    from pystencils_autodiff_amd import workloads as W
+    from pystencils_autodiff_amd.zslab import ZSlabOp, slab_bounds
+    dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank, world_size=world)
+    try:
+        op = pa.AutoDiffOp(W.varcoef_diffusion_7pt(), boundary_handling='zeros')
+        u, k, d = _varcoef_inputs(shape)
+        lo, hi = slab_bounds(shape[0], world, rank)
+        dev = 'cuda' if use_cuda else 'cpu'
+        ul, kl, dl = (torch.from_numpy(a[lo:hi].copy()).to(dev) for a in (u, k, d))
+        out, du, dk = (torch.zeros_like(ul) for _ in range(3))
+        z = ZSlabOp(op, use_cuda=use_cuda)
+        z.fwd(u=ul, k=kl, out=out)
+        z.bwd(u=ul, k=kl, diffout=dl, diffu=du, diffk=dk)
+        if use_cuda:
+            torch.cuda.synchronize()
+        for n, t in (('out', out), ('du', du), ('dk', dk)):
+            np.save(os.path.join(result_dir, f'{n}_{rank}.npy'), t.cpu().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def _varcoef_inputs(shape):
+    rng = np.random.default_rng(4)
+    return (rng.uniform(-1, 1, shape).astype(np.float32), rng.uniform(0.1, 1.1, shape).astype(np.float32),
+            rng.uniform(-1, 1, shape).astype(np.float32))
+
+
+def _run_varcoef(world, shape, use_cuda, tmp_path):
+    from oracle import evaluate as OE
+    from tests.conftest import assert_close_rel
+    import pystencils_autodiff_amd as pa
+    from pystencils_autodiff_amd import workloads as W
+    port = _free_port()
+    mp.spawn(_worker_varcoef, args=(world, port, shape, use_cuda, str(tmp_path)), nprocs=world, join=True)
+    got = {n: np.concatenate([np.load(tmp_path / f'{n}_{r}.npy') for r in range(world)]) for n in ('out', 'du', 'dk')}
+    op = pa.AutoDiffOp(W.varcoef_diffusion_7pt(), boundary_handling='zeros')
+    u, k, d = (a.astype(np.float64) for a in _varcoef_inputs(shape))
+    ref = {**OE.evaluate(op.forward_assignments, {'u': u, 'k': k}),
+           **OE.evaluate(op.backward_assignments, {'u': u, 'k': k, 'diffout': d})}
+    assert_close_rel(got['out'], ref['out'], 1e-6, 'out')
+    assert_close_rel(got['du'], ref['diffu'], 1e-6, 'diffu')
+    assert_close_rel(got['dk'], ref['diffk'], 1e-6, 'diffk')
+
+
+@pytest.mark.parametrize('world,shape', [(2, (10, 9, 12)), (3, (13, 6, 8))])
+def test_zslab_two_input_nonlinear_gloo_cpu(world, shape, tmp_path):
+    _run_varcoef(world, shape, False, tmp_path)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('world,shape', [(2, (24, 40, 64)), (3, (19, 33, 72))])
+def test_zslab_two_input_nonlinear_gloo_gpu(world, shape, tmp_path):
+    """The plane ring (LDS-DMA form at these widths) with halo planes of two / three fields across ranks."""
+    _run_varcoef(world, shape, True, tmp_path)

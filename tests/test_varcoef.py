@@ -191,3 +191,44 @@ def test_varcoef_ring_tilings_gpu(params):
     check(out, ref['out'], ab['out'], False, f'{params} out')
     check(du, ref['diffu'], ab['diffu'], False, f'{params} diffu')
     check(dk, ref['diffk'], ab['diffk'], False, f'{params} diffk')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('params', [None, dict(WS=0)], ids=['ring_dma', 'ring_registers'])
+def test_varcoef_slab_halos_and_two_range_launches_gpu(params):
+    """The z-slab launch pattern on the plane ring, forward and adjoint: halo planes of every stencil field read in
+    place, interior planes first, both faces in one two-range launch == one full-domain launch, bitwise."""
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    op = _op()
+    kf = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='vch_f', target='gpu',
+                       gpu_indexing_params=params).compile()
+    kb = StencilKernel(op.backward_assignments, boundary_handling='zeros', function_name='vch_b', target='gpu',
+                       gpu_indexing_params=params).compile()
+    Z = 30
+    u, k, d = _inputs((Z, 21, 136), torch.float32, 'cuda', seed=11)
+    full = torch.empty_like(u)
+    kf(u=u, k=k, out=full)
+    fdu, fdk = torch.empty_like(u), torch.empty_like(u)
+    kb(u=u, k=k, diffout=d, diffu=fdu, diffk=fdk)
+    assert kf.last_variant[1].WS == (params is None) and kb.last_variant[1].WS == (params is None)
+    outs, dus, dks = [], [], []
+    for a, b in [(0, 11), (11, 19), (19, Z)]:
+        sl = {n: t[a:b].contiguous() for n, t in (('u', u), ('k', k), ('diffout', d))}
+        halo = {n: (t[a - 1:a].contiguous() if a > 0 else None, t[b:b + 1].contiguous() if b < Z else None)
+                for n, t in (('u', u), ('k', k), ('diffout', d))}
+        out, du, dk = (torch.full_like(sl['u'], float('nan')) for _ in range(3))
+        kf(u=sl['u'], k=sl['k'], out=out, z_range=(1, b - a - 1))
+        kf(u=sl['u'], k=sl['k'], out=out, halos={'u': halo['u'], 'k': halo['k']},
+           z_range=((0, 1), (b - a - 1, b - a)))
+        kb(**sl, diffu=du, diffk=dk, z_range=(1, b - a - 1))
+        kb(**sl, diffu=du, diffk=dk, halos=halo, z_range=((0, 1), (b - a - 1, b - a)))
+        outs.append(out)
+        dus.append(du)
+        dks.append(dk)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(outs), full)
+    assert torch.equal(torch.cat(dus), fdu)
+    assert torch.equal(torch.cat(dks), fdk)
+    ref, ab = oracle(op, *(x.double().cpu().numpy() for x in (u, k, d)))
+    check(full, ref['out'], ab['out'], False, 'out')
+    check(fdu, ref['diffu'], ab['diffu'], False, 'diffu')
