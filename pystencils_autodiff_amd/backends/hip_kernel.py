@@ -308,6 +308,18 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             cfg['NR'] //= 2
         else:
             cfg['CX'] //= 2
+    if cfg.get('WS') and not cfg['ZSUM'] and lds(cfg) > 160 * 1024:
+        # a plane ring that does not fit even at the smallest tile (many fields of wide radius): the register form
+        cfg['WS'] = False
+        if cfg.get('NW', 4) == 8:                             # (eight compute waves only on the LDS-DMA ring)
+            cfg['NW'], cfg['WX'] = 4, min(cfg['WX'], 4)
+        while lds(cfg) > budget and (cfg['NR'] > 1 or cfg['CX'] > 1):
+            if cfg['NR'] >= cfg['CX'] and cfg['NR'] > 1:
+                cfg['NR'] //= 2
+            else:
+                cfg['CX'] //= 2
+    if ir.ndim == 3 and lds(cfg) > 160 * 1024:
+        raise ValueError(f'no tile of this kernel fits the 160 KB LDS ({lds(cfg)} B at {cfg})')
     if star_ws and cfg.get('WS') and shape is not None and 'MAP' not in over:
         ntx = -(-int(shape[-1]) // (64 * cfg['CX'] * cfg['WX']))
         if ntx & (ntx - 1):

@@ -232,3 +232,43 @@ def test_varcoef_slab_halos_and_two_range_launches_gpu(params):
     ref, ab = oracle(op, *(x.double().cpu().numpy() for x in (u, k, d)))
     check(full, ref['out'], ab['out'], False, 'out')
     check(fdu, ref['diffu'], ab['diffu'], False, 'diffu')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('params', [None, dict(WS=0), dict(WS=1, NW=8, CX=2, NR=2, D=2)], ids=['dma', 'registers', 'dma8'])
+@pytest.mark.parametrize('dtype', ['float32', 'float64'])
+def test_plane_ring_radius2_full_ring_fields_gpu(params, dtype):
+    """Nonlinear stencil of radius 2 whose fields are read off-centre BEHIND the centre plane (full rings of
+    2·RZ + 1 + D slots, no register queue), two outputs, on unaligned tiles — forward and TF-MAD adjoint against the
+    oracle evaluating the op's own assignments."""
+    import sympy as sp
+    from pystencils_autodiff_amd import ps
+    from pystencils_autodiff_amd.backends.hip_emitter import march_geometry
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    a, b, o1, o2 = ps.fields(f'a, b, o1, o2: {dtype}[3d]')
+    ac = ps.AssignmentCollection({
+        o1.center: a[0, 0, 2] * b[0, 0, -2] + sp.sin(a[-2, 1, 0]) * b.center + 0.5 * a[1, -1, -1] * a[-1, 2, 0],
+        o2.center: b[2, 0, 1] * b[-1, -2, 0] - a[0, 1, 0] * b[-2, 0, 0]})
+    op = pa.AutoDiffOp(ac, boundary_handling='zeros')
+    shape = (23, 35, 140)
+    g = torch.Generator().manual_seed(9)
+    tdt = torch.float32 if dtype == 'float32' else torch.float64
+    A, Bf, D1, D2 = (torch.rand(shape, generator=g, dtype=torch.float64).mul(2).sub(1).to(tdt).cuda() for _ in range(4))
+    fk = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='r2_f', target='gpu',
+                       gpu_indexing_params=params).compile()
+    bk = StencilKernel(op.backward_assignments, boundary_handling='zeros', function_name='r2_b', target='gpu',
+                       gpu_indexing_params=params).compile()
+    O1, O2, DA, DB = (torch.zeros_like(A) for _ in range(4))
+    fk(a=A, b=Bf, o1=O1, o2=O2)
+    bk(a=A, b=Bf, diffo1=D1, diffo2=D2, diffa=DA, diffb=DB)
+    torch.cuda.synchronize()
+    cfg = fk.last_variant[1]
+    assert fk.last_variant[0] == 'march' and not cfg.ZSUM and cfg.WS == (params is None or bool(params['WS']))
+    assert march_geometry(fk.ir, cfg)['RZ'] == 2 and not march_geometry(fk.ir, cfg)['lite']
+    arr = {n: t.double().cpu().numpy() for n, t in (('a', A), ('b', Bf))}
+    ref = {**OE.evaluate(op.forward_assignments, arr, boundary_handling='zeros'),
+           **OE.evaluate(op.backward_assignments, {**arr, 'diffo1': D1.double().cpu().numpy(),
+                                                   'diffo2': D2.double().cpu().numpy()}, boundary_handling='zeros')}
+    tol = 1e-5 if dtype == 'float32' else 1e-12
+    for name, got in (('o1', O1), ('o2', O2), ('diffa', DA), ('diffb', DB)):
+        np.testing.assert_allclose(got.double().cpu().numpy(), ref[name], rtol=tol, atol=tol * 4, err_msg=name)
