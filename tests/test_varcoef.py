@@ -272,3 +272,45 @@ def test_plane_ring_radius2_full_ring_fields_gpu(params, dtype):
     tol = 1e-5 if dtype == 'float32' else 1e-12
     for name, got in (('o1', O1), ('o2', O2), ('diffa', DA), ('diffb', DB)):
         np.testing.assert_allclose(got.double().cpu().numpy(), ref[name], rtol=tol, atol=tol * 4, err_msg=name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('mode', ['none', 'time_constant'])
+def test_varcoef_ring_none_mode_and_time_constant_gpu(mode):
+    """The plane ring under ``boundary_handling=None`` (interior cells only, the border untouched) and with a
+    time-constant conductivity (``diffk`` accumulated: read-modify-write of the adjoint, ``_autodiff.py:110-113``),
+    every cell against the oracle; NaN-poisoned outputs show any write outside the written box."""
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    ac = W.varcoef_diffusion_7pt()
+    bh = None if mode == 'none' else 'zeros'
+    kfield = next(f for f in ac.free_symbols if hasattr(f, 'field') and f.field.name == 'k').field
+    op = pa.AutoDiffOp(ac, boundary_handling=bh, time_constant_fields=[kfield] if mode == 'time_constant' else None)
+    shape = (19, 37, 136)
+    u, k, d = _inputs(shape, torch.float32, 'cuda', seed=13)
+    fk = StencilKernel(op.forward_assignments, boundary_handling=bh, function_name='vn_f', target='gpu').compile()
+    bk = StencilKernel(op.backward_assignments, boundary_handling=bh, function_name='vn_b', target='gpu').compile()
+    fill = float('nan') if mode == 'none' else 0.0
+    out = torch.full_like(u, fill)
+    du = torch.full_like(u, fill)
+    dk = torch.full_like(u, fill) if mode == 'none' else torch.rand(shape, device='cuda')
+    dk0 = dk.clone()
+    fk(u=u, k=k, out=out)
+    bk(u=u, k=k, diffout=d, diffu=du, diffk=dk)
+    torch.cuda.synchronize()
+    assert fk.last_variant[1].WS and not fk.last_variant[1].ZSUM
+    arr = {n: t.double().cpu().numpy() for n, t in (('u', u), ('k', k))}
+    ref = OE.evaluate(op.forward_assignments, arr, boundary_handling=bh)
+    refb = OE.evaluate(op.backward_assignments, {**arr, 'diffout': d.double().cpu().numpy()}, boundary_handling=bh,
+                       outputs={'diffk': dk0.double().cpu().numpy()} if mode == 'time_constant' else None)
+    if mode == 'none':
+        inner = (slice(1, -1),) * 3
+        for got, name, r in ((out, 'out', ref), (du, 'diffu', refb), (dk, 'diffk', refb)):
+            g_ = got.double().cpu().numpy()
+            np.testing.assert_allclose(g_[inner], r[name][inner], rtol=1e-5, atol=1e-5, err_msg=name)
+            border = np.ones(shape, bool)
+            border[inner] = False
+            assert np.isnan(g_[border]).all(), f'{name}: a border cell was written'
+    else:
+        np.testing.assert_allclose(out.double().cpu().numpy(), ref['out'], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(du.double().cpu().numpy(), refb['diffu'], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(dk.double().cpu().numpy(), refb['diffk'], rtol=1e-5, atol=1e-5)
