@@ -1,0 +1,51 @@
+"""A nonlinear stencil on a vector field (index dimension, components fastest): first-order upwind-free advection
+``out(c) = u(c) − α Σ_d u(d)·(u[+e_d](c) − u[−e_d](c))/2`` on u(3) fp32 — which schedule it takes and its forward /
+adjoint rate through the op (HIP events, median of 20). Timing only.  python scripts/probes/vector_nonlinear.py [n=256]"""
+import os
+import sys
+
+import sympy as sp
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', '..'))
+import pystencils_autodiff_amd as pa  # noqa: E402
+from pystencils_autodiff_amd import ps  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    u, out = ps.fields('u(3), out(3): float32[3d]')
+    e = [(1, 0, 0), (0, 1, 0), (0, 0, 1)]
+    m = [(-1, 0, 0), (0, -1, 0), (0, 0, -1)]
+    ac = ps.AssignmentCollection({out.center(c): u.center(c) - 0.05 * sp.Add(
+        *[u.center(d) * (u[e[d]](c) - u[m[d]](c)) / 2 for d in range(3)]) for c in range(3)})
+    op = pa.AutoDiffOp(ac, boundary_handling='zeros')
+    fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    x = torch.rand((n, n, n, 3), device='cuda').requires_grad_(True)
+    g = torch.rand((n, n, n, 3), device='cuda')
+    for _ in range(5):
+        (o,) = fn.apply(x)
+        o.backward(g)
+        x.grad = None
+    fw, bw = [], []
+    for _ in range(20):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record()
+        (o,) = fn.apply(x)
+        ev[1].record()
+        o.backward(g)
+        ev[2].record()
+        torch.cuda.synchronize()
+        x.grad = None
+        fw.append(ev[0].elapsed_time(ev[1]))
+        bw.append(ev[1].elapsed_time(ev[2]))
+    fw.sort()
+    bw.sort()
+    b = n ** 3 * 3 * 4
+    print(f'vector advection {n}^3x3 fp32: fwd {fw[10]:.4f} ms ({2 * b / fw[10] / 1e6 / 8000:.3f} of 8 TB/s at 24 B/cell), '
+          f'bwd {bw[10]:.4f} ms ({3 * b / bw[10] / 1e6 / 8000:.3f} at 36 B/cell); schedules '
+          f'{op.forward_ast_gpu.compile().last_variant[0]} / {op.backward_ast_gpu.compile().last_variant[0]}', flush=True)
+
+
+if __name__ == '__main__':
+    main()
