@@ -68,12 +68,12 @@ def band_padded(X, es, pad):
     return bool(pad) and (X * es) % 16 == 0
 
 
-def band_geometry(X, TY, R, D, es=2, pad=0, reg=0, lw=1):
+def band_geometry(X, TY, R, D, es=2, pad=0, reg=0):
     """Launch / LDS geometry of a band of ``TY`` rows (``R`` per lane) on rows of ``X`` elements of ``es`` bytes.
     Rows whose pitch is not a multiple of 16 bytes (``X % VE``) take ``ceil(X / VE)`` chunks, the last one partial.
     ``pad``: every image row is preceded by one zero 16-byte piece and the slot ends with one (x neighbours of a row's
     end chunks read as zeros straight from LDS). ``reg``: rows of a partial last chunk on a padded image filled through
-    registers (``BREG``). ``lw``: loader waves sharing each plane's pieces (the piece count rounded up to a multiple)."""
+    registers (``BREG``)."""
     VE = 16 // es
     CPR = -(-X // VE)
     reg = bool(reg) and X % VE != 0
@@ -89,12 +89,10 @@ def band_geometry(X, TY, R, D, es=2, pad=0, reg=0, lw=1):
     NCT = -(-ntask // 64) * 64
     NPIECE = (TY + 2) * (XP // VE) + (1 if padded else 0)
     NI = -(-NPIECE // 64)
-    lw = 1 if reg else max(1, int(lw))
-    NI = -(-NI // lw) * lw
     SLOT = NI * 64 * VE
     NS = 3 if reg else D + 1
-    return dict(VE=VE, CPR=CPR, XP=XP, G=G, ntask=ntask, NCT=NCT, NT=NCT + 64 * lw, NPIECE=NPIECE, NI=NI, SLOT=SLOT,
-                NS=NS, lds_bytes=(NS * SLOT + 64) * es, LW=lw, NIL=NI // lw)
+    return dict(VE=VE, CPR=CPR, XP=XP, G=G, ntask=ntask, NCT=NCT, NT=NCT + 64, NPIECE=NPIECE, NI=NI, SLOT=SLOT,
+                NS=NS, lds_bytes=(NS * SLOT + 64) * es)
 
 
 def _fits(X, TY, R, D, es=2, pad=0, reg=0, idle=False):
@@ -151,52 +149,6 @@ def band_choice(X, nstore=1, es=2, pad=0, reg=0, idle=False, star=False, wide16=
     return None
 
 
-def band_dpp_edges_ok(CPR):
-    """Edge dwords by DPP ``row_shr/row_shl:1`` (``BPE=3``) need every row-group boundary (and the last task) on a
-    16-lane row boundary of the wave: rows of a multiple of 16 chunks."""
-    return CPR % 16 == 0
-
-
-def band_edge_table(g, R, es):
-    """Per compute task (``ctid``): the element offset from the lane's chunk of the one LDS dword it reads per image
-    row under ``BPE=3``. Lanes 0 / 15 of each 16-lane row (DPP ``row_shr:1`` / ``row_shl:1`` has no source for them)
-    read their true left / right dword (a zero pad at a row end); the other lanes read a dword chosen so that each
-    32-lane half's addresses spread over the 32 banks of ``ds_read_b32`` ((a/4) mod 32, MI355X_MICROARCH.md §LDS).
-    Banks are computed relative to the wave's slot row base, which every lane shares (row and slot offsets are
-    uniform), so the table holds for every image row and slot. Returns (offsets, worst bank multiplicity)."""
-    VE, CPR, XP, NCT, ntask = g['VE'], g['CPR'], g['XP'], g['NCT'], g['ntask']
-    dw = 4 // es                                    # elements per dword
-    c0 = VE                                         # padded image: a row's first element sits after its zero piece
-    offs, worst = [0] * NCT, 1
-    for w in range(NCT // 64):
-        for h in range(2):
-            lanes = range(64 * w + 32 * h, 64 * w + 32 * h + 32)
-            pos = {}
-            for t in lanes:
-                tt = min(t, ntask - 1)
-                grp, col = divmod(tt, CPR)
-                pos[t] = (grp * R * XP + c0 + col * VE) // dw        # the chunk's first dword
-            used = {}
-            for t in lanes:
-                L = t % 16
-                if L == 0:
-                    offs[t] = -dw
-                elif L == 15:
-                    offs[t] = VE
-                else:
-                    continue
-                b = (pos[t] + offs[t] // dw) % 32
-                used[b] = used.get(b, 0) + 1
-            for t in lanes:
-                if t % 16 in (0, 15):
-                    continue
-                b = min(range(32), key=lambda k: (used.get(k, 0), k))
-                used[b] = used.get(b, 0) + 1
-                offs[t] = ((b - pos[t]) % 32) * dw
-            worst = max(worst, max(used.values()))
-    return offs, worst
-
-
 def emit_band(ir, name, cfg):
     """HIP source of the band kernel (signature identical to the march / zsum kernels: fields, 2 halo pointers
     per stencil field, Z Y X zlo zhi ylo yhi xlo xhi zc zstep ntx nty, scalars)."""
@@ -209,12 +161,10 @@ def emit_band(ir, name, cfg):
     TY, R, D = cfg.BTY, cfg.BAND, cfg.D
     breg = bool(cfg.BREG) and X % (16 // es) != 0     # partial rows on a padded image filled through registers
     padded = breg or band_padded(X, es, cfg.BPAD)
-    g = band_geometry(X, TY, R, D, es, padded, breg, cfg.BLW)
+    g = band_geometry(X, TY, R, D, es, padded, breg)
     VE, CPR, G, NCT, NT, NPIECE, NI, SLOT, NS = (g[k] for k in ('VE', 'CPR', 'G', 'NCT', 'NT', 'NPIECE', 'NI', 'SLOT',
                                                                  'NS'))
-    LW, NIL = g['LW'], g['NIL']            # loader waves, pieces per plane each
-    assert D * NIL <= 63 and NT <= 1024, (X, TY, R, D, LW)
-    assert LW == 1 or not cfg.BLDR, 'the rotating loader role takes one loader wave'
+    assert D * NI <= 63 and NT <= 1024, (X, TY, R, D)
     assert not fixed or int(fixed[0].spatial_shape[-1]) == X, 'band kernel compiled for another row length'
     S = ir.stencil_fields[0]
     half = es == 2
@@ -227,9 +177,6 @@ def emit_band(ir, name, cfg):
     bo = not breg and (X * es) % 4 != 0             # rows on half dwords (fp16, X odd): realigned in registers
     assert not partial or cfg.BMASK, 'rows of a partial last chunk need the masked stores'
     czf = bu and not cfg.BZF                        # BZF=0: the first element past a row zeroed in registers
-    # (the loader's zero fill of unaligned rows needs every piece of the plane landed: one loader wave there)
-    assert LW == 1 or not (bu or bo), 'several loader waves need rows of a multiple of 16 bytes'
-    dpp_edges = padded and not breg and cfg.BPE == 3 and band_dpp_edges_ok(CPR)
     pr = KernelExprPrinter('float', dict(ir.symbol_names))
     W = []
     for pl in plans:
@@ -261,13 +208,7 @@ def emit_band(ir, name, cfg):
     L.append(f'// band schedule: {TY}-row bands of full {X}-element rows, {R} rows x {VE} cells per lane, {NCT // 64} '
              f'compute waves + LDS-DMA loader wave, {NS}-slot {et} plane ring ({D} planes in flight), z partial sums '
              f'in 3 rotating register sets, LDS {g["lds_bytes"]} B')
-    if dpp_edges:
-        etab, eworst = band_edge_table(g, R, es)
-        L.append(f'// x-edge dwords: DPP row_shr/row_shl:1, one ds_read_b32 per row for the 16-lane rows\' end lanes '
-                 f'(worst bank multiplicity {eworst})')
-        L.append(f'__constant__ short {name}_eoff[{NCT}] = {{{", ".join(str(v) for v in etab)}}};')
-    wpe = f' __attribute__((amdgpu_waves_per_eu({int(cfg.BWPE)}, {int(cfg.BWPE)})))' if cfg.BWPE else ''
-    L.append(f'extern "C" __global__ void __launch_bounds__({NT}){wpe} {name}({", ".join(params)})\n{{')
+    L.append(f'extern "C" __global__ void __launch_bounds__({NT}) {name}({", ".join(params)})\n{{')
     L.append(f'  __shared__ __attribute__((aligned(1024))) {et} lds[{NS * SLOT + 64}];')
     L.append('  const int tid = threadIdx.x, lane = tid & 63;')
     L.append('  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);')
@@ -286,28 +227,16 @@ def emit_band(ir, name, cfg):
     L.append(f'  const i64 YX = (i64)Y * {X};')
     L.append('  const int nplanes = ze - zb + 2;')
     # ---- loader wave
-    if cfg.BLDR:
-        # the loader role rotates with the workgroup index: its wave lands on a different SIMD from workgroup to
-        # workgroup even if every workgroup's waves start on the same SIMD
-        L.append(f'  const int ldw = blockIdx.x % {NCT // 64 + 1};')
-    else:
-        L.append(f'  const int ldw = {NCT // 64};')
-    if LW > 1:
-        # several loader waves: wave ldw + l streams pieces [l·NIL, (l+1)·NIL) of every plane, counts its own vmcnt
-        L.append(f'  if (wave >= ldw) {{')
-        L.append(f'    const int lw0 = (wave - ldw) * {NIL};')
-    else:
-        L.append('  if (wave == ldw) {')
-    if cfg.BPRIO:
-        L.append(f'    __builtin_amdgcn_s_setprio({int(cfg.BPRIO)});')
+    L.append(f'  const int ldw = {NCT // 64};')
+    L.append('  if (wave == ldw) {')
     if not breg:
-        L.append(f'    int vo[{NIL}];')
+        L.append(f'    int vo[{NI}];')
         if bo:
-            L.append(f'    int vo1[{NIL}];')
+            L.append(f'    int vo1[{NI}];')
             L.append('    auto hpar = [&](const void* b) { return (int)(((unsigned long long)b >> 1) & 1); };   // 0 for nullptr')
         L.append('    #pragma unroll')
-        L.append(f'    for (int i = 0; i < {NIL}; ++i) {{')
-        L.append('      const int k = ' + ('(lw0 + i)' if LW > 1 else 'i') + ' * 64 + lane;')
+        L.append(f'    for (int i = 0; i < {NI}; ++i) {{')
+        L.append('      const int k = i * 64 + lane;')
         if padded:
             # image row rr = one zero piece (out of range: the DMA writes zeros) + the row's pieces; one zero piece ends
             # the slot (the right neighbour of the last row's end)
@@ -341,18 +270,14 @@ def emit_band(ir, name, cfg):
         else:
             L.append(f'      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pb ? pb : '
                      f'f_{S.name}), (short)0, pb ? (int)(YX * {es}) : 0, 0x00020000);')
-        L.append(f'      {et}* dst = lds + slot * {SLOT}' + (f' + lw0 * {64 * VE};' if LW > 1 else ';'))
+        L.append(f'      {et}* dst = lds + slot * {SLOT};')
         if cfg.BABL == 3:
             L.append('      if (Z < 0)   // ablation probe: no plane loads')
         L.append('      #pragma unroll')
-        L.append(f'      for (int i = 0; i < {NIL}; ++i)')
+        L.append(f'      for (int i = 0; i < {NI}; ++i)')
         L.append(f'        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + i * '
-                 f'{64 * VE}), 16, {"pp ? vo1[i] : vo[i]" if bo else "vo[i]"}, 0, 0, {int(cfg.BLAUX)});')
+                 f'{64 * VE}), 16, {"pp ? vo1[i] : vo[i]" if bo else "vo[i]"}, 0, 0, 0);')
         L.append('    };')
-        if cfg.BSTAG:
-            # probe: the co-resident workgroups of a CU's first round start a fraction of a plane apart
-            L.append(f'    {{ const int st = (blockIdx.x >> 8) % 3; for (int i = 0; i < st; ++i) '
-                     f'__builtin_amdgcn_s_sleep({int(cfg.BSTAG)}); }}')
         L.append(f'    for (int i = 0; i < {D}; ++i)')
         L.append('      if (i < nplanes) issue(zb - 1 + i, i);')
         L.append('    for (int j = 0; j < nplanes; ++j) {')
@@ -360,7 +285,7 @@ def emit_band(ir, name, cfg):
         L.append(f'      const int after = min({D - 1}, nplanes - 1 - j);')
         L.append('      switch (after) {')
         for a in range(D):
-            L.append(f'        case {a}: asm volatile("s_waitcnt vmcnt({a * NIL})" ::: "memory"); break;')
+            L.append(f'        case {a}: asm volatile("s_waitcnt vmcnt({a * NI})" ::: "memory"); break;')
         L.append('      }')
         if bo and not czf:
             # plane j has landed: zeros over the image columns past each row's last element (X + the row's parity .. XP)
@@ -423,9 +348,9 @@ def emit_band(ir, name, cfg):
                  '      #pragma unroll',
                  f'      for (int i = 0; i < {NI}; ++i) {{',
                  f'        const int o = ((okm >> i) & 1u) ? ((a{sname} + go[i]) & ~3) : 0x7ffffff0;',
-                 f'        r{sname}[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, {int(cfg.BLAUX)});']
+                 f'        r{sname}[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);']
             if half:
-                B.append(f'        e{sname}[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 16, 0, {int(cfg.BLAUX)});')
+                B.append(f'        e{sname}[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 16, 0, 0);')
             B += ['      }', '    }']
             return B
 
@@ -480,8 +405,7 @@ def emit_band(ir, name, cfg):
     # ---- compute lanes
     if bo:
         L.append('  auto hpar = [&](const void* b) { return (int)(((unsigned long long)b >> 1) & 1); };   // 0 for nullptr')
-    L.append('  const int ctid = (wave - (wave > ldw ? 1 : 0)) * 64 + lane;   // compute task' if LW == 1 else
-             '  const int ctid = wave * 64 + lane;                          // compute task (loaders: the last waves)')
+    L.append('  const int ctid = (wave - (wave > ldw ? 1 : 0)) * 64 + lane;   // compute task')
     L.append(f'  const bool active = ctid < {g["ntask"]};')
     L.append(f'  const int t = active ? ctid : {g["ntask"] - 1};')
     L.append(f'  const int grp = t / {CPR}, col = t - grp * {CPR};')
@@ -509,9 +433,7 @@ def emit_band(ir, name, cfg):
     L.append("  // column 0 (x boundary, masked) reads its own first dword instead of the one before the slot.")
     dw = 4 // es                                          # elements per dword
     # dword targets relative to the wave's block (64 chunks of 4 dwords): -1, 0 .. 30 | 33 .. 63, 256
-    if dpp_edges:
-        L.append(f'  const int eoff = {name}_eoff[ctid < {NCT} ? ctid : 0];')
-    elif padded:
+    if padded:
         pass                                              # x neighbours read from the image (zero pads at row ends)
     elif cfg.BEDGE:
         L.append(f'  const int eoff = {dw} * (lane == 0 ? (col == 0 ? 0 : -1) : (lane == 63 ? 256 : (lane < 32 ? lane - 1 '
@@ -551,30 +473,20 @@ def emit_band(ir, name, cfg):
                   f'{ind}    const f32x2 P3 = {{(float)w1[1], (float)w3[1]}}, P4 = {{(float)w2[0], (float)w4[0]}}, '
                   'P5 = {(float)w2[1], (float)rr};']
             return B
-        if dpp_edges:
-            # the dwords left and right of the lane's chunk from the neighbour lanes (DPP within 16-lane rows); the rows'
-            # end lanes take the one LDS dword they read (their true edge, a zero pad at a row end), the other lanes'
-            # reads are spread over the banks (band_edge_table)
-            vt = 'f16x8' if half else 'f32x4'
-            B += [f'{ind}    const {vt} v = *(const {vt}*)rp;',
-                  f'{ind}    const unsigned e = *(const unsigned*)(rp + eoff);',
-                  f'{ind}    const u32x4 d = __builtin_bit_cast(u32x4, v);',
-                  f'{ind}    const unsigned el = __builtin_amdgcn_update_dpp(e, d.w, 0x111, 0xf, 0xf, false);   // row_shr:1',
-                  f'{ind}    const unsigned er = __builtin_amdgcn_update_dpp(e, d.x, 0x101, 0xf, 0xf, false);   // row_shl:1']
-        elif padded:
+        if padded:
             # the dwords left and right of the lane's chunk straight from the image (a row's end chunks meet the zero
             # pads): no DPP, no boundary selects (one ds_read2_b32 per row)
             B += [f'{ind}    const unsigned el = *(const unsigned*)(rp - {dw}), er = *(const unsigned*)(rp + {VE});']
         if padded:
             if half:
-                B += [f'{ind}    const f16x8 v = *(const f16x8*)rp;'] * (not dpp_edges) + [
+                B += [f'{ind}    const f16x8 v = *(const f16x8*)rp;',
                       f'{ind}    const _Float16 l = __builtin_bit_cast(f16x2, el)[1], rr = __builtin_bit_cast(f16x2, er)[0];',
                       f'{ind}    const f32x2 P0 = {{(float)l, (float)v[3]}}, P1 = {{(float)v[0], (float)v[4]}}, '
                       'P2 = {(float)v[1], (float)v[5]};',
                       f'{ind}    const f32x2 P3 = {{(float)v[2], (float)v[6]}}, P4 = {{(float)v[3], (float)v[7]}}, '
                       'P5 = {(float)v[4], (float)rr};']
             else:
-                B += [f'{ind}    const f32x4 v = *(const f32x4*)rp;'] * (not dpp_edges) + [
+                B += [f'{ind}    const f32x4 v = *(const f32x4*)rp;',
                       f'{ind}    const float H0 = __builtin_bit_cast(float, el), H5 = __builtin_bit_cast(float, er);',
                       f'{ind}    const float H1 = v.x, H2 = v.y, H3 = v.z, H4 = v.w;']
             return B
@@ -645,16 +557,14 @@ def emit_band(ir, name, cfg):
         for o in (range(R) if rows is None else rows):
             vals = ', '.join(cell(si, sp, o, q) for q in range(VE))
             st = (f'__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ov), ors, sofs + '
-                  f'{o * X * es + cfg.BSHIFT}u, 0, 2);')
+                  f'{o * X * es}u, 0, 2);')
             if not cfg.BMASK:
                 # every row of every band inside [ylo, yhi), x range = whole rows (checked at plan time)
-                dead = (f' __builtin_amdgcn_raw_buffer_store_b96((u32x3)__builtin_bit_cast(u32x4, ov).xyz, ors, '
-                        f'0x7ffffff0u + {cfg.BDEAD - 1}u * lane, 0, 2);' if cfg.BDEAD else '')
-                B.append(f'{ind}  {{ const {vt} ov = {{{vals}}}; {st}{dead} }}')
+                B.append(f'{ind}  {{ const {vt} ov = {{{vals}}}; {st} }}')
                 continue
             nb_t = (X % VE) * es if partial else 0           # bytes of a row's partial last chunk
             ndw_t, nh_t = nb_t // 4, (nb_t % 4) // 2       # whole dwords, then one half (X odd)
-            if cfg.BXW and not cfg.BMBR:
+            if cfg.BXW:
                 # whole rows: no branches. A row outside [ylo, yhi) (or an idle lane's) stores at an offset past the
                 # buffer's range, which the range check drops; a partial last chunk stores its whole dwords (and
                 # half) at the row offset while its 16-byte store is dropped, every other lane the reverse
@@ -664,11 +574,8 @@ def emit_band(ir, name, cfg):
                     c = 'xyzw'
                     B.append(f'{ind}    const u32x4 ow = __builtin_bit_cast(u32x4, ov);')
                     B.append(f'{ind}    __builtin_amdgcn_raw_buffer_store_b128(ow, ors, xtail ? 0x7ffffff0u : ro, 0, 2);')
-                    # the tail store under a branch on the tail lanes (BTB=1): a store whose 64 lanes all move data
-                    # costs the memory pipe about a full store even where the range check drops 63 of them
-                    # (profiles/r05_pitch_ablation.log: without output stores 510-wide rows run as fast as 512)
-                    B.append(f'{ind}    const unsigned rt = ro;' if cfg.BTB else
-                             f'{ind}    const unsigned rt = xtail ? ro : 0x7ffffff0u;')
+                    # (the tail store under a branch on the tail lanes measured slower: profiles/r05_pitch_btb.log)
+                    B.append(f'{ind}    const unsigned rt = xtail ? ro : 0x7ffffff0u;')
                     tb = []
                     if ndw_t:
                         ty = {1: 'unsigned', 2: 'u32x2', 3: 'u32x3'}[ndw_t]
@@ -676,10 +583,7 @@ def emit_band(ir, name, cfg):
                     if nh_t:
                         tb.append(f'__builtin_amdgcn_raw_buffer_store_b16((unsigned short)ow.{c[ndw_t]}, ors, '
                                   f'rt + {4 * ndw_t}u, 0, 2);')
-                    if cfg.BTB:
-                        B.append(f'{ind}    if (xtail) {{ ' + ' '.join(tb) + ' }')
-                    else:
-                        B += [f'{ind}    {t}' for t in tb]
+                    B += [f'{ind}    {t}' for t in tb]
                 else:
                     B.append(f'{ind}    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ov), ors, ro, 0, 2);')
                 B.append(f'{ind}  }}')
@@ -718,12 +622,7 @@ def emit_band(ir, name, cfg):
                     out.append(f'{dst}.{c[ndw_t]} = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(ors, '
                                f'sofs + {o * X * es + 4 * ndw_t}u, 0, 0);')
                 return ' '.join(out)
-            if cfg.BXW:
-                # the launch's x range is the whole row: the only chunk not stored whole is a 'bu' row's partial last
-                if partial:
-                    B.append(f'{ind}      const u32x4 ow = __builtin_bit_cast(u32x4, ov);')
-                    B.append(f'{ind}      {tail_store("ow")}')
-            elif cfg.XB:
+            if cfg.XB:
                 # x border cells: zeros (the row is stored whole); each cell selected on its own
                 sel = ', '.join(f'(x + {q} >= xlo && x + {q} < xhi) ? {cell(si, sp, o, q)} : ({et})0' for q in range(VE))
                 B.append(f'{ind}      const {vt} zv = {{{sel}}};')
@@ -799,7 +698,6 @@ def emit_band(ir, name, cfg):
         # idle lanes (band tasks not a multiple of 64) compute on a clamped task with wrong x neighbours: no stores
         act = 'active' if g['ntask'] != NCT else ''
         cond = ' && '.join(c for c in (store, act) if c) if store is not None else None
-        interleave = cfg.BSI and store is not None
         for r in range(R + 2):
             B.append(f'{ind}  {{')
             B += row_prologue(ind, r)
@@ -807,12 +705,6 @@ def emit_band(ir, name, cfg):
             # FMAs between two dependent ones)
             B += taps(f'{ind}    ', r, sets, first)
             B.append(f'{ind}  }}')
-            if interleave and r >= 2:
-                # output row r-2 of plane q-1 took its last taps (input row r, dy = +1): store it now
-                B.append(f'{ind}  if ({cond}) {{' if cond else f'{ind}  {{')
-                for si, fld in enumerate(store_field):
-                    B += stores(f'{ind}    ', si, sp, fld, [r - 2])
-                B.append(f'{ind}  }}')
         # outputs of q+1 that received no tap this plane (no dz = -1 taps) start from zero
         if any(dz == -1 for _, dz in sets):
             for si in range(NP):
@@ -822,7 +714,7 @@ def emit_band(ir, name, cfg):
                             B.append(f'{ind}  {A(si, sn, o, a)} = {azero};')
         if cfg.BABL == 2 and cond is not None:
             cond = f'({cond}) && Z < 0' if cond else 'Z < 0'          # ablation probe: no output stores
-        if store is not None and not interleave:
+        if store is not None:
             B.append(f'{ind}  if ({cond}) {{' if cond else f'{ind}  {{')
             for si, fld in enumerate(store_field):
                 B += stores(f'{ind}    ', si, sp, fld)

@@ -73,8 +73,12 @@ RING_WS_TILES = ((4, 4), (4, 2), (2, 4), (2, 2), (1, 4), (1, 2), (1, 1))
 # describe a one-thread-per-cell launch these schedules do not have, so they are accepted and ignored. Upper-case
 # keys are this layer's tile parameters; an unknown one is a typo and raises.
 TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
-             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BSTAG', 'BWPE', 'BLDR', 'BLAUX', 'BPAD', 'BZF', 'BREG', 'BMBR', 'BNT', 'BPE', 'BSI',
-             'BPRIO', 'BABL', 'BLW', 'BTB', 'BSHIFT', 'BDEAD', 'BFM', 'SFAST')
+             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BPAD', 'BZF', 'BREG', 'BNT', 'SFAST')
+# Ablation knobs that make results WRONG (timing probes: ``BABL``). They are not tile keys — ``gpu_indexing_params`` and
+# ``PSAD_MARCH`` reject them — and reach the planner only through this dict, which nothing on the op's path writes:
+# a probe script sets it explicitly (``scripts/probes/op_band_ab.py``) and clears it again.
+PROBE_KEYS = ('BABL',)
+PROBE_KNOBS = {}
 
 
 def _band_config(ir, ve, shape, over):
@@ -132,8 +136,8 @@ def _band_config(ir, ve, shape, over):
         R = int(over['BAND'])
     TY = int(over.get('BTY', TY if TY % R == 0 else R * max(1, TY // R)))
     D = int(over.get('D', D))
-    g = band_geometry(X, TY, R, D, es, pad, reg, int(over.get('BLW', 1)))
-    if TY % R or g['NCT'] > 960 or D * g['NIL'] > 63 or g['lds_bytes'] > 160 * 1024 or g['NT'] > 1024:
+    g = band_geometry(X, TY, R, D, es, pad, reg)
+    if TY % R or g['NCT'] > 960 or D * g['NI'] > 63 or g['lds_bytes'] > 160 * 1024 or g['NT'] > 1024:
         raise ValueError(f'band schedule: BTY={TY} BAND={R} D={D} do not fit rows of {X} elements')
     nty, Z = -(-int(shape[-2]) // TY), int(shape[0])
     min_wg = BAND_MIN_WG
@@ -158,14 +162,18 @@ def _band_config(ir, ve, shape, over):
         btrim = 1                       # chunk length not fixed at compile time: peel the chunk's first planes only
     return MarchConfig(VE=ve, BAND=R, BTY=TY, BX=X, D=D, ZSUM=True, NT_STORE=True, ZMIN=zc,
                        ZMAX=zmax, BLK=int(over.get('BLK', 512)), MAP=int(over.get('MAP', 0)),
-                       BTRIM=btrim, BEDGE=int(over.get('BEDGE', 1)),
-                       BSTAG=int(over.get('BSTAG', 0)), BWPE=int(over.get('BWPE', 0)), BLDR=int(over.get('BLDR', 0)),
-                       BLAUX=int(over.get('BLAUX', 0)), BPAD=pad, BZF=int(over.get('BZF', 1)), BREG=reg,
-                       BMBR=int(over.get('BMBR', 0)), BNT=int(over.get('BNT', 2)), BPE=int(over.get('BPE', 0)),
-                       BSI=int(over.get('BSI', 0)), BPRIO=int(over.get('BPRIO', 0)), BABL=int(over.get('BABL', 0)),
-                       BLW=int(over.get('BLW', 1)), BTB=int(over.get('BTB', 0)),
-                       BSHIFT=int(over.get('BSHIFT', 0)), BDEAD=int(over.get('BDEAD', 0)),
-                       BFM=int(over.get('BFM', 0)))
+                       BTRIM=btrim, BEDGE=int(over.get('BEDGE', 1)), BPAD=pad, BZF=int(over.get('BZF', 1)), BREG=reg,
+                       BNT=int(over.get('BNT', 2)), BABL=int(PROBE_KNOBS.get('BABL', 0)))
+
+
+def ws_fallback_config(cfg):
+    """The register-prefetch form of a WS (LDS-DMA loader) config, for planes beyond the loader's 32-bit buffer
+    offsets: eight compute waves exist only on the LDS-DMA ring, so NW drops to 4 (and WX to at most 4) as in
+    ``default_march_config``'s own fallback."""
+    c = {**cfg.__dict__, 'WS': False}
+    if c['NW'] == 8:
+        c['NW'], c['WX'] = 4, min(c['WX'], 4)
+    return MarchConfig(**c)
 
 
 def default_march_config(ir, ve, shape=None, tuning=None, band=True):
@@ -264,8 +272,8 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             cfg[k] = str(v)
         elif k == 'SFAST':
             cfg[k] = int(v)
-        elif k == 'BABL' and ring_ws:
-            cfg[k] = int(v)                 # (timing probe of the march ring, as on the band: 3 = no plane loads)
+    if ring_ws and PROBE_KNOBS.get('BABL'):
+        cfg['BABL'] = int(PROBE_KNOBS['BABL'])   # (timing probe of the march ring, as on the band: 3 = no plane loads)
     bc = _band_config(ir, ve, shape, over) if band else None
     if bc is not None:
         return bc
@@ -803,7 +811,7 @@ class HipStencilKernel:
             # planes beyond the loader's 32-bit buffer offsets: register-prefetch form of the same schedule
             # (never with XM: its rows straddle, which only the loader's zero fill repairs)
             assert not cfg.XM
-            cfg = MarchConfig(**{**cfg.__dict__, 'WS': False})
+            cfg = ws_fallback_config(cfg)
         xlo, xhi = ir.iteration_bounds(shape)[-1]
         if x_border and cfg.ZSUM and (xlo > 0 or xhi < shape[-1]) and \
                 not (ir.ndim == 2 and cfg.VIEW2D == 'zy'):
@@ -812,7 +820,7 @@ class HipStencilKernel:
             # unmasked stores when every band row lies in [ylo, yhi) and the x range is whole rows
             g0 = self.march_launch_geometry(shape, cfg, z_range, z_limits=z_limits)
             if not (g0['ylo'] == 0 and g0['yhi'] == g0['nty'] * cfg.BTY and g0['xlo'] == 0 and g0['xhi'] == g0['X']) or \
-                    g0['X'] % (16 // esize) or cfg.BFM:               # a partial last chunk per row (BFM: probe)
+                    g0['X'] % (16 // esize):                          # a partial last chunk per row
                 cfg = MarchConfig(**{**cfg.__dict__, 'BMASK': True,
                                      'BXW': g0['xlo'] == 0 and g0['xhi'] == g0['X'] and not cfg.XB})
         variant = ('march', cfg)
@@ -836,7 +844,7 @@ class HipStencilKernel:
                                           'nty')]
         kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics) + \
             [self._scalar_kind()] * len(ir.scalars)
-        block = ws['block'] if ws else (band_geometry(cfg.BX, cfg.BTY, cfg.BAND, cfg.D, esize, cfg.BPAD, cfg.BREG, cfg.BLW)['NT'] if cfg.BAND else
+        block = ws['block'] if ws else (band_geometry(cfg.BX, cfg.BTY, cfg.BAND, cfg.D, esize, cfg.BPAD, cfg.BREG)['NT'] if cfg.BAND else
                                         cfg.NT)
         return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics, xb=cfg.XB, block=block)
 

@@ -229,13 +229,15 @@ def create_lb_update_rule(stencil='D2Q9', relaxation_rate=None, compressible=Fal
 
         dst = f − Σ_g s_g P_g (f − feq),   P_g = M⁻¹ E_g M   (``mrt_relaxation_matrices``)
 
-    — all rates ω is SRT, ``[ω, ω, ω₋, ω]`` is TRT (the odd non-conserved moments are the third-order ones). The
-    rule keeps ``ac.mrt_rates`` (per group) for the lattice kernels.
+    — all rates ω is SRT. On D2Q9 and D3Q19 ``[ω, ω, ω₋, ω]`` is TRT (there the odd non-conserved moments are exactly
+    the third-order ones); on D3Q27 it is not: its odd fifth-order moments x²y²z, x²yz², xy²z² relax with the
+    fourth-order rate (``tests/test_lbm.py::test_lbm_mrt_trt_equivalence_per_stencil``). The rule keeps
+    ``ac.mrt_rates`` (per group) for the lattice kernels.
 
     Fields: ``src(q)``/``dst(q)`` vector fields in ``layout`` (``'fzyx'``: components slowest, lbmpy's default)
-    unless given. ``force_model`` ('simple' or 'guo'; TRT: 'simple') with ``force``: a body force — constant (numbers
-    or symbols per axis) or per cell (a vector field of D components: an additional input of the rule, its adjoint
-    accumulated over the steps)."""
+    unless given. ``force_model`` ('simple' or 'guo', with every method: Guo's force term is scaled by 1 − ω/2 with
+    the shear rate ω) with ``force``: a body force — constant (numbers or symbols per axis) or per cell (a vector
+    field of D components: an additional input of the rule, its adjoint accumulated over the steps)."""
     if kernel_type != 'stream_pull_collide':
         raise NotImplementedError("only kernel_type='stream_pull_collide' is restated")
     method = str(method).lower()

@@ -180,7 +180,13 @@ class FixedDensity(Boundary):
         comp = self.compressible if self.compressible is not None else getattr(lb_method, 'compressible', None)
         if comp is None:
             raise ValueError('FixedDensity: the method\'s compressibility is unknown (pass compressible=)')
-        rw = float(sp.sympify(self.density))
+        dens = sp.sympify(self.density)
+        if not dens.is_number:
+            # a symbolic wall density (a trained or scheduled pressure) is not a constant of the compiled link
+            # program; the general derivation refuses free symbols the same way (link_program)
+            raise NotImplementedError(f'FixedDensity({self.density!r}): the lattice kernels take a numeric wall '
+                                      'density (a symbol would have to be a kernel parameter)')
+        rw = float(dens)
         pr = _c_printer()
         D, Q = st.D, st.Q
         dirs = [tuple(int(v) for v in c) for c in st.directions]

@@ -12,6 +12,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', '..'))
 import pystencils_autodiff_amd as pa  # noqa: E402
+from pystencils_autodiff_amd.backends import hip_kernel as HK  # noqa: E402
 from pystencils_autodiff_amd import workloads as W  # noqa: E402
 
 WL = {'f7': (W.diffusion_7pt, torch.float32), 'h7': (lambda: W.diffusion_7pt(dtype='float16'), torch.float16),
@@ -40,8 +41,13 @@ def inputs(name, n):
 def make(name, n, band, march=''):
     b, dt = WL[name]
     os.environ['PSAD_BAND'] = '1' if band else '0'
-    if march:
-        os.environ['PSAD_MARCH'] = march
+    # ablation knobs (wrong results, timing only) go through the probe-only entry, the rest through PSAD_MARCH
+    kv = [t for t in march.split(',') if t]
+    HK.PROBE_KNOBS.clear()
+    HK.PROBE_KNOBS.update({t.split('=')[0]: int(t.split('=')[1]) for t in kv if t.split('=')[0] in HK.PROBE_KEYS})
+    tile = ','.join(t for t in kv if t.split('=')[0] not in HK.PROBE_KEYS)
+    if tile:
+        os.environ['PSAD_MARCH'] = tile
     op = pa.AutoDiffOp(b(), boundary_handling='zeros')
     fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
     u, d = inputs(name, n)
@@ -57,6 +63,7 @@ def make(name, n, band, march=''):
     if cfg.BAND:
         march = f'{march} BMASK={int(cfg.BMASK)} BPAD={cfg.BPAD} ZC={cfg.ZMIN}'.strip()
     os.environ.pop('PSAD_MARCH', None)
+    HK.PROBE_KNOBS.clear()
     return step, f'BAND={cfg.BAND} BTY={cfg.BTY} {march}'
 
 

@@ -10,6 +10,7 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', '..'))
 import pystencils_autodiff_amd as pa  # noqa: E402
 from pystencils_autodiff_amd import workloads as W  # noqa: E402
+from pystencils_autodiff_amd.backends import hip_kernel as HK  # noqa: E402
 from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel  # noqa: E402
 
 TILES = {
@@ -60,13 +61,16 @@ def main():
     out, du, dk = (torch.empty(shape, device='cuda', dtype=dt) for _ in range(3))
     cells = n ** 3
     for name in names:
-        p = TILES[name]
+        p = dict(TILES[name])
+        HK.PROBE_KNOBS.clear()          # ablation knobs are not tile keys: the probe-only entry
+        HK.PROBE_KNOBS.update({key: p.pop(key) for key in HK.PROBE_KEYS if key in p})
         fk = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='vcf', target='gpu',
                            gpu_indexing_params=p or None).compile()
         bk = StencilKernel(op.backward_assignments, boundary_handling='zeros', function_name='vcb', target='gpu',
                            gpu_indexing_params=p or None).compile()
         tf = timed(lambda: fk(u=u, k=k, out=out))
         tb = timed(lambda: bk(u=u, k=k, diffout=d, diffu=du, diffk=dk))
+        HK.PROBE_KNOBS.clear()
         v = fk.last_variant[1] if len(fk.last_variant) > 1 else None
         bv = bk.last_variant[1] if len(bk.last_variant) > 1 else None
         print(f'varcoef {n}^3 {name:10s} fwd {tf:.4f} ms ({3 * es * cells / tf / 1e6 / 8000:.3f})  bwd {tb:.4f} ms '

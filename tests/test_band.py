@@ -138,6 +138,28 @@ def test_band_default_selection_16_row_bands(builder, shape, expect):
     assert (cfg.BTY, cfg.BAND, cfg.D, cfg.ZMIN) == expect, cfg
 
 
+def test_probe_knobs_are_not_tile_keys(monkeypatch):
+    """Ablation knobs that give wrong results (``BABL``) and the removed probe knobs are rejected as tile parameters,
+    through ``gpu_indexing_params`` and ``PSAD_MARCH`` alike; only ``hip_kernel.PROBE_KNOBS`` (set by probe scripts,
+    never by the op) reaches the planner."""
+    from pystencils_autodiff_amd.backends import hip_kernel as HK
+    op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
+    ir = HipStencilKernel(_kernel(op.forward_assignments)).ir
+    for key in ('BABL', 'BSHIFT', 'BDEAD', 'BPE', 'BSI', 'BPRIO', 'BLAUX', 'BSTAG', 'BWPE', 'BLDR', 'BMBR', 'BTB',
+                'BFM', 'BLW'):
+        with pytest.raises(ValueError, match='unknown tile parameter'):
+            default_march_config(ir, 8, (768, 768, 768), {key: 1})
+        with pytest.raises(ValueError, match='unknown tile parameter'):        # the kernel's gpu_indexing_params
+            HipStencilKernel(_kernel(op.forward_assignments, **{key: 1}))._march_cfg(8, (768, 768, 768))
+        monkeypatch.setenv('PSAD_MARCH', f'{key}=1')
+        with pytest.raises(ValueError, match='unknown tile parameter'):
+            default_march_config(ir, 8, (768, 768, 768))
+        monkeypatch.delenv('PSAD_MARCH')
+    assert default_march_config(ir, 8, (768, 768, 768)).BABL == 0
+    monkeypatch.setitem(HK.PROBE_KNOBS, 'BABL', 2)
+    assert default_march_config(ir, 8, (768, 768, 768)).BABL == 2
+
+
 def test_band_sources_compile():
     from pystencils_autodiff_amd.backends import hip_runtime as rt
     from pystencils_autodiff_amd.backends.hip_emitter import MarchConfig
@@ -150,8 +172,7 @@ def test_band_sources_compile():
                   MarchConfig(**{**cfg.__dict__, 'BTRIM': 1}), MarchConfig(**{**cfg.__dict__, 'BTRIM': 2}),
                   MarchConfig(**{**cfg.__dict__, 'BTRIM': 3, 'ZMIN': 16, 'ZMAX': 16}),
                   MarchConfig(**{**cfg.__dict__, 'BPAD': 1}), MarchConfig(**{**cfg.__dict__, 'BPAD': 1, 'BMASK': True}),
-                  # round 3's branched masked stores, the store cache-policy probe
-                  MarchConfig(**{**cfg.__dict__, 'BMASK': True, 'BXW': True, 'BMBR': 1}),
+                  # the store cache-policy probe
                   MarchConfig(**{**cfg.__dict__, 'BMASK': True, 'BXW': True, 'BNT': 0})):
             src, kname = hk.source(('march', c))
             assert kname.endswith('_band') and 'band schedule' in src
@@ -183,14 +204,11 @@ def test_band_vs_oracle(case, shape, bh):
 @pytest.mark.parametrize('case', CASES, ids=lambda c: c[0])
 @pytest.mark.parametrize('shape', [(9, 21, 256), (7, 16, 768)])
 @pytest.mark.parametrize('bh', ['zeros', None])
-@pytest.mark.parametrize('knob', [{'BPAD': 1}, {'BPAD': 1, 'BPE': 3}, {'BPAD': 1, 'BSI': 1}, {'BPAD': 0},
-                                  {'BPAD': 1, 'BLW': 2}, {'BPAD': 0, 'BLW': 3}],
-                         ids=['pad', 'pad-dppedge', 'pad-storeil', 'dpp', 'pad-2loaders', 'dpp-3loaders'])
+@pytest.mark.parametrize('knob', [{'BPAD': 1}, {'BPAD': 0}], ids=['pad', 'dpp'])
 def test_band_padded_rows_vs_oracle(case, shape, bh, knob):
-    """Zero-padded LDS image rows (``BPAD=1``: row ends meet the zero pads) with the x-edge dwords read from LDS
-    (``BPE=0``) or taken from the neighbour lanes by DPP within 16-lane rows (``BPE=3``, the rows' end lanes read
-    theirs from LDS), output rows stored as soon as they are complete (``BSI=1``), and the unpadded image (``BPAD=0``:
-    wave-wide DPP plus boundary selects) vs the oracle, forward and adjoint, whole and masked stores."""
+    """Zero-padded LDS image rows (``BPAD=1``: row ends meet the zero pads, the x-edge dwords read from LDS) and the
+    unpadded image (``BPAD=0``: wave-wide DPP plus boundary selects) vs the oracle, forward and adjoint, whole and
+    masked stores."""
     _band_vs_oracle(case, shape, bh, **knob)
 
 
@@ -257,13 +275,12 @@ def test_band_unaligned_vs_oracle(case_shape, bh):
 @pytest.mark.gpu
 @pytest.mark.parametrize('case_shape', UNALIGNED, ids=lambda c: f'{c[0]}-{c[1][2]}')
 @pytest.mark.parametrize('bh', ['zeros', None])
-@pytest.mark.parametrize('knob', [{'BZF': 0}, {'BREG': 1}, {'BMBR': 1}], ids=['BZF0', 'BREG1', 'BMBR1'])
+@pytest.mark.parametrize('knob', [{'BZF': 0}, {'BREG': 1}], ids=['BZF0', 'BREG1'])
 def test_band_unaligned_variants_vs_oracle(case_shape, bh, knob):
     """Unaligned rows, forward and adjoint vs the oracle: ``BZF=0`` (no loader zero fill past each row end; the
     compute lanes of a row's last chunk zero its first element past X in registers) and ``BREG=1`` (a padded image
     filled through registers: row pieces read at the dword at or below them, realigned by v_alignbyte, cells past X
-    zeroed, written with ds_write_b128) and ``BMBR=1`` (round 3's masked stores behind per-row branches instead of
-    range-check drops)."""
+    zeroed, written with ds_write_b128)."""
     name, shape = case_shape
     _band_vs_oracle(next(c for c in CASES if c[0] == name), shape, bh, **knob)
 
@@ -308,11 +325,10 @@ def test_band_zslab_launch_pattern_bitwise(bh):
 @pytest.mark.gpu
 def test_band_chunk_length_and_band_height_bitwise():
     """Every output plane sees the same FMA sequence whatever the chunk length, band height (idle lanes on a 12-row
-    band), trimmed chunk-edge planes, loader placement or store placement: results bitwise equal WITHIN each image
-    layout / edge source. The layouts (padded image rows with the edge dwords from LDS, ``BPAD=1``; DPP across the
-    whole wave with boundary selects, ``BPAD=0``; the padded image with DPP edges, ``BPE=3``) compile to different
-    FMA contractions and differ by one fp16 ulp in ~3e-5 of the cells (DESIGN.md §4 band (7)): each layout's
-    reference is checked element-wise against the oracle instead."""
+    band) or trimmed chunk-edge planes: results bitwise equal WITHIN each image layout. The layouts (padded image rows
+    with the edge dwords from LDS, ``BPAD=1``; DPP across the whole wave with boundary selects, ``BPAD=0``) compile to
+    different FMA contractions and differ by one fp16 ulp in ~3e-5 of the cells (DESIGN.md §4 band (7)): each
+    layout's reference is checked element-wise against the oracle instead."""
     torch = _torch()
     op = pa.AutoDiffOp(W.stencil_27pt(), boundary_handling='zeros')
     g = torch.Generator().manual_seed(11)
@@ -324,16 +340,9 @@ def test_band_chunk_length_and_band_height_bitwise():
               {'BTRIM': 2, 'ZMIN': 9, 'ZMAX': 9},
               {'BTRIM': 2, 'ZMIN': 2, 'ZMAX': 2},               # chunks of < 3 planes: the untrimmed loop
               # both chunk ends peeled with a compile-time chunk length (ragged chunks: the BTRIM=1 path)
-              {'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13}, {'BTRIM': 3, 'ZMIN': 37, 'ZMAX': 37}, {'BTRIM': 3, 'ZMIN': 3, 'ZMAX': 3},
-              {'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13, 'BLDR': 1},  # the loader role rotating over waves
-              {'BSI': 1}, {'BSI': 1, 'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13},
-              {'BLW': 2}, {'BLW': 3, 'D': 3, 'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13})      # several loader waves
+              {'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13}, {'BTRIM': 3, 'ZMIN': 37, 'ZMAX': 37}, {'BTRIM': 3, 'ZMIN': 3, 'ZMAX': 3})
     layouts = {'BPAD=1': [{'BAND': 4, 'BPAD': 1, **t} for t in common],
-               'BPAD=0': [{'BAND': 4, 'BPAD': 0, **t} for t in common],
-               # x-edge dwords by DPP within 16-lane rows on the padded image: the compiler contracts these FMAs as on
-               # the unpadded image (the same 37 cells differ by one ulp from BPAD=1, gpurun_out r05_tests1.log)
-               'BPAD=1 BPE=3': [{'BAND': 4, 'BPAD': 1, 'BPE': 3, **t} for t in ({}, {'BTY': 12}, {'BSI': 1},
-                                                                             {'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13})]}
+               'BPAD=0': [{'BAND': 4, 'BPAD': 0, **t} for t in common]}
     ref64 = OE.evaluate(op.forward_assignments, {'u': u.double().cpu().numpy()}, boundary_handling='zeros')['out']
     absr = abs_terms(op.forward_assignments, {'u': u.double().cpu().numpy()}, 'zeros')['out']
     bad = []
@@ -344,7 +353,7 @@ def test_band_chunk_length_and_band_height_bitwise():
             out = torch.full_like(u, float('nan'))
             k(u=u, out=out)
             cfg = k.last_variant[1]
-            assert cfg.BAND == 4 and cfg.BPAD == tun['BPAD'] and cfg.BPE == tun.get('BPE', 0), cfg
+            assert cfg.BAND == 4 and cfg.BPAD == tun['BPAD'], cfg
             res.append((tun, cfg, out))
         torch.cuda.synchronize()
         assert_cells(res[0][2].double().cpu().numpy(), ref64, absr, 27, np.float16, f'{layout} reference')

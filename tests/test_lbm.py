@@ -4,6 +4,7 @@ through that restatement, conservation at full sizes. Parity with lbmpy itself i
 the oracle restates lbmpy's published SRT equations."""
 import numpy as np
 import pytest
+import sympy as sp
 
 from oracle import lbm as OL
 from pystencils_autodiff_amd import lbm, ps
@@ -865,6 +866,31 @@ def test_lbm_trt_cpu_vs_oracle(stencil, shape, compressible, odd, layout, walls,
     assert np.abs(step.adjoint_pdf_array - gref.numpy()).max() <= 1e-12 * np.abs(gref.numpy()).max()
 
 
+@pytest.mark.parametrize('stencil,equal', [('D2Q9', True), ('D3Q19', True), ('D3Q27', False)])
+def test_lbm_mrt_trt_equivalence_per_stencil(stencil, equal):
+    """MRT with rates [ω, ω, ω₋, ω] relaxes the non-equilibrium part like TRT — ω on the even part (f + f_ī)/2, ω₋ on
+    the odd part (f − f_ī)/2 — on D2Q9 and D3Q19, whose odd non-conserved moments are the third-order ones. Not on
+    D3Q27: its odd fifth-order moments x²y²z, x²yz², xy²z² sit in the fourth-order group (rate ω)."""
+    from pystencils_autodiff_amd.lbm._method import MRT_GROUPS, mrt_moments, mrt_relaxation_matrices
+    st = lbm.LBStencil(stencil)
+    Q = st.Q
+    P = {g: np.array(m, dtype=np.float64) for g, m in mrt_relaxation_matrices(st).items()}
+    cons = [np.array(r, dtype=np.float64) for g, r in mrt_moments(st) if g == 'conserved']
+    w_even, w_odd = 1.3, 0.7
+    R = sum({'third': w_odd}.get(g, w_even) * P[g] for g in MRT_GROUPS)
+    inv = [st.inverse_direction_index(i) for i in range(Q)]
+    Pi = np.zeros((Q, Q))
+    Pi[np.arange(Q), inv] = 1.0
+    T = w_even * (np.eye(Q) + Pi) / 2 + w_odd * (np.eye(Q) - Pi) / 2
+    rng = np.random.default_rng(7)
+    A = np.stack(cons)                                     # non-equilibrium parts carry no conserved moments
+    for _ in range(4):
+        v = rng.normal(size=Q)
+        v -= A.T @ np.linalg.lstsq(A @ A.T, A @ v, rcond=None)[0]
+        assert np.allclose(A @ v, 0, atol=1e-12)
+        assert np.allclose(R @ v, T @ v, atol=1e-12) == equal
+
+
 def test_lbm_trt_rule_api():
     """The TRT rule: ω₊ = ω₋ is SRT; lbmpy's magic-number relation; the odd rate as a kernel symbol runs on the
     AutoDiffOp kernels; unsupported combinations raise."""
@@ -1091,6 +1117,21 @@ def test_lbm_pressure_drives_flow():
     interior = ux[2:-2, 2:-2]
     assert interior.mean() > 1e-4
     assert rho[1, 5] > rho[-2, 5]
+
+
+def test_lbm_fixed_density_symbolic_raises_clearly():
+    """A FixedDensity with a symbolic density: a clear NotImplementedError from the link program (the lattice
+    kernels compile the wall density in), not a bare TypeError from float(); the forward link itself stays symbolic."""
+    st = lbm.LBStencil('D2Q9')
+    view = lbm.boundaries.LBMethodView(st, True)
+    rho = sp.Symbol('rho_w')
+    fd = lbm.FixedDensity(rho)
+    with pytest.raises(NotImplementedError, match='numeric wall density'):
+        fd.program(view)
+    with pytest.raises(NotImplementedError):
+        lbm.link_program(fd, lbm.AdjointBoundaryCondition(fd), view)
+    f = ps.fields('pdf(9): [2D]')
+    assert any(rho in a.rhs.free_symbols for a in fd(f, 1, view))
 
 
 def test_lbm_link_program_paths_agree():

@@ -135,6 +135,23 @@ def test_varcoef_tfmad_is_reverse_mode_for_uniform_k():
         assert not torch.allclose(gk[inner], tk[inner], rtol=1e-6, atol=1e-6)
 
 
+def test_ws_fallback_config_drops_eight_waves():
+    """Planes beyond the loader's 32-bit offsets take the register-prefetch form of the same schedule; an NW=8
+    override (LDS-DMA ring only) falls back to four waves instead of raising (geometry only, no GPU)."""
+    from pystencils_autodiff_amd.backends.hip_emitter import MarchConfig
+    from pystencils_autodiff_amd.backends.hip_kernel import HipStencilKernel, ws_fallback_config
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    op = _op('float32')
+    k = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='vcfb', target='gpu',
+                      gpu_indexing_params=dict(WS=1, NW=8, CX=2, WX=2, NR=1, D=2))
+    cfg = HipStencilKernel(k)._march_cfg(4, (64, 64, 256))
+    assert cfg.WS and cfg.NW == 8 and not cfg.ZSUM
+    fb = ws_fallback_config(cfg)
+    assert not fb.WS and fb.NW == 4 and fb.WX == 2 and (fb.CX, fb.NR) == (cfg.CX, cfg.NR)
+    four = ws_fallback_config(MarchConfig(**{**cfg.__dict__, 'NW': 4, 'WX': 1}))
+    assert not four.WS and four.NW == 4 and four.WX == 1
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize('shape', [(17, 33, 45), (9, 20, 128), (5, 7, 3), (40, 64, 256), (33, 50, 130)])
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float64, torch.float16], ids=['f32', 'f64', 'f16'])
