@@ -173,7 +173,8 @@ def roofline(name, r, world):
     traffic = tf + tb if tf is not None and tb is not None else None      # per step, like ``achieved``
     src = entry.get('source')
     if src and entry.get('git_head'):
-        src = f'{src}; collected at commit {entry["git_head"]}'
+        src = (f'{src}; collected at commit {entry["git_head"]} — the kernel sha (traffic_kernel_sha16 vs kernel_sha16), '
+               f'not the commit, ties the PMC passes to the kernels benched here')
     match = entry.get('kernel_sha16') == r['ksha'] if entry.get('kernel_sha16') else None
     return {'bound': 'hbm', 'achieved': round(r['achieved'], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': _sig(r['achieved'] / HBM_PEAK_GBS),

@@ -68,12 +68,13 @@ def band_padded(X, es, pad):
     return bool(pad) and (X * es) % 16 == 0
 
 
-def band_geometry(X, TY, R, D, es=2, pad=0, reg=0):
+def band_geometry(X, TY, R, D, es=2, pad=0, reg=0, free=0):
     """Launch / LDS geometry of a band of ``TY`` rows (``R`` per lane) on rows of ``X`` elements of ``es`` bytes.
     Rows whose pitch is not a multiple of 16 bytes (``X % VE``) take ``ceil(X / VE)`` chunks, the last one partial.
     ``pad``: every image row is preceded by one zero 16-byte piece and the slot ends with one (x neighbours of a row's
     end chunks read as zeros straight from LDS). ``reg``: rows of a partial last chunk on a padded image filled through
-    registers (``BREG``)."""
+    registers (``BREG``). ``free``: the LDS handshake instead of plane barriers (``BFREE``), ``free - 1`` slots beyond
+    ``D + 1``."""
     VE = 16 // es
     CPR = -(-X // VE)
     reg = bool(reg) and X % VE != 0
@@ -90,9 +91,9 @@ def band_geometry(X, TY, R, D, es=2, pad=0, reg=0):
     NPIECE = (TY + 2) * (XP // VE) + (1 if padded else 0)
     NI = -(-NPIECE // 64)
     SLOT = NI * 64 * VE
-    NS = 3 if reg else D + 1
+    NS = 3 if reg else D + 1 + max(0, int(free) - 1)
     return dict(VE=VE, CPR=CPR, XP=XP, G=G, ntask=ntask, NCT=NCT, NT=NCT + 64, NPIECE=NPIECE, NI=NI, SLOT=SLOT,
-                NS=NS, lds_bytes=(NS * SLOT + 64) * es)
+                NS=NS, lds_bytes=(NS * SLOT + 64) * es + (64 if free else 0))
 
 
 def _fits(X, TY, R, D, es=2, pad=0, reg=0, idle=False):
@@ -161,7 +162,7 @@ def emit_band(ir, name, cfg):
     TY, R, D = cfg.BTY, cfg.BAND, cfg.D
     breg = bool(cfg.BREG) and X % (16 // es) != 0     # partial rows on a padded image filled through registers
     padded = breg or band_padded(X, es, cfg.BPAD)
-    g = band_geometry(X, TY, R, D, es, padded, breg)
+    g = band_geometry(X, TY, R, D, es, padded, breg, cfg.BFREE)
     VE, CPR, G, NCT, NT, NPIECE, NI, SLOT, NS = (g[k] for k in ('VE', 'CPR', 'G', 'NCT', 'NT', 'NPIECE', 'NI', 'SLOT',
                                                                  'NS'))
     assert D * NI <= 63 and NT <= 1024, (X, TY, R, D)
@@ -177,6 +178,9 @@ def emit_band(ir, name, cfg):
     bo = not breg and (X * es) % 4 != 0             # rows on half dwords (fp16, X odd): realigned in registers
     assert not partial or cfg.BMASK, 'rows of a partial last chunk need the masked stores'
     czf = bu and not cfg.BZF                        # BZF=0: the first element past a row zeroed in registers
+    free = bool(cfg.BFREE)                          # LDS handshake instead of the plane barriers
+    assert not (free and breg), 'the LDS handshake takes the LDS-DMA loader'
+    NCW = NCT // 64                                 # compute waves
     pr = KernelExprPrinter('float', dict(ir.symbol_names))
     W = []
     for pl in plans:
@@ -212,6 +216,14 @@ def emit_band(ir, name, cfg):
     L.append(f'  __shared__ __attribute__((aligned(1024))) {et} lds[{NS * SLOT + 64}];')
     L.append('  const int tid = threadIdx.x, lane = tid & 63;')
     L.append('  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);')
+    if free:
+        # hs[0]: planes landed (the loader's), hs[1 + w]: planes compute wave w has finished reading (its own word).
+        # Set before the one workgroup barrier of the kernel; the plane steps then never meet at a barrier
+        L.append(f'  __shared__ unsigned hs[{NCW + 1}];          // (relaxed workgroup atomics: ds_read / ds_write, not flat)')
+        L.append('  auto hs_ld = [&](const int i) { return __hip_atomic_load(&hs[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };')
+        L.append('  auto hs_st = [&](const int i, const unsigned v) { __hip_atomic_store(&hs[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };')
+        L.append(f'  if (tid <= {NCW}) hs[tid] = 0u;')
+        L.append('  __syncthreads();')
     if cfg.MAP == 1:
         L.append('  const int lb = blockIdx.x;')
     else:
@@ -278,6 +290,18 @@ def emit_band(ir, name, cfg):
         L.append(f'        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + i * '
                  f'{64 * VE}), 16, {"pp ? vo1[i] : vo[i]" if bo else "vo[i]"}, 0, 0, 0);')
         L.append('    };')
+        if free:
+            # slot reuse: plane p goes into the slot of plane p - NS, which every compute wave must have released
+            # (hs[1 + w] >= p - NS + 1); one LDS dword per lane, a wave-wide vote, s_sleep between polls
+            L.append('    auto wait_free = [&](const int need) {')
+            L.append('      if (need <= 0) return;')
+            L.append('      while (true) {')
+            L.append(f'        const unsigned v = lane < {NCW} ? hs_ld(1 + lane) : 0xffffffffu;')
+            L.append('        if (__builtin_amdgcn_ballot_w64(v < (unsigned)need) == 0ull) break;')
+            L.append('        __builtin_amdgcn_s_sleep(1);')
+            L.append('      }')
+            L.append('      asm volatile("" ::: "memory");')
+            L.append('    };')
         L.append(f'    for (int i = 0; i < {D}; ++i)')
         L.append('      if (i < nplanes) issue(zb - 1 + i, i);')
         L.append('    for (int j = 0; j < nplanes; ++j) {')
@@ -309,8 +333,13 @@ def emit_band(ir, name, cfg):
                      f'img[(i / {ndw}) * {XP * es // 4} + {X * es // 4} + i % {ndw}] = 0u;')
             L.append('        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
             L.append('      }')
-        L.append('      __builtin_amdgcn_s_barrier();')
-        L.append(f'      if (j + {D} < nplanes) issue(zb - 1 + j + {D}, (j + {D}) % {NS});')
+        if free:
+            # publish plane j (its DMA landed: the vmcnt wait above; the zero fill: its lgkmcnt wait), then refill
+            L.append('      if (lane == 0) hs_st(0, (unsigned)(j + 1));')
+            L.append(f'      if (j + {D} < nplanes) {{ wait_free(j + {D} - {NS} + 1); issue(zb - 1 + j + {D}, (j + {D}) % {NS}); }}')
+        else:
+            L.append('      __builtin_amdgcn_s_barrier();')
+            L.append(f'      if (j + {D} < nplanes) issue(zb - 1 + j + {D}, (j + {D}) % {NS});')
         L.append('    }')
         L.append('    return;')
         L.append('  }')
@@ -677,9 +706,18 @@ def emit_band(ir, name, cfg):
         # (lgkmcnt) before it and none of them moves past it, none of this plane's moves above it (with
         # __syncthreads() hipcc 7.2 sank a peeled step's reads below the next step's barrier on the padded-row
         # image: the loader had already refilled that slot; scripts/probes/band_determinism.py)
-        B = [f'{ind}if ({guard}) {{' if guard else f'{ind}{{',
-             f'{ind}  asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");',
-             f'{ind}  const {et}* sl = lds + (jj % {NS}) * {SLOT} + lofs;']
+        B = [f'{ind}if ({guard}) {{' if guard else f'{ind}{{']
+        if free:
+            # acquire: plane jj has landed once the loader's word exceeds jj (the last value seen is kept, so a wave
+            # behind the loader polls no more); the memory clobbers keep this plane's LDS reads below the poll
+            B += [f'{ind}  while ((int)seen <= jj) {{',
+                  f'{ind}    seen = __builtin_amdgcn_readfirstlane(hs_ld(0));',
+                  f'{ind}    if ((int)seen <= jj) __builtin_amdgcn_s_sleep(1);',
+                  f'{ind}  }}',
+                  f'{ind}  asm volatile("" ::: "memory");']
+        else:
+            B.append(f'{ind}  asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");')
+        B.append(f'{ind}  const {et}* sl = lds + (jj % {NS}) * {SLOT} + lofs;')
         if bo:
             # v_perm selectors: input row parity = plane parity ^ (y0 - 1 + row) & 1, y0 and R even -> odd rows r of
             # the lane take the plane's parity (selA), even rows the other one (selB); 0x05040302 = elements shifted
@@ -698,6 +736,7 @@ def emit_band(ir, name, cfg):
         # idle lanes (band tasks not a multiple of 64) compute on a clamped task with wrong x neighbours: no stores
         act = 'active' if g['ntask'] != NCT else ''
         cond = ' && '.join(c for c in (store, act) if c) if store is not None else None
+
         for r in range(R + 2):
             B.append(f'{ind}  {{')
             B += row_prologue(ind, r)
@@ -705,6 +744,11 @@ def emit_band(ir, name, cfg):
             # FMAs between two dependent ones)
             B += taps(f'{ind}    ', r, sets, first)
             B.append(f'{ind}  }}')
+        if free:
+            # release: this plane's LDS reads are complete; the loader may refill its slot
+            B += [f'{ind}  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");',
+                  f'{ind}  if (lane == 0) hs_st(1 + wave, (unsigned)(jj + 1));',
+                  f'{ind}  asm volatile("" ::: "memory");']
         # outputs of q+1 that received no tap this plane (no dz = -1 taps) start from zero
         if any(dz == -1 for _, dz in sets):
             for si in range(NP):
@@ -722,6 +766,9 @@ def emit_band(ir, name, cfg):
         B.append(f'{ind}  ++jj;')
         B.append(f'{ind}}}')
         return B
+
+    if free:
+        L.append('  unsigned seen = 0u;                               // planes known landed (hs[0])')
     L.append('  int jj = 0;')
     if cfg.BTRIM == 1:
         # the chunk's first two input planes run peeled steps without the taps of outputs before it (27 of 27·(zc+2)

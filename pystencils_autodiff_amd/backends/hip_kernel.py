@@ -73,7 +73,8 @@ RING_WS_TILES = ((4, 4), (4, 2), (2, 4), (2, 2), (1, 4), (1, 2), (1, 1))
 # describe a one-thread-per-cell launch these schedules do not have, so they are accepted and ignored. Upper-case
 # keys are this layer's tile parameters; an unknown one is a typo and raises.
 TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
-             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BPAD', 'BZF', 'BREG', 'BNT', 'SFAST')
+             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BPAD', 'BZF', 'BREG', 'BNT', 'BFREE',
+             'SFAST')
 # Ablation knobs that make results WRONG (timing probes: ``BABL``). They are not tile keys — ``gpu_indexing_params`` and
 # ``PSAD_MARCH`` reject them — and reach the planner only through this dict, which nothing on the op's path writes:
 # a probe script sets it explicitly (``scripts/probes/op_band_ab.py``) and clears it again.
@@ -115,7 +116,8 @@ def _band_config(ir, ve, shape, over):
         return None
     TY, R, D = choice
     pad = int(over.get('BPAD', BAND_PAD_BOX if ntaps > 12 else 0))
-    reg = int(over.get('BREG', BAND_REG_STAR_ODD if ntaps <= 12 and es == 2 and X % 2 else 0))
+    reg = int(over.get('BREG', BAND_REG_STAR_ODD if ntaps <= 12 and es == 2 and X % 2 and not int(over.get('BFREE', 0))
+                       else 0))                 # (the LDS handshake takes the LDS-DMA loader)
     # fp32 star stencils: 8-row bands of 4 rows per lane (see BAND_F32_STAR_MAX_X) — one output only (band_choice's
     # rule: at most 2 rows per lane when a kernel stores two fields)
     g8 = band_geometry(X, 8, 4, 2, 4, pad, reg) if es == 4 and len(plans) == 1 else None
@@ -136,7 +138,7 @@ def _band_config(ir, ve, shape, over):
         R = int(over['BAND'])
     TY = int(over.get('BTY', TY if TY % R == 0 else R * max(1, TY // R)))
     D = int(over.get('D', D))
-    g = band_geometry(X, TY, R, D, es, pad, reg)
+    g = band_geometry(X, TY, R, D, es, pad, reg, free=int(over.get('BFREE', 0)))
     if TY % R or g['NCT'] > 960 or D * g['NI'] > 63 or g['lds_bytes'] > 160 * 1024 or g['NT'] > 1024:
         raise ValueError(f'band schedule: BTY={TY} BAND={R} D={D} do not fit rows of {X} elements')
     nty, Z = -(-int(shape[-2]) // TY), int(shape[0])
@@ -163,7 +165,8 @@ def _band_config(ir, ve, shape, over):
     return MarchConfig(VE=ve, BAND=R, BTY=TY, BX=X, D=D, ZSUM=True, NT_STORE=True, ZMIN=zc,
                        ZMAX=zmax, BLK=int(over.get('BLK', 512)), MAP=int(over.get('MAP', 0)),
                        BTRIM=btrim, BEDGE=int(over.get('BEDGE', 1)), BPAD=pad, BZF=int(over.get('BZF', 1)), BREG=reg,
-                       BNT=int(over.get('BNT', 2)), BABL=int(PROBE_KNOBS.get('BABL', 0)))
+                       BNT=int(over.get('BNT', 2)), BFREE=int(over.get('BFREE', 0)),
+                       BABL=int(PROBE_KNOBS.get('BABL', 0)))
 
 
 def ws_fallback_config(cfg):
@@ -844,7 +847,7 @@ class HipStencilKernel:
                                           'nty')]
         kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics) + \
             [self._scalar_kind()] * len(ir.scalars)
-        block = ws['block'] if ws else (band_geometry(cfg.BX, cfg.BTY, cfg.BAND, cfg.D, esize, cfg.BPAD, cfg.BREG)['NT'] if cfg.BAND else
+        block = ws['block'] if ws else (band_geometry(cfg.BX, cfg.BTY, cfg.BAND, cfg.D, esize, cfg.BPAD, cfg.BREG, cfg.BFREE)['NT'] if cfg.BAND else
                                         cfg.NT)
         return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics, xb=cfg.XB, block=block)
 

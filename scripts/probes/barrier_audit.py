@@ -6,6 +6,14 @@ every ``s_barrier`` of a kernel, the worst number of ``ds_read`` instructions no
 ``s_waitcnt lgkmcnt`` on any path reaching it (a dataflow fixed point over the kernel's basic blocks, so the
 loops' back edges count). Exit status 1 if any barrier has one.
 
+With the band schedule's LDS handshake (``BFREE``: no plane barriers) the same dataflow checks the two halves of
+the handshake instead: at every ``ds_write`` (a compute wave's release word, the loader's published-plane word and
+zero fill) no ``ds_read`` may be outstanding — a release issued before the plane's reads returned would let the
+loader refill the slot under them — and on every path the plane reads between two releases (poll reads, a
+``ds_read_b32`` whose value goes through ``v_readfirstlane``, not counted) are the same count, so no read crossed a
+release into another plane step. (A read hoisted above its own step's poll is excluded at the source: a memory
+clobber follows the poll; the compiler may place the poll loops out of line, so program order says nothing here.)
+
 python scripts/probes/barrier_audit.py <workload> <Z,Y,X> [KEY=VAL,...] [forward|backward]   (no GPU needed)
 python scripts/probes/barrier_audit.py --isa kernel.s
 """
@@ -56,8 +64,8 @@ def parse(text):
     return ins
 
 
-def audit(ins):
-    """Worst outstanding ds_read count at each s_barrier: {index: count}."""
+def audit(ins, at=('s_barrier',)):
+    """Worst outstanding ds_read count at each instruction whose opcode starts with one of ``at``: {index: count}."""
     base = ins[0][0] if ins else 0
     index = {a - base: i for i, (a, _, _, _) in enumerate(ins)}
     # successors of each instruction
@@ -96,7 +104,58 @@ def audit(ins):
             if new != state[j]:
                 state[j] = new
                 work.append(j)
-    return {i: state[i][1] for i, (_, op, _, _) in enumerate(ins) if op == 's_barrier' and state[i] is not None}
+    return {i: state[i][1] for i, (_, op, _, _) in enumerate(ins) if op.startswith(at) and state[i] is not None}
+
+
+def polls(ins):
+    """Indices of the acquire polls: a ds_read_b32 whose destination is read by a v_readfirstlane_b32 within the next
+    few instructions (the wave-uniform read of the loader's published-plane word)."""
+    out = []
+    for i, (_, op, args, _) in enumerate(ins):
+        if op != 'ds_read_b32':
+            continue
+        dst = args.split(',')[0].strip()
+        for j in range(i + 1, min(i + 6, len(ins))):
+            if ins[j][1] == 'v_readfirstlane_b32' and dst in ins[j][2].split(',')[1:][0]:
+                out.append(i)
+                break
+    return out
+
+
+def release_intervals(ins, poll_reads):
+    """(min, max) plane reads since the previous ds_write on any path reaching each ds_write."""
+    base = ins[0][0] if ins else 0
+    index = {a - base: i for i, (a, _, _, _) in enumerate(ins)}
+    succ = []
+    for i, (a, op, args, tgt) in enumerate(ins):
+        s = []
+        if op == 's_branch':
+            s.append(index.get(tgt))
+        elif op != 's_endpgm':
+            if i + 1 < len(ins):
+                s.append(i + 1)
+            if tgt is not None:
+                s.append(index.get(tgt))
+        succ.append([j for j in s if j is not None])
+    state = [None] * len(ins)
+    state[0] = (0, 0)
+    work = [0]
+    out = {}
+    while work:
+        i = work.pop()
+        lo, hi = state[i]
+        op = ins[i][1]
+        if op.startswith('ds_write'):
+            out[i] = (lo, hi)
+            lo = hi = 0
+        elif op.startswith('ds_read') and i not in poll_reads:
+            lo, hi = min(lo + 1, 999), min(hi + 1, 999)
+        for j in succ[i]:
+            new = (lo, hi) if state[j] is None else (min(state[j][0], lo), max(state[j][1], hi))
+            if new != state[j]:
+                state[j] = new
+                work.append(j)
+    return out
 
 
 def main():
@@ -112,6 +171,16 @@ def main():
         text, cfg = disassemble(sys.argv[1], tuple(int(v) for v in sys.argv[2].split(',')), tun, which)
     ins = parse(text)
     res = audit(ins)
+    if cfg is not None and getattr(cfg, 'BFREE', 0):
+        wr = audit(ins, ('ds_write',))
+        bad = sum(1 for v in wr.values() if v > 0)
+        ps = polls(ins)
+        iv = release_intervals(ins, set(ps))
+        counts = sorted({v for lo_hi in iv.values() for v in lo_hi})
+        print(f'  handshake: {len(wr)} ds_write, {bad} with a ds_read outstanding on the worst path; {len(ps)} acquire '
+              f'polls; plane reads between releases on any path: {counts}')
+        print(f'{" ".join(sys.argv[1:])} [band, LDS handshake]: {"FAIL" if bad else "ok"}')
+        sys.exit(1 if bad else 0)
     bad = 0
     bars = sorted(res)
     for k, i in enumerate(bars):

@@ -30,6 +30,8 @@ def main():
         r = []
         if 'SQ_WAIT_ANY' in c and c.get('SQ_WAVE_CYCLES'):
             r.append(f"SQ_WAIT_ANY / SQ_WAVE_CYCLES = {c['SQ_WAIT_ANY'] / c['SQ_WAVE_CYCLES']:.3f}")
+        if 'SQ_WAIT_INST_ANY' in c and c.get('SQ_WAVE_CYCLES'):
+            r.append(f"SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES = {c['SQ_WAIT_INST_ANY'] / c['SQ_WAVE_CYCLES']:.3f}")
         if 'SQ_ACTIVE_INST_VALU' in c and c.get('SQ_WAVE_CYCLES'):
             r.append(f"SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES = {c['SQ_ACTIVE_INST_VALU'] / c['SQ_WAVE_CYCLES']:.3f}")
         if 'SQ_LDS_BANK_CONFLICT' in c and c.get('SQ_LDS_IDX_ACTIVE'):

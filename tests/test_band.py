@@ -173,7 +173,10 @@ def test_band_sources_compile():
                   MarchConfig(**{**cfg.__dict__, 'BTRIM': 3, 'ZMIN': 16, 'ZMAX': 16}),
                   MarchConfig(**{**cfg.__dict__, 'BPAD': 1}), MarchConfig(**{**cfg.__dict__, 'BPAD': 1, 'BMASK': True}),
                   # the store cache-policy probe
-                  MarchConfig(**{**cfg.__dict__, 'BMASK': True, 'BXW': True, 'BNT': 0})):
+                  MarchConfig(**{**cfg.__dict__, 'BMASK': True, 'BXW': True, 'BNT': 0}),
+                  # the LDS handshake instead of plane barriers
+                  MarchConfig(**{**cfg.__dict__, 'BFREE': 1}), MarchConfig(**{**cfg.__dict__, 'BFREE': 2, 'BMASK': True}),
+                  MarchConfig(**{**cfg.__dict__, 'BFREE': 3, 'BTRIM': 3, 'ZMIN': 16, 'ZMAX': 16, 'BMASK': True})):
             src, kname = hk.source(('march', c))
             assert kname.endswith('_band') and 'band schedule' in src
             assert len(rt.compile_hip(src)) > 0
@@ -204,11 +207,14 @@ def test_band_vs_oracle(case, shape, bh):
 @pytest.mark.parametrize('case', CASES, ids=lambda c: c[0])
 @pytest.mark.parametrize('shape', [(9, 21, 256), (7, 16, 768)])
 @pytest.mark.parametrize('bh', ['zeros', None])
-@pytest.mark.parametrize('knob', [{'BPAD': 1}, {'BPAD': 0}], ids=['pad', 'dpp'])
+@pytest.mark.parametrize('knob', [{'BPAD': 1}, {'BPAD': 0}, {'BPAD': 1, 'BFREE': 1}, {'BPAD': 0, 'BFREE': 2},
+                                  {'BPAD': 1, 'BFREE': 3}],
+                         ids=['pad', 'dpp', 'pad-handshake', 'dpp-handshake4', 'pad-handshake5'])
 def test_band_padded_rows_vs_oracle(case, shape, bh, knob):
     """Zero-padded LDS image rows (``BPAD=1``: row ends meet the zero pads, the x-edge dwords read from LDS) and the
     unpadded image (``BPAD=0``: wave-wide DPP plus boundary selects) vs the oracle, forward and adjoint, whole and
-    masked stores."""
+    masked stores; the same with the per-plane LDS handshake instead of the plane barriers (``BFREE``, deeper rings
+    at 2 and 3)."""
     _band_vs_oracle(case, shape, bh, **knob)
 
 
@@ -275,7 +281,7 @@ def test_band_unaligned_vs_oracle(case_shape, bh):
 @pytest.mark.gpu
 @pytest.mark.parametrize('case_shape', UNALIGNED, ids=lambda c: f'{c[0]}-{c[1][2]}')
 @pytest.mark.parametrize('bh', ['zeros', None])
-@pytest.mark.parametrize('knob', [{'BZF': 0}, {'BREG': 1}], ids=['BZF0', 'BREG1'])
+@pytest.mark.parametrize('knob', [{'BZF': 0}, {'BREG': 1}, {'BFREE': 2}], ids=['BZF0', 'BREG1', 'BFREE2'])
 def test_band_unaligned_variants_vs_oracle(case_shape, bh, knob):
     """Unaligned rows, forward and adjoint vs the oracle: ``BZF=0`` (no loader zero fill past each row end; the
     compute lanes of a row's last chunk zero its first element past X in registers) and ``BREG=1`` (a padded image
@@ -340,7 +346,10 @@ def test_band_chunk_length_and_band_height_bitwise():
               {'BTRIM': 2, 'ZMIN': 9, 'ZMAX': 9},
               {'BTRIM': 2, 'ZMIN': 2, 'ZMAX': 2},               # chunks of < 3 planes: the untrimmed loop
               # both chunk ends peeled with a compile-time chunk length (ragged chunks: the BTRIM=1 path)
-              {'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13}, {'BTRIM': 3, 'ZMIN': 37, 'ZMAX': 37}, {'BTRIM': 3, 'ZMIN': 3, 'ZMAX': 3})
+              {'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13}, {'BTRIM': 3, 'ZMIN': 37, 'ZMAX': 37}, {'BTRIM': 3, 'ZMIN': 3, 'ZMAX': 3},
+              # the LDS handshake instead of plane barriers: synchronisation only, the same FMAs
+              {'BFREE': 1}, {'BFREE': 2, 'BTRIM': 3, 'ZMIN': 13, 'ZMAX': 13}, {'BFREE': 3, 'ZMIN': 5, 'ZMAX': 5},
+              {'BFREE': 2, 'BTY': 12}, {'BFREE': 1, 'BTRIM': 1, 'ZMIN': 16, 'ZMAX': 16})
     layouts = {'BPAD=1': [{'BAND': 4, 'BPAD': 1, **t} for t in common],
                'BPAD=0': [{'BAND': 4, 'BPAD': 0, **t} for t in common]}
     ref64 = OE.evaluate(op.forward_assignments, {'u': u.double().cpu().numpy()}, boundary_handling='zeros')['out']

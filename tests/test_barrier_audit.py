@@ -30,3 +30,26 @@ def test_no_lds_read_outstanding_at_any_barrier(workload, shape, tun, which):
     assert res, 'no s_barrier found'
     bad = {i: n for i, n in res.items() if n}
     assert not bad, f'{workload} {which}: LDS reads outstanding at {len(bad)} barrier(s): {bad}'
+
+
+HANDSHAKE = [('stencil27', (768, 768, 768), {'BFREE': 2}), ('diffusion7_f16', (768, 768, 768), {'BFREE': 1}),
+             ('stencil27', (64, 64, 512), {'BFREE': 3, 'BAND': 4}), ('diffusion7_f16', (64, 64, 1024), {'BFREE': 2, 'BAND': 2})]
+
+
+@pytest.mark.skipif(not os.path.exists(OBJDUMP), reason='llvm-objdump not in this image')
+@pytest.mark.parametrize('which', ['forward', 'backward'])
+@pytest.mark.parametrize('workload,shape,tun', HANDSHAKE, ids=[f'{c[0]}-{c[1][2]}-{c[2]["BFREE"]}' for c in HANDSHAKE])
+def test_band_handshake_releases_after_reads(workload, shape, tun, which):
+    """The band's LDS handshake (``BFREE``, no plane barriers): at every ``ds_write`` — a compute wave's release word,
+    the loader's published-plane word or its zero fill — no ``ds_read`` is outstanding on any path, and the handshake
+    words are LDS operations (``ds_``), not flat ones (a flat access would also wait on the wave's stores)."""
+    import barrier_audit as B
+    text, cfg = B.disassemble(workload, shape, tun, which)
+    assert cfg.BAND and cfg.BFREE == tun['BFREE'], cfg
+    ins = B.parse(text)
+    assert not [op for _, op, _, _ in ins if op.startswith('flat_')], 'flat memory operations in the band kernel'
+    res = B.audit(ins, ('ds_write',))
+    assert len(res) >= 6, f'expected release / publish writes, found {len(res)}'
+    bad = {i: n for i, n in res.items() if n}
+    assert not bad, f'{workload} {which}: LDS reads outstanding at {len(bad)} ds_write(s): {bad}'
+    assert B.polls(ins), 'no acquire poll (ds_read_b32 -> v_readfirstlane_b32) found'

@@ -497,7 +497,7 @@ def test_zslab_full_size_eight_ranks_emulated(builder_name, edge, tmp_path):
     world = 8
     from oracle import stencils as S
     from pystencils_autodiff_amd.zslab import slab_bounds
-    from tests.conftest import assert_close_rel
+    from tests.conftest import assert_cells, assert_close_rel
     mp.spawn(_full_size_worker, args=(world, _free_port(), builder_name, edge, str(tmp_path)), nprocs=world,
              join=True)
     f16 = builder_name == 'stencil_27pt'
@@ -506,17 +506,22 @@ def test_zslab_full_size_eight_ranks_emulated(builder_name, edge, tmp_path):
     tol = 1e-3 if f16 else 1e-6
 
     def ref_plane(p, seed, signed, tp):
+        """(the oracle's plane p, Σ|w·u| per cell: the same stencil with |w| on |u|)"""
         a, b = max(0, p - 1), min(edge, p + 2)
         block = np.zeros((3, edge, edge))
         block[a - (p - 1):b - (p - 1)] = _synth_planes(a, b, edge, edge, seed, dt, signed)
-        return S.linear_stencil(block, tp)[1]
+        absw = {o: abs(w) for o, w in tp.items()}
+        return S.linear_stencil(block, tp)[1], S.linear_stencil(np.abs(block), absw)[1]
     for r in range(world):
         lo, hi = slab_bounds(edge, world, r)
         assert hi - lo == edge // world
         out, du = np.load(tmp_path / f'out_{r}.npy'), np.load(tmp_path / f'du_{r}.npy')
         for k, p in enumerate((lo, hi - 1)):
-            assert_close_rel(out[k], ref_plane(p, 1, False, taps), tol, f'rank {r} out plane {p}')
-            assert_close_rel(du[k], ref_plane(p, 2, True, S.flip(taps)), tol, f'rank {r} diffu plane {p}')
+            for got, (ref, absr), name in ((out[k], ref_plane(p, 1, False, taps), 'out'),
+                                           (du[k], ref_plane(p, 2, True, S.flip(taps)), 'diffu')):
+                assert_close_rel(got, ref, tol, f'rank {r} {name} plane {p}')
+                # element-wise: the north star's relative error plus the fp32 sum bound (+ half an fp16 ulp)
+                assert_cells(got, ref, absr, len(taps), dt, f'rank {r} {name} plane {p}')
     ad, ua, mass, fin_o, fin_d = json.load(open(tmp_path / 'dots.json'))
     assert fin_o == world and fin_d == world
     assert mass > 0
