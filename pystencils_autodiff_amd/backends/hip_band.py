@@ -24,7 +24,8 @@ in ``scripts/probes/rowblock27r.py`` (``profiles/r03_band_*.log``).
 """
 import numpy as np
 
-from .hip_emitter import PRELUDE, MarchConfig, _field_params, _scalar_params, _ws_plane_base, zsum_plan
+from .hip_emitter import (PRELUDE, SIG_PARAMS, MarchConfig, _field_params, _scalar_params, _ws_plane_base,
+                          start_signal_lines, zsum_plan)
 from .printer import KernelExprPrinter
 
 __all__ = ['band_plans', 'band_geometry', 'band_choice', 'band_esize', 'emit_band']
@@ -206,6 +207,7 @@ def emit_band(ir, name, cfg):
     params += ['const int Z', 'const int Y', 'const int X', 'const int zlo', 'const int zhi', 'const int ylo',
                'const int yhi', 'const int xlo', 'const int xhi', 'const int zc', 'const int zstep', 'const int ntx',
                'const int nty']
+    params += SIG_PARAMS if cfg.SIG else []
     params += _scalar_params(ir)
     L = [PRELUDE, 'typedef unsigned u32x4 __attribute__((ext_vector_type(4)));',
          'typedef unsigned u32x3 __attribute__((ext_vector_type(3)));', 'typedef unsigned u32x2 __attribute__((ext_vector_type(2)));']
@@ -213,6 +215,8 @@ def emit_band(ir, name, cfg):
              f'compute waves + LDS-DMA loader wave, {NS}-slot {et} plane ring ({D} planes in flight), z partial sums '
              f'in 3 rotating register sets, LDS {g["lds_bytes"]} B')
     L.append(f'extern "C" __global__ void __launch_bounds__({NT}) {name}({", ".join(params)})\n{{')
+    if cfg.SIG:
+        L += start_signal_lines()
     L.append(f'  __shared__ __attribute__((aligned(1024))) {et} lds[{NS * SLOT + 64}];')
     L.append('  const int tid = threadIdx.x, lane = tid & 63;')
     L.append('  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);')

@@ -481,9 +481,12 @@ class HipStencilKernel:
             rt.launch(fn, (grid,), (block,), packed, stream)
         return xb
 
-    def prepare(self, halos=None, force_schedule=None, z_range=None, x_border=False, z_limits=None, **kwargs):
+    def prepare(self, halos=None, force_schedule=None, z_range=None, x_border=False, z_limits=None,
+                start_signal=False, **kwargs):
         """Everything of a launch but the launch: ``(function, grid, block, packed args, x_border done,
-        device)``, or None for an empty domain (arguments as for ``__call__``)."""
+        device)``, or None for an empty domain (arguments as for ``__call__``). ``start_signal=True`` (march
+        schedules, the z-slab interior): the kernel takes a signal word and a value after its extents, both zero in
+        the packed arguments (no store) — the caller patches them at ``last_plan.sig_offsets``."""
         torch = _torch()
         ir = self.ir
         if self._soa:
@@ -531,14 +534,14 @@ class HipStencilKernel:
         align = tuple(_align_class(p) for p in ptrs + hptrs)
         key = (force_schedule, bool(x_border), shape, strides, align,
                tuple(h.numel() if h is not None else -1 for h in halo_list), _zkey(z_range),
-               tuple(z_limits) if z_limits is not None else None, device)
+               tuple(z_limits) if z_limits is not None else None, device) + (('sig',) if start_signal else ())
         plan = self._plans.get(key)
         if plan is None:
             if z_limits is not None:
                 if not ir.ndim == 3 or not 0 <= int(z_limits[0]) <= int(z_limits[1]) <= shape[0]:
                     raise ValueError(f'z_limits {z_limits} must lie in [0, {shape[0]}] of a 3-D kernel')
             plan = self._make_plan(tensors, halo_list, shape, device, contiguous, force_schedule, z_range, x_border,
-                                   z_limits)
+                                   z_limits, start_signal)
             self._plans[key] = plan
         self.last_variant = plan.variant
         self.last_plan = plan
@@ -573,19 +576,19 @@ class HipStencilKernel:
         return kwargs
 
     def _make_plan(self, tensors, halo_list, shape, device, contiguous, force_schedule, z_range, x_border=False,
-                   z_limits=None):
+                   z_limits=None, start_signal=False):
         torch = _torch()
         ir = self.ir
         sched = force_schedule or self.schedule()
         if sched != 'generic' and not contiguous:
             sched = 'generic'
-        if (halo_list or z_range is not None or z_limits is not None) and sched != 'march':
-            raise ValueError('halo planes / z ranges are only supported by the march schedule')
+        if (halo_list or z_range is not None or z_limits is not None or start_signal) and sched != 'march':
+            raise ValueError('halo planes / z ranges / start signals are only supported by the march schedule')
         with torch.cuda.device(device):
             if sched == 'pointwise':
                 return self._plan_pointwise(tensors, shape, device)
             if sched == 'march':
-                return self._plan_march(tensors, halo_list, shape, device, z_range, x_border, z_limits)
+                return self._plan_march(tensors, halo_list, shape, device, z_range, x_border, z_limits, start_signal)
             return self._plan_generic(tensors, shape, device)
 
     def _scalar_kind(self):
@@ -740,7 +743,8 @@ class HipStencilKernel:
         return dict(Z=Z, Y=Y, X=X, zlo=zlo, zhi=zhi, ylo=ylo, yhi=yhi, xlo=xlo, xhi=xhi, zc=zc, zstep=zc,
                     ntx=ntx, nty=nty, grid=nt * nchunks)
 
-    def _plan_march(self, tensors, halo_list, shape, device, z_range, x_border=False, z_limits=None):
+    def _plan_march(self, tensors, halo_list, shape, device, z_range, x_border=False, z_limits=None,
+                    start_signal=False):
         torch = _torch()
         ir = self.ir
         ve = self._vec_elems()
@@ -826,6 +830,8 @@ class HipStencilKernel:
                     g0['X'] % (16 // esize):                          # a partial last chunk per row
                 cfg = MarchConfig(**{**cfg.__dict__, 'BMASK': True,
                                      'BXW': g0['xlo'] == 0 and g0['xhi'] == g0['X'] and not cfg.XB})
+        if start_signal:
+            cfg = MarchConfig(**{**cfg.__dict__, 'SIG': True})
         variant = ('march', cfg)
         fn = self.function(variant, device)
         ws = ws_geometry(ir, cfg)
@@ -845,11 +851,18 @@ class HipStencilKernel:
             raise ValueError('field extent too large for the march schedule')
         statics = [int(geo[k]) for k in ('Z', 'Y', 'X', 'zlo', 'zhi', 'ylo', 'yhi', 'xlo', 'xhi', 'zc', 'zstep', 'ntx',
                                           'nty')]
-        kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics) + \
-            [self._scalar_kind()] * len(ir.scalars)
+        kinds = ['ptr'] * (len(tensors) + 2 * len(stencil)) + ['i32'] * len(statics)
+        if cfg.SIG:
+            kinds += ['ptr', 'u32']                     # the start signal: word and value, patched by the caller
+            statics += [0, 0]
+        kinds += [self._scalar_kind()] * len(ir.scalars)
         block = ws['block'] if ws else (band_geometry(cfg.BX, cfg.BTY, cfg.BAND, cfg.D, esize, cfg.BPAD, cfg.BREG, cfg.BFREE)['NT'] if cfg.BAND else
                                         cfg.NT)
-        return _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics, xb=cfg.XB, block=block)
+        plan = _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics, xb=cfg.XB, block=block)
+        if cfg.SIG:
+            i = len(tensors) + 2 * len(stencil) + 13
+            plan.sig_offsets = (plan.offsets[i], plan.offsets[i + 1])
+        return plan
 
 
 class _Plane:
@@ -934,6 +947,7 @@ class _Plan:
         self.n_ptr = n_ptr
         self.n_halo = n_halo
         self.statics = list(statics)
+        self.sig_offsets = None          # (byte offset of the start-signal word, of its value): SIG launches
 
     def scalar_slots(self, n):
         """``(byte offset, is f64)`` of the last ``n`` arguments (the kernel's scalar parameters)."""

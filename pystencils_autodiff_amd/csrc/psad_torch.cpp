@@ -43,6 +43,7 @@ struct Launch {
     std::string args;          // packed template; pointer i at byte 8*i
     std::vector<int64_t> slot; // pointer i <- table[slot[i]]
     std::vector<int64_t> s_off, s_f64, s_idx;   // scalar j at byte s_off[j] (f64 or f32) <- scalars[s_idx[j]]
+    int64_t sig_ptr_off = -1, sig_val_off = -1; // start signal (hip_emitter SIG): word pointer and value, or -1
 };
 
 struct Alloc {
@@ -88,7 +89,7 @@ at::Tensor allocate(const Alloc& a, int device) {
 bool aligned(const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 31u) == 0; }
 
 void launch_on(const Launch& l, const std::vector<at::Tensor>& table, const std::vector<double>& scalars,
-               hipStream_t stream);
+               hipStream_t stream, uint32_t* sig = nullptr, uint32_t sig_value = 0);
 
 void launch(const Launch& l, const std::vector<at::Tensor>& table, const std::vector<double>& scalars,
             int device) {
@@ -98,8 +99,13 @@ void launch(const Launch& l, const std::vector<at::Tensor>& table, const std::ve
 }
 
 void launch_on(const Launch& l, const std::vector<at::Tensor>& table, const std::vector<double>& scalars,
-               hipStream_t stream) {
+               hipStream_t stream, uint32_t* sig, uint32_t sig_value) {
     std::string args = l.args;
+    if (sig != nullptr) {       // the launch stores sig_value to *sig when it starts (its template holds nullptr)
+        TORCH_CHECK(l.sig_ptr_off >= 0 && l.sig_val_off >= 0, "psad: launch without a start-signal slot");
+        std::memcpy(&args[l.sig_ptr_off], &sig, sizeof(sig));
+        std::memcpy(&args[l.sig_val_off], &sig_value, sizeof(sig_value));
+    }
     for (size_t i = 0; i < l.slot.size(); ++i) {
         void* p = table[l.slot[i]].data_ptr();
         std::memcpy(&args[8 * i], &p, sizeof(p));
@@ -195,10 +201,18 @@ struct Exchange {
     mutable uint32_t seq = 0;
     mutable hipStream_t sig_stream = nullptr;   // (torch's default stream IS nullptr: sig_bound says whether it is set)
     mutable bool sig_bound = false;
+    // compute -> halo by event record + wait (a marker packet on the compute queue) and halo -> compute by the
+    // stream memory operation (PSAD_SLAB_SYNC=mixed): the compute queue then carries one ROCclr stream-op kernel per
+    // sweep instead of two
+    bool faces_by_event = false;
+    // the interior launch writes the compute -> halo signal itself (default; PSAD_SLAB_START_SIG=0: a
+    // hipStreamWriteValue32 on the compute stream)
+    bool start_sig = true;
 };
 
 std::mutex g_sweep_mutex;               // serialises the enqueue of exchanging sweeps (counter order = stream order)
 std::atomic<int64_t> g_event_sweeps{0};  // exchanging sweeps ordered by events (tests)
+std::atomic<int64_t> g_start_sig_sweeps{0};   // exchanging sweeps whose interior launch wrote the signal (tests)
 
 struct Sweep {
     Exchange ex;
@@ -245,10 +259,16 @@ void run_sweep(const Sweep& w, const std::vector<at::Tensor>& table, const std::
         ex.sig_bound = true;
         seq = ++ex.seq;
     }
-    if (sig) {
-        hip_ok(hipStreamWriteValue32(cur, ex.sig, seq, 0), "hipStreamWriteValue32");
+    // the interior launch stores seq to the signal word when it starts (every earlier launch of the compute stream
+    // has completed then): the compute queue carries no stream-memory write kernel for this ordering
+    const bool start_sig = sig && !ex.faces_by_event && w.has_inner && w.inner.sig_ptr_off >= 0 && ex.start_sig;
+    if (sig && !ex.faces_by_event) {
+        if (!start_sig) hip_ok(hipStreamWriteValue32(cur, ex.sig, seq, 0), "hipStreamWriteValue32");
         hip_ok(hipStreamWaitValue32(ex.stream, ex.sig, seq, hipStreamWaitValueGte, 0xffffffffu),
                "hipStreamWaitValue32");
+    } else if (sig) {
+        hip_ok(hipEventRecord(ex.ev_faces, cur), "hipEventRecord");           // the faces are final
+        hip_ok(hipStreamWaitEvent(ex.stream, ex.ev_faces, 0), "hipStreamWaitEvent");
     } else if (n) {
         g_event_sweeps.fetch_add(1);
         hip_ok(hipEventRecord(ex.ev_faces, cur), "hipEventRecord");           // the faces are final
@@ -270,7 +290,14 @@ void run_sweep(const Sweep& w, const std::vector<at::Tensor>& table, const std::
     }
     if (n && w.faces_on_halo)                                                // faces beside the interior
         for (const auto& f : w.faces) launch_on(f, table, scalars, ex.stream);
-    if (w.has_inner) launch(w.inner, table, scalars, device);                // interior overlaps the exchange
+    if (w.has_inner) {                                                       // interior overlaps the exchange
+        if (start_sig) {
+            g_start_sig_sweeps.fetch_add(1);
+            launch_on(w.inner, table, scalars, cur, ex.sig, seq);
+        }
+        else
+            launch(w.inner, table, scalars, device);
+    }
     if (sig) {
         hip_ok(hipStreamWriteValue32(ex.stream, ex.sig_halo, seq, 0), "hipStreamWriteValue32");
         hip_ok(hipStreamWaitValue32(cur, ex.sig_halo, seq, hipStreamWaitValueGte, 0xffffffffu),
@@ -392,9 +419,21 @@ int64_t register_plan(const std::string& name, int64_t device, std::vector<std::
 
 // (fn, grid, block, args, slot, scal) → Launch
 Launch launch_from(const py::tuple& t, int64_t n_scalars) {
-    TORCH_CHECK(t.size() == 6, "psad: launch spec is (fn, grid, block, args, slot, scal)");
-    return make_launch(t[0].cast<uint64_t>(), t[1].cast<int64_t>(), t[2].cast<int64_t>(), t[3].cast<py::bytes>(),
-                       t[4].cast<std::vector<int64_t>>(), t[5].cast<std::vector<std::vector<int64_t>>>(), n_scalars);
+    TORCH_CHECK(t.size() == 6 || t.size() == 7, "psad: launch spec is (fn, grid, block, args, slot, scal[, sig])");
+    Launch l = make_launch(t[0].cast<uint64_t>(), t[1].cast<int64_t>(), t[2].cast<int64_t>(), t[3].cast<py::bytes>(),
+                           t[4].cast<std::vector<int64_t>>(), t[5].cast<std::vector<std::vector<int64_t>>>(), n_scalars);
+    if (t.size() == 7) {
+        const auto sig = t[6].cast<std::vector<int64_t>>();     // (word offset, value offset) or empty
+        TORCH_CHECK(sig.empty() || (sig.size() == 2 && sig[0] >= 8 * static_cast<int64_t>(l.slot.size()) &&
+                                    sig[0] % 8 == 0 && sig[0] + 8 <= static_cast<int64_t>(l.args.size()) &&
+                                    sig[1] >= sig[0] + 8 && sig[1] + 4 <= static_cast<int64_t>(l.args.size())),
+                    "psad: start-signal offsets out of range");
+        if (!sig.empty()) {
+            l.sig_ptr_off = sig[0];
+            l.sig_val_off = sig[1];
+        }
+    }
+    return l;
 }
 
 // inner (launch spec or None), faces [launch spec], exchange (slot, last_off, recv_lo, recv_hi, bytes, peer_lo,
@@ -452,6 +491,9 @@ Sweep sweep_from(const py::object& inner, const py::list& faces, const py::tuple
             hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
             w.ex.sig = static_cast<uint32_t*>(p);
             w.ex.sig_halo = static_cast<uint32_t*>(q);
+            w.ex.faces_by_event = sy != nullptr && std::string(sy) == "mixed";
+            const char* ss = std::getenv("PSAD_SLAB_START_SIG");
+            w.ex.start_sig = !(ss != nullptr && std::string(ss) == "0");
         }
     }
     return w;
@@ -536,6 +578,8 @@ PYBIND11_MODULE(_psad_torch, m) {
     });
     m.def("num_event_sweeps", []() { return g_event_sweeps.load(); },
           "exchanging slab sweeps ordered by event record + wait (PSAD_SLAB_SYNC=event, or another compute stream)");
+    m.def("num_start_signal_sweeps", []() { return g_start_sig_sweeps.load(); },
+          "exchanging slab sweeps whose interior launch signalled the halo stream itself (tests)");
     m.def("set_debug_poison", [](bool on) { g_poison.store(on); },
           "fill the outputs allocated uninitialised with NaN (tests: a kernel that leaves cells unwritten shows)");
     m.def("num_plans", []() {

@@ -707,8 +707,11 @@ class _NativeSlab:
                 sn = [sc.name for sc in compiled.ir.scalars]
                 slots = [[off, int(f64), scalar_names.index(n)]
                          for (off, f64), n in zip(compiled.last_plan.scalar_slots(len(sn)), sn)]
-                return (int(fn), int(grid), int(block), bytes(packed), [table.index(n) for n in fnames], slots)
-            inner_l = resolve(z_range=inner) if inner else None
+                sig = list(compiled.last_plan.sig_offsets or ())
+                return (int(fn), int(grid), int(block), bytes(packed), [table.index(n) for n in fnames], slots, sig)
+            # the interior launch signals its own start (the halo stream's exchange waits for it): no stream-memory
+            # write kernel on the compute queue (csrc/psad_torch.cpp run_sweep)
+            inner_l = resolve(z_range=inner, start_signal=True) if inner else None
             if inner and inner_l is None:
                 return None
             if len(faces) == 2 and faces[0][1] - faces[0][0] == faces[1][1] - faces[1][0]:

@@ -608,6 +608,7 @@ def test_zslab_native_node_loopback(builder_name, shape, monkeypatch):
         z.warm_exchange(u=tu, diffout=td)
         fn = z.autograd_function()
         n0 = _psad_torch.num_slab_plans()
+        s0 = _psad_torch.num_start_signal_sweeps()
         res = []
         for native in ('1', '1', '0'):
             monkeypatch.setenv('PSAD_NATIVE_SLAB', native)
@@ -618,6 +619,9 @@ def test_zslab_native_node_loopback(builder_name, shape, monkeypatch):
             torch.cuda.synchronize()
             res.append((o.detach().clone(), uu.grad.clone()))
         assert _psad_torch.num_slab_plans() == n0 + 1
+        # slabs with interior planes: each native sweep's interior launch wrote the halo stream's signal itself (no
+        # stream-memory write kernel on the compute queue); a slab of faces only keeps hipStreamWriteValue32
+        assert _psad_torch.num_start_signal_sweeps() - s0 == (4 if shape[0] > 2 else 0)
         assert torch.equal(res[0][0], res[2][0]) and torch.equal(res[0][1], res[2][1])
         assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
