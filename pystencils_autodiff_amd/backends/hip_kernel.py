@@ -230,7 +230,7 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             cfg.update(WS=True, CX=4, NR=8 if ws0['kind'] == 'h' else 4, D=4, ZMIN=8, ZMAX=128, BLK=256)
             star_ws = True
     ring_ws = False
-    if ir.ndim == 3 and not zsum_ok and not ir.has_index_dims:
+    if ir.ndim == 3 and not zsum_ok:
         # stencils not linear off the centre plane (products / functions of neighbour taps): the plane ring fed by
         # an LDS-DMA loader wave, 2 planes in flight, the widest tile whose ring fits the LDS
         for cx, nr in RING_WS_TILES:
@@ -242,9 +242,9 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
                 break
     if ir.ndim == 2:
         cfg.update(CX=4, WX=1, NR=4, VIEW2D='yx', NT_STORE=False)   # 256×16 tiles (4096²: 0.024 ms, 5.6 TB/s)
-    if ir.has_index_dims:
-        # vector fields (components interleaved in the plane image): only the zsum schedule handles them;
-        # narrower tiles keep the image (TX + 2H)·C elements wide
+    if ir.has_index_dims and not ring_ws:
+        # vector fields (components interleaved in the plane image) linear off the centre plane: the zsum schedule;
+        # narrower tiles keep the image (TX + 2H)·C elements wide (the plane ring picked its tile above)
         from .hip_emitter import ncomp
         cmax = max([ncomp(f) for f in ir.stencil_fields] + [1])
         cfg.update(ZSUM=True, PK=False, AR=False)
@@ -382,9 +382,13 @@ class HipStencilKernel:
                 len({f.dtype for f in ir.fields}) == 1:
             if ir.has_index_dims:
                 # vector fields: the zsum schedule (components interleaved in the plane image) when the
-                # stencil is linear off the centre plane, else one thread per cell
+                # stencil is linear off the centre plane, the LDS-DMA plane ring (components interleaved the same
+                # way) for other 3-D stencils, else one thread per cell
                 probe = MarchConfig(VE=self._vec_elems(), ZSUM=True)
-                return 'march' if ir.stencil_fields and zsum_plan(ir, probe) is not None else 'generic'
+                if ir.stencil_fields and zsum_plan(ir, probe) is not None:
+                    return 'march'
+                ring = self._march_cfg(self._vec_elems())
+                return 'march' if ir.stencil_fields and ring.WS and not ring.ZSUM else 'generic'
             return 'march'
         return 'generic'
 
@@ -808,7 +812,7 @@ class HipStencilKernel:
         if halo_list and ir.ndim == 2 and cfg.VIEW2D == 'yx':
             cfg = MarchConfig(**{**cfg.__dict__, 'VIEW2D': 'zy'})
         from .hip_emitter import ncomp
-        if ir.has_index_dims and not cfg.ZSUM:
+        if ir.has_index_dims and not cfg.ZSUM and not (cfg.WS and ws_geometry(ir, cfg)):
             if halo_list or z_range is not None or z_limits is not None:
                 raise ValueError('vector-field kernels take halo planes / z ranges only in the zsum schedule')
             return self._plan_generic(tensors, shape, device)
@@ -818,6 +822,11 @@ class HipStencilKernel:
             # planes beyond the loader's 32-bit buffer offsets: register-prefetch form of the same schedule
             # (never with XM: its rows straddle, which only the loader's zero fill repairs)
             assert not cfg.XM
+            if ir.has_index_dims and not cfg.ZSUM:
+                # (the register-prefetch ring takes scalar fields only)
+                if halo_list or z_range is not None or z_limits is not None:
+                    raise ValueError('vector-field kernels beyond 32-bit plane offsets take no halo planes / z ranges')
+                return self._plan_generic(tensors, shape, device)
             cfg = ws_fallback_config(cfg)
         xlo, xhi = ir.iteration_bounds(shape)[-1]
         if x_border and cfg.ZSUM and (xlo > 0 or xhi < shape[-1]) and \

@@ -44,11 +44,15 @@ def graph_step(fn, ins, grads, steps):
 
 
 def graph_sweeps(fn, ins, grads, K=20, reps=30):
-    """Per-sweep GPU time of a small op without the host in it: K forward applies captured in one HIP graph, and K
-    (apply + backward) steps in another, each replayed ``reps`` times between two HIP events on the stream. The
-    forward sweep = the first graph / K, the adjoint = (second − first) / K. For configs whose kernels take tens of
-    µs, events around each eager apply / backward time the host's launch latency as much as the kernel (BASELINE
-    config 2 measured 0.024–0.037 ms per sweep from run to run that way)."""
+    """Per-sweep GPU time of a small op without the host in it: K forward applies captured in one HIP graph, K
+    backward passes of ONE eager forward (``autograd.grad(..., retain_graph=True)``) in a second, each replayed
+    ``reps`` times between two HIP events on the stream: forward = the first graph / K, adjoint = the second / K —
+    each sweep timed on its own, both writing K fresh output blocks per replay. (Until round 6 the adjoint was
+    (K apply + backward steps − K applies) / K: that charged the adjoint with what the forward loses when the
+    adjoint's writes share the Infinity Cache with it — config 2's "adjoint 7–12 % slower than the forward".)
+    For configs whose kernels take tens of µs, events around each eager apply / backward time the host's launch
+    latency as much as the kernel (BASELINE config 2 measured 0.024–0.037 ms per sweep from run to run that way,
+    VERDICT r04 item 5). Returns (fwd, adjoint, adjoint by the old subtraction)."""
     import torch
     static = [t.detach().clone().requires_grad_(True) for t in ins]
     s = torch.cuda.Stream()
@@ -59,13 +63,19 @@ def graph_sweeps(fn, ins, grads, K=20, reps=30):
             for t in static:
                 t.grad = None
     torch.cuda.current_stream().wait_stream(s)
-    gf, gs = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    gf, gs, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
     with torch.cuda.graph(gf):
         keep = [fn.apply(*static) for _ in range(K)]
     with torch.cuda.graph(gs):
         keep2 = [torch.autograd.grad(list(fn.apply(*static)), static, grads) for _ in range(K)]
+    with torch.cuda.stream(s):
+        outs0 = list(fn.apply(*static))             # one eager forward: its autograd graph is replayed K times below
+        torch.autograd.grad(outs0, static, grads, retain_graph=True)
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(gb):
+        keep3 = [torch.autograd.grad(outs0, static, grads, retain_graph=True) for _ in range(K)]
     out = []
-    for g in (gf, gs):
+    for g in (gf, gs, gb):
         for _ in range(3):
             g.replay()
         torch.cuda.synchronize()
@@ -76,8 +86,8 @@ def graph_sweeps(fn, ins, grads, K=20, reps=30):
         b.record()
         torch.cuda.synchronize()
         out.append(a.elapsed_time(b) / (reps * K))
-    del keep, keep2
-    return out[0], out[1] - out[0]
+    del keep, keep2, keep3, outs0
+    return out[0], out[2], out[1] - out[0]
 
 
 SETTLE_MS = 400.0
@@ -161,7 +171,7 @@ def run(name, builder, shape, dtype, bh, nin, steps=20, warmup=3, bytes_fwd=None
     b_ev = sorted(b.elapsed_time(c) for _, b, c in ev)[len(ev) // 2]
     # small configs: the per-sweep GPU time from graph replays (events around eager calls time the host too)
     small = cells <= 1 << 26
-    f_ms, b_ms = graph_sweeps(fn, ins, grads) if small else (f_ev, b_ev)
+    f_ms, b_ms, b_sub = graph_sweeps(fn, ins, grads) if small else (f_ev, b_ev, None)
     res = {'config': name, 'shape': list(shape), 'dtype': str(dtype).replace('torch.', ''),
            'mcells_per_s': round(cells * steps / el / 1e6, 1), 'ms_per_step': round(el / steps * 1e3, 4),
            'mcells_per_s_autograd_1thread': round(cells * steps / el_st / 1e6, 1),
@@ -170,7 +180,8 @@ def run(name, builder, shape, dtype, bh, nin, steps=20, warmup=3, bytes_fwd=None
                'ms_per_step_hip_graph': round(el_graph * 1e3, 4)} if el_graph else {}),
            'fwd_ms': round(f_ms, 4), 'bwd_ms': round(b_ms, 4),
            'sweep_timing': 'hip_graph_replay' if small else 'hip_events_per_call',
-           **({'fwd_ms_events': round(f_ev, 4), 'bwd_ms_events': round(b_ev, 4)} if small else {}),
+           **({'fwd_ms_events': round(f_ev, 4), 'bwd_ms_events': round(b_ev, 4),
+               'bwd_ms_step_minus_fwd': round(b_sub, 4)} if small else {}),
            'fwd_schedule': op.forward_ast_gpu.compile().last_variant[0],
            'bwd_schedule': op.backward_ast_gpu.compile().last_variant[0]}
     if bytes_fwd:

@@ -331,3 +331,111 @@ def test_varcoef_ring_none_mode_and_time_constant_gpu(mode):
         np.testing.assert_allclose(out.double().cpu().numpy(), ref['out'], rtol=1e-5, atol=1e-5)
         np.testing.assert_allclose(du.double().cpu().numpy(), refb['diffu'], rtol=1e-5, atol=1e-5)
         np.testing.assert_allclose(dk.double().cpu().numpy(), refb['diffk'], rtol=1e-5, atol=1e-5)
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# nonlinear stencils on vector fields (index dimension, components fastest): the LDS-DMA plane ring with the
+# components interleaved in each plane image (as the zsum schedule keeps them) — reference vector-field TF-MAD branch
+# _autodiff.py:125-152 (only the last component's adjoint assignment is kept), tests/test_tfmad.py:381-401
+E3 = [(1, 0, 0), (0, 1, 0), (0, 0, 1)]
+M3 = [(-1, 0, 0), (0, -1, 0), (0, 0, -1)]
+
+
+def _advection(dts='float32', C=3):
+    """``out(c) = u(c) − α Σ_d u(d)·(u[+e_d](c) − u[−e_d](c))/2`` (scripts/probes/vector_nonlinear.py)."""
+    u, out = ps.fields(f'u({C}), out({C}): {dts}[3d]')
+    return ps.AssignmentCollection({out.center(c): u.center(c) - 0.05 * sp.Add(
+        *[u.center(d % C) * (u[E3[d]](c) - u[M3[d]](c)) / 2 for d in range(3)]) for c in range(C)})
+
+
+def _adv_oracle(op, bh, un, dn):
+    """(out, diffu) of the op's assignments and their Σ|terms|, float64 numpy, fields [Z, Y, X, C]."""
+    ref = {**OE.evaluate(op.forward_assignments, {'u': un}, boundary_handling=bh),
+           **OE.evaluate(op.backward_assignments, {'u': un, 'diffout': dn}, boundary_handling=bh)}
+    ab = {**OE.evaluate(_abs_terms(op.forward_assignments), {'u': np.abs(un)}, boundary_handling=bh),
+          **OE.evaluate(_abs_terms(op.backward_assignments), {'u': np.abs(un), 'diffout': np.abs(dn)},
+                        boundary_handling=bh)}
+    return ref, ab
+
+
+def test_vector_nonlinear_takes_the_plane_ring():
+    """Schedule selection (no GPU): the advection forward and its TF-MAD adjoint are not linear off the centre plane,
+    so not zsum; they take the LDS-DMA plane ring with interleaved components (they took one thread per cell before
+    round 6), and the emitted sources compile for gfx950."""
+    from pystencils_autodiff_amd.backends import hip_runtime as rt
+    from pystencils_autodiff_amd.backends.hip_kernel import HipStencilKernel
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    op = pa.AutoDiffOp(_advection(), boundary_handling='zeros')
+    assert [str(a.lhs) for a in op.backward_assignments.main_assignments] == ['\\hat{u}[0,0,0,2]']   # the quirk
+    for asg in (op.forward_assignments, op.backward_assignments):
+        hk = HipStencilKernel(StencilKernel(asg, boundary_handling='zeros', function_name='advr', target='gpu'))
+        assert hk.schedule() == 'march'
+        cfg = hk._march_cfg(4, (64, 64, 256))
+        assert cfg.WS and not cfg.ZSUM, cfg
+        src = hk.source(('march', cfg))[0]
+        assert 'LDS-DMA loader wave' in src and len(rt.compile_hip(src)) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape', [(17, 33, 45), (9, 20, 128), (40, 64, 256), (5, 7, 3), (33, 50, 130),
+                                   (21, 30, 132), (70, 9, 264)])
+@pytest.mark.parametrize('bh', ['zeros', None])
+def test_vector_advection_ring_gpu_vs_oracle(shape, bh):
+    """The advection op through the drop-in Function on the vector plane ring, forward and TF-MAD adjoint vs the
+    float64 oracle, cell by cell (``check``: 1e-6·|ref| + 32·2⁻²⁴·Σ|terms|), both boundary modes; the adjoint's
+    first two components are the zeros of the reference's last-component quirk (``_autodiff.py:138-152``)."""
+    op = pa.AutoDiffOp(_advection(), boundary_handling=bh)
+    g = torch.Generator().manual_seed(sum(shape))
+    u = (torch.rand(shape + (3,), generator=g, dtype=torch.float64) * 2 - 1).float()
+    d = (torch.rand(shape + (3,), generator=g, dtype=torch.float64) * 2 - 1).float()
+    fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    uu = u.cuda().requires_grad_(True)
+    (out,) = fn.apply(uu)
+    out.backward(d.cuda())
+    torch.cuda.synchronize()
+    fk, bk = op.forward_ast_gpu.compile(), op.backward_ast_gpu.compile()
+    for k in (fk, bk):
+        if shape[2] % 4 == 0:             # rows of whole 16-byte pieces (the others: one thread per cell)
+            assert k.last_variant[0] == 'march' and k.last_variant[1].WS and not k.last_variant[1].ZSUM, k.last_variant
+    ref, ab = _adv_oracle(op, bh, u.double().numpy(), d.double().numpy())
+    check(out, ref['out'], ab['out'], False, f'{shape} {bh} out')
+    check(uu.grad, ref['diffu'], ab['diffu'], False, f'{shape} {bh} diffu')
+    assert not uu.grad[..., :2].any()
+
+
+@pytest.mark.gpu
+def test_vector_advection_ring_tilings_and_slab_gpu():
+    """Other ring tilings of the vector advection (8 compute waves, depth 1 and 3) and the z-slab launch pattern
+    (interior z range, then both faces in one launch reading halo planes in place) bitwise equal to one full launch."""
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    from pystencils_autodiff_amd.zslab import ZSlabOp
+    op = pa.AutoDiffOp(_advection(), boundary_handling='zeros')
+    shape = (23, 37, 200)
+    g = torch.Generator().manual_seed(4)
+    u = (torch.rand(shape + (3,), generator=g) * 2 - 1).cuda()
+    ref, ab = _adv_oracle(op, 'zeros', u.double().cpu().numpy(), np.zeros(shape + (3,)))
+    for params in (dict(WS=1, NW=8, CX=2, NR=1, D=2), dict(WS=1, CX=1, NR=4, D=1), dict(WS=1, CX=2, NR=2, D=3)):
+        k = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='advt', target='gpu',
+                          gpu_indexing_params=params).compile()
+        out = torch.full_like(u, float('nan'))
+        k(u=u, out=out)
+        torch.cuda.synchronize()
+        assert k.last_variant[1].WS and not k.last_variant[1].ZSUM
+        check(out, ref['out'], ab['out'], False, f'{params} out')
+    k = op.forward_ast_gpu.compile()
+    full = torch.zeros_like(u)
+    k(u=u, out=full)
+    outs = []
+    for a, b in [(0, 9), (9, 16), (16, 23)]:
+        sl = u[a:b].contiguous()
+        o = torch.zeros_like(sl)
+        lo = u[a - 1:a].contiguous() if a > 0 else None
+        hi = u[b:b + 1].contiguous() if b < shape[0] else None
+        inner, faces = ZSlabOp._launches(b - a, 1, (0, b - a))
+        if inner:
+            k(u=sl, out=o, z_range=inner)
+        ZSlabOp._launch_faces(k, {'u': (lo, hi)}, faces, None, {'u': sl, 'out': o})
+        assert k.last_variant[1].WS and not k.last_variant[1].ZSUM
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(outs), full)
