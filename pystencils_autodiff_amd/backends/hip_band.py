@@ -582,6 +582,34 @@ def emit_band(ir, name, cfg):
                                 B.append(f'{ind}{acc} = {acc} + {term};')
         return B
 
+    # the partial last chunk stored as one shifted 16-byte chunk (BTAIL): needs a left neighbour chunk of the same row in
+    # the same wave for every row group's tail lane (never lane 0 of a wave)
+    tail_sb = ((VE - X % VE) % VE) * es                 # bytes the row's last chunk lacks
+    tail_shift = bool(cfg.BTAIL) and partial and cfg.BXW and CPR >= 2 and \
+        all((grp * CPR + CPR - 1) % 64 != 0 for grp in range(G))
+
+    def tail_shift_lines(src, dst):
+        """``dst`` = the 16 bytes ending at the row's end: the left lane's last ``tail_sb`` bytes, then ``src``'s
+        first 16 - tail_sb bytes (dword selects, and v_alignbyte when the shift is not whole dwords)."""
+        q, b = tail_sb // 4, tail_sb % 4
+        k0 = 4 - q - (1 if b else 0)                      # first dword of the result in (left lane | own)
+        need = sorted({k0 + i for i in range(4)} | ({k0 + i + 1 for i in range(4)} if b else set()))
+        out = []
+        seq = {}
+        for k in need:
+            if k < 4:                                     # the left lane's dword k (wave_shr:1)
+                out.append(f'const unsigned nb{k} = __builtin_amdgcn_update_dpp(0u, {src}.{"xyzw"[k]}, 0x138, 0xf, 0xf, '
+                           'false);')
+                seq[k] = f'nb{k}'
+            else:
+                seq[k] = f'{src}.{"xyzw"[k - 4]}'
+        if b:
+            parts = [f'__builtin_amdgcn_alignbyte({seq[k0 + i + 1]}, {seq[k0 + i]}, {4 - b}u)' for i in range(4)]
+        else:
+            parts = [seq[k0 + i] for i in range(4)]
+        out.append(f'const u32x4 {dst} = {{{", ".join(parts)}}};')
+        return out
+
     def stores(ind, si, sp, fld, rows=None):
         B = [f'{ind}{{',
              f'{ind}  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc('
@@ -603,7 +631,16 @@ def emit_band(ir, name, cfg):
                 # half) at the row offset while its 16-byte store is dropped, every other lane the reverse
                 ro = f'((rowok & {1 << o}u) ? sofs + {o * X * es}u : 0x7ffffff0u)'
                 B.append(f'{ind}  {{ const {vt} ov = {{{vals}}}; const unsigned ro = {ro};')
-                if partial:
+                if partial and tail_shift:
+                    # the row's partial last chunk as ONE 16-byte store of the row's last VE cells, shifted left by
+                    # the sb bytes the chunk lacks: the first of them are the left lane's last cells (DPP wave_shr:1,
+                    # the same row; that lane stores the same values there), so the row takes one store instruction
+                    # instead of three (16-byte, then dword and half stores that drop 63 lanes each)
+                    B.append(f'{ind}    const u32x4 ow = __builtin_bit_cast(u32x4, ov);')
+                    B += [f'{ind}    {ln}' for ln in tail_shift_lines('ow', 'tw')]
+                    B.append(f'{ind}    __builtin_amdgcn_raw_buffer_store_b128(xtail ? tw : ow, ors, xtail ? ro - {tail_sb}u : ro, '
+                             f'0, 2);')
+                elif partial:
                     c = 'xyzw'
                     B.append(f'{ind}    const u32x4 ow = __builtin_bit_cast(u32x4, ov);')
                     B.append(f'{ind}    __builtin_amdgcn_raw_buffer_store_b128(ow, ors, xtail ? 0x7ffffff0u : ro, 0, 2);')

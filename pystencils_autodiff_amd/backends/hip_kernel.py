@@ -73,7 +73,7 @@ RING_WS_TILES = ((4, 4), (4, 2), (2, 4), (2, 2), (1, 4), (1, 2), (1, 1))
 # describe a one-thread-per-cell launch these schedules do not have, so they are accepted and ignored. Upper-case
 # keys are this layer's tile parameters; an unknown one is a typo and raises.
 TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
-             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BPAD', 'BZF', 'BREG', 'BNT', 'BFREE',
+             'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BPAD', 'BZF', 'BREG', 'BNT', 'BFREE', 'BTAIL',
              'SFAST')
 # Ablation knobs that make results WRONG (timing probes: ``BABL``). They are not tile keys — ``gpu_indexing_params`` and
 # ``PSAD_MARCH`` reject them — and reach the planner only through this dict, which nothing on the op's path writes:
@@ -165,7 +165,7 @@ def _band_config(ir, ve, shape, over):
     return MarchConfig(VE=ve, BAND=R, BTY=TY, BX=X, D=D, ZSUM=True, NT_STORE=True, ZMIN=zc,
                        ZMAX=zmax, BLK=int(over.get('BLK', 512)), MAP=int(over.get('MAP', 0)),
                        BTRIM=btrim, BEDGE=int(over.get('BEDGE', 1)), BPAD=pad, BZF=int(over.get('BZF', 1)), BREG=reg,
-                       BNT=int(over.get('BNT', 2)), BFREE=int(over.get('BFREE', 0)),
+                       BNT=int(over.get('BNT', 2)), BFREE=int(over.get('BFREE', 0)), BTAIL=int(over.get('BTAIL', 1)),
                        BABL=int(PROBE_KNOBS.get('BABL', 0)))
 
 

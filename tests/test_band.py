@@ -281,7 +281,8 @@ def test_band_unaligned_vs_oracle(case_shape, bh):
 @pytest.mark.gpu
 @pytest.mark.parametrize('case_shape', UNALIGNED, ids=lambda c: f'{c[0]}-{c[1][2]}')
 @pytest.mark.parametrize('bh', ['zeros', None])
-@pytest.mark.parametrize('knob', [{'BZF': 0}, {'BREG': 1}, {'BFREE': 2}], ids=['BZF0', 'BREG1', 'BFREE2'])
+@pytest.mark.parametrize('knob', [{'BZF': 0}, {'BREG': 1}, {'BFREE': 2}, {'BTAIL': 0}],
+                         ids=['BZF0', 'BREG1', 'BFREE2', 'BTAIL0'])
 def test_band_unaligned_variants_vs_oracle(case_shape, bh, knob):
     """Unaligned rows, forward and adjoint vs the oracle: ``BZF=0`` (no loader zero fill past each row end; the
     compute lanes of a row's last chunk zero its first element past X in registers) and ``BREG=1`` (a padded image
