@@ -24,8 +24,8 @@ in ``scripts/probes/rowblock27r.py`` (``profiles/r03_band_*.log``).
 """
 import numpy as np
 
-from .hip_emitter import (PRELUDE, SIG_PARAMS, MarchConfig, _field_params, _scalar_params, _ws_plane_base,
-                          start_signal_lines, zsum_plan)
+from .hip_emitter import (PRELUDE, MarchConfig, _field_params, _scalar_params, _ws_plane_base, extra_params,
+                          halo_wait_lines, start_signal_lines, zsum_plan)
 from .printer import KernelExprPrinter
 
 __all__ = ['band_plans', 'band_geometry', 'band_choice', 'band_esize', 'emit_band']
@@ -181,6 +181,7 @@ def emit_band(ir, name, cfg):
     czf = bu and not cfg.BZF                        # BZF=0: the first element past a row zeroed in registers
     free = bool(cfg.BFREE)                          # LDS handshake instead of the plane barriers
     assert not (free and breg), 'the LDS handshake takes the LDS-DMA loader'
+    assert not (cfg.HWAIT and breg), 'the halo wait is the LDS-DMA loader\'s'
     NCW = NCT // 64                                 # compute waves
     pr = KernelExprPrinter('float', dict(ir.symbol_names))
     W = []
@@ -207,7 +208,7 @@ def emit_band(ir, name, cfg):
     params += ['const int Z', 'const int Y', 'const int X', 'const int zlo', 'const int zhi', 'const int ylo',
                'const int yhi', 'const int xlo', 'const int xhi', 'const int zc', 'const int zstep', 'const int ntx',
                'const int nty']
-    params += SIG_PARAMS if cfg.SIG else []
+    params += extra_params(cfg)
     params += _scalar_params(ir)
     L = [PRELUDE, 'typedef unsigned u32x4 __attribute__((ext_vector_type(4)));',
          'typedef unsigned u32x3 __attribute__((ext_vector_type(3)));', 'typedef unsigned u32x2 __attribute__((ext_vector_type(2)));']
@@ -306,6 +307,8 @@ def emit_band(ir, name, cfg):
             L.append('      }')
             L.append('      asm volatile("" ::: "memory");')
             L.append('    };')
+        if cfg.HWAIT:
+            L += halo_wait_lines()
         L.append(f'    for (int i = 0; i < {D}; ++i)')
         L.append('      if (i < nplanes) issue(zb - 1 + i, i);')
         L.append('    for (int j = 0; j < nplanes; ++j) {')

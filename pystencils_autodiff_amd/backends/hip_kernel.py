@@ -74,7 +74,7 @@ RING_WS_TILES = ((4, 4), (4, 2), (2, 4), (2, 2), (1, 4), (1, 2), (1, 1))
 # keys are this layer's tile parameters; an unknown one is a typo and raises.
 TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
              'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BPAD', 'BZF', 'BREG', 'BNT', 'BFREE', 'BTAIL',
-             'SFAST')
+             'SFAST', 'SLP')
 # Ablation knobs that make results WRONG (timing probes: ``BABL``). They are not tile keys — ``gpu_indexing_params`` and
 # ``PSAD_MARCH`` reject them — and reach the planner only through this dict, which nothing on the op's path writes:
 # a probe script sets it explicitly (``scripts/probes/op_band_ab.py``) and clears it again.
@@ -273,7 +273,7 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
         elif k == 'VIEW2D':
             cfg[k] = str(v)
-        elif k == 'SFAST':
+        elif k in ('SFAST', 'SLP'):
             cfg[k] = int(v)
     if ring_ws and PROBE_KNOBS.get('BABL'):
         cfg['BABL'] = int(PROBE_KNOBS['BABL'])   # (timing probe of the march ring, as on the band: 3 = no plane loads)
@@ -432,17 +432,27 @@ class HipStencilKernel:
     def code(self):
         return self.source(self.primary_variant())[0]
 
+    @staticmethod
+    def options(variant):
+        """hiprtc options of a variant: the plane ring of nonlinear stencils (``emit_march``) compiles without the SLP
+        vectorizer unless ``SLP=1`` — it paired scalar fp32 ops into ``v_pk_*`` at the price of register moves (varcoef
+        fp16 adjoint: 1030 → 871 VALU instructions, 246 → 200 VGPRs); the zsum / band kernels form their packed math
+        from explicit vector types and keep the default."""
+        if variant[0] == 'march' and not variant[1].ZSUM and not variant[1].BAND and not variant[1].SLP:
+            return rt.DEFAULT_OPTIONS + ('-fno-slp-vectorize',)
+        return rt.DEFAULT_OPTIONS
+
     def function(self, variant, device):
         src, kname = self.source(variant)
-        code = rt.compile_hip(src)
+        code = rt.compile_hip(src, self.options(variant))
         if variant[0] == 'pointwise':
             return {k: rt.load_function(code, f"{kname}_{k}", device) for k in ('v4', 'v1')}
         return rt.load_function(code, kname, device)
 
     def build(self):
         """Compile the primary variant ahead of time (hiprtc works without a GPU)."""
-        src, _ = self.source(self.primary_variant())
-        return rt.compile_hip(src)
+        v = self.primary_variant()
+        return rt.compile_hip(self.source(v)[0], self.options(v))
 
     # -- launch ---------------------------------------------------------------------------------
     def _field_specs(self):
@@ -486,11 +496,14 @@ class HipStencilKernel:
         return xb
 
     def prepare(self, halos=None, force_schedule=None, z_range=None, x_border=False, z_limits=None,
-                start_signal=False, **kwargs):
+                start_signal=False, halo_wait=False, **kwargs):
         """Everything of a launch but the launch: ``(function, grid, block, packed args, x_border done,
         device)``, or None for an empty domain (arguments as for ``__call__``). ``start_signal=True`` (march
         schedules, the z-slab interior): the kernel takes a signal word and a value after its extents, both zero in
-        the packed arguments (no store) — the caller patches them at ``last_plan.sig_offsets``."""
+        the packed arguments (no store) — the caller patches them at ``last_plan.sig_offsets``. ``halo_wait=True``
+        (LDS-DMA loader schedules, the z-slab faces on the compute stream): the loader waits for a word to reach a
+        value before its first plane load; both zero (no wait) until patched at ``last_plan.hwait_offsets``; a plan
+        without an LDS-DMA loader raises ``ValueError``."""
         torch = _torch()
         ir = self.ir
         if self._soa:
@@ -538,14 +551,15 @@ class HipStencilKernel:
         align = tuple(_align_class(p) for p in ptrs + hptrs)
         key = (force_schedule, bool(x_border), shape, strides, align,
                tuple(h.numel() if h is not None else -1 for h in halo_list), _zkey(z_range),
-               tuple(z_limits) if z_limits is not None else None, device) + (('sig',) if start_signal else ())
+               tuple(z_limits) if z_limits is not None else None, device) + (('sig',) if start_signal else ()) + \
+            (('hwait',) if halo_wait else ())
         plan = self._plans.get(key)
         if plan is None:
             if z_limits is not None:
                 if not ir.ndim == 3 or not 0 <= int(z_limits[0]) <= int(z_limits[1]) <= shape[0]:
                     raise ValueError(f'z_limits {z_limits} must lie in [0, {shape[0]}] of a 3-D kernel')
             plan = self._make_plan(tensors, halo_list, shape, device, contiguous, force_schedule, z_range, x_border,
-                                   z_limits, start_signal)
+                                   z_limits, start_signal, halo_wait)
             self._plans[key] = plan
         self.last_variant = plan.variant
         self.last_plan = plan
@@ -580,19 +594,21 @@ class HipStencilKernel:
         return kwargs
 
     def _make_plan(self, tensors, halo_list, shape, device, contiguous, force_schedule, z_range, x_border=False,
-                   z_limits=None, start_signal=False):
+                   z_limits=None, start_signal=False, halo_wait=False):
         torch = _torch()
         ir = self.ir
         sched = force_schedule or self.schedule()
         if sched != 'generic' and not contiguous:
             sched = 'generic'
-        if (halo_list or z_range is not None or z_limits is not None or start_signal) and sched != 'march':
+        if (halo_list or z_range is not None or z_limits is not None or start_signal or halo_wait) and \
+                sched != 'march':
             raise ValueError('halo planes / z ranges / start signals are only supported by the march schedule')
         with torch.cuda.device(device):
             if sched == 'pointwise':
                 return self._plan_pointwise(tensors, shape, device)
             if sched == 'march':
-                return self._plan_march(tensors, halo_list, shape, device, z_range, x_border, z_limits, start_signal)
+                return self._plan_march(tensors, halo_list, shape, device, z_range, x_border, z_limits, start_signal,
+                                        halo_wait)
             return self._plan_generic(tensors, shape, device)
 
     def _scalar_kind(self):
@@ -748,7 +764,7 @@ class HipStencilKernel:
                     ntx=ntx, nty=nty, grid=nt * nchunks)
 
     def _plan_march(self, tensors, halo_list, shape, device, z_range, x_border=False, z_limits=None,
-                    start_signal=False):
+                    start_signal=False, halo_wait=False):
         torch = _torch()
         ir = self.ir
         ve = self._vec_elems()
@@ -841,6 +857,10 @@ class HipStencilKernel:
                                      'BXW': g0['xlo'] == 0 and g0['xhi'] == g0['X'] and not cfg.XB})
         if start_signal:
             cfg = MarchConfig(**{**cfg.__dict__, 'SIG': True})
+        if halo_wait:
+            if not ((cfg.BAND and not (cfg.BREG and shape[-1] % (16 // esize))) or ws_geometry(ir, cfg)):
+                raise ValueError('a halo wait needs an LDS-DMA loader (band or WS schedule)')
+            cfg = MarchConfig(**{**cfg.__dict__, 'HWAIT': True})
         variant = ('march', cfg)
         fn = self.function(variant, device)
         ws = ws_geometry(ir, cfg)
@@ -864,13 +884,19 @@ class HipStencilKernel:
         if cfg.SIG:
             kinds += ['ptr', 'u32']                     # the start signal: word and value, patched by the caller
             statics += [0, 0]
+        if cfg.HWAIT:
+            kinds += ['ptr', 'u32']                     # the halo wait: word and value, patched by the caller
+            statics += [0, 0]
         kinds += [self._scalar_kind()] * len(ir.scalars)
         block = ws['block'] if ws else (band_geometry(cfg.BX, cfg.BTY, cfg.BAND, cfg.D, esize, cfg.BPAD, cfg.BREG, cfg.BFREE)['NT'] if cfg.BAND else
                                         cfg.NT)
         plan = _Plan(variant, fn, grid, kinds, len(tensors), 2 * len(stencil), statics, xb=cfg.XB, block=block)
+        i = len(tensors) + 2 * len(stencil) + 13
         if cfg.SIG:
-            i = len(tensors) + 2 * len(stencil) + 13
             plan.sig_offsets = (plan.offsets[i], plan.offsets[i + 1])
+            i += 2
+        if cfg.HWAIT:
+            plan.hwait_offsets = (plan.offsets[i], plan.offsets[i + 1])
         return plan
 
 
@@ -957,6 +983,7 @@ class _Plan:
         self.n_halo = n_halo
         self.statics = list(statics)
         self.sig_offsets = None          # (byte offset of the start-signal word, of its value): SIG launches
+        self.hwait_offsets = None        # (byte offset of the halo-wait word, of its value): HWAIT launches
 
     def scalar_slots(self, n):
         """``(byte offset, is f64)`` of the last ``n`` arguments (the kernel's scalar parameters)."""

@@ -44,6 +44,7 @@ struct Launch {
     std::vector<int64_t> slot; // pointer i <- table[slot[i]]
     std::vector<int64_t> s_off, s_f64, s_idx;   // scalar j at byte s_off[j] (f64 or f32) <- scalars[s_idx[j]]
     int64_t sig_ptr_off = -1, sig_val_off = -1; // start signal (hip_emitter SIG): word pointer and value, or -1
+    int64_t hw_ptr_off = -1, hw_val_off = -1;   // halo wait (hip_emitter HWAIT): word pointer and value, or -1
 };
 
 struct Alloc {
@@ -89,7 +90,8 @@ at::Tensor allocate(const Alloc& a, int device) {
 bool aligned(const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 31u) == 0; }
 
 void launch_on(const Launch& l, const std::vector<at::Tensor>& table, const std::vector<double>& scalars,
-               hipStream_t stream, uint32_t* sig = nullptr, uint32_t sig_value = 0);
+               hipStream_t stream, uint32_t* sig = nullptr, uint32_t sig_value = 0, const uint32_t* hw = nullptr,
+               uint32_t hw_value = 0);
 
 void launch(const Launch& l, const std::vector<at::Tensor>& table, const std::vector<double>& scalars,
             int device) {
@@ -99,12 +101,17 @@ void launch(const Launch& l, const std::vector<at::Tensor>& table, const std::ve
 }
 
 void launch_on(const Launch& l, const std::vector<at::Tensor>& table, const std::vector<double>& scalars,
-               hipStream_t stream, uint32_t* sig, uint32_t sig_value) {
+               hipStream_t stream, uint32_t* sig, uint32_t sig_value, const uint32_t* hw, uint32_t hw_value) {
     std::string args = l.args;
     if (sig != nullptr) {       // the launch stores sig_value to *sig when it starts (its template holds nullptr)
         TORCH_CHECK(l.sig_ptr_off >= 0 && l.sig_val_off >= 0, "psad: launch without a start-signal slot");
         std::memcpy(&args[l.sig_ptr_off], &sig, sizeof(sig));
         std::memcpy(&args[l.sig_val_off], &sig_value, sizeof(sig_value));
+    }
+    if (hw != nullptr) {        // the launch's loader waits for *hw >= hw_value (its template holds nullptr)
+        TORCH_CHECK(l.hw_ptr_off >= 0 && l.hw_val_off >= 0, "psad: launch without a halo-wait slot");
+        std::memcpy(&args[l.hw_ptr_off], &hw, sizeof(hw));
+        std::memcpy(&args[l.hw_val_off], &hw_value, sizeof(hw_value));
     }
     for (size_t i = 0; i < l.slot.size(); ++i) {
         void* p = table[l.slot[i]].data_ptr();
@@ -208,11 +215,14 @@ struct Exchange {
     // the interior launch writes the compute -> halo signal itself (default; PSAD_SLAB_START_SIG=0: a
     // hipStreamWriteValue32 on the compute stream)
     bool start_sig = true;
+    // the face launches on the compute stream, waiting in their loaders (PSAD_SLAB_FACE_WAIT=1; default: see sweep_from)
+    bool faces_wait = false;
 };
 
 std::mutex g_sweep_mutex;               // serialises the enqueue of exchanging sweeps (counter order = stream order)
 std::atomic<int64_t> g_event_sweeps{0};  // exchanging sweeps ordered by events (tests)
 std::atomic<int64_t> g_start_sig_sweeps{0};   // exchanging sweeps whose interior launch wrote the signal (tests)
+std::atomic<int64_t> g_face_wait_sweeps{0};   // ... whose face launches waited in-kernel on the compute stream (tests)
 
 struct Sweep {
     Exchange ex;
@@ -262,8 +272,21 @@ void run_sweep(const Sweep& w, const std::vector<at::Tensor>& table, const std::
     // the interior launch stores seq to the signal word when it starts (every earlier launch of the compute stream
     // has completed then): the compute queue carries no stream-memory write kernel for this ordering
     const bool start_sig = sig && !ex.faces_by_event && w.has_inner && w.inner.sig_ptr_off >= 0 && ex.start_sig;
-    if (sig && !ex.faces_by_event) {
-        if (!start_sig) hip_ok(hipStreamWriteValue32(cur, ex.sig, seq, 0), "hipStreamWriteValue32");
+    // ... and the face launches behind the interior on the compute stream, their loaders waiting for the halo stream's
+    // word: no stream-memory operation on the compute queue at all (the receive buffers are not reused before the next
+    // exchange, which waits for the next interior's start — after these faces in stream order)
+    bool faces_wait = start_sig && w.faces_on_halo && ex.faces_wait && !w.faces.empty();
+    for (const auto& f : w.faces) faces_wait = faces_wait && f.hw_ptr_off >= 0;
+    if (start_sig) {
+        // the interior launch (which stores seq when it starts) is ENQUEUED before the halo stream's wait for it: streams
+        // may share a hardware queue (GPU_MAX_HW_QUEUES), and a wait packet ahead of the launch that satisfies it in
+        // one queue would never complete
+        g_start_sig_sweeps.fetch_add(1);
+        launch_on(w.inner, table, scalars, cur, ex.sig, seq);
+        hip_ok(hipStreamWaitValue32(ex.stream, ex.sig, seq, hipStreamWaitValueGte, 0xffffffffu),
+               "hipStreamWaitValue32");
+    } else if (sig && !ex.faces_by_event) {
+        hip_ok(hipStreamWriteValue32(cur, ex.sig, seq, 0), "hipStreamWriteValue32");
         hip_ok(hipStreamWaitValue32(ex.stream, ex.sig, seq, hipStreamWaitValueGte, 0xffffffffu),
                "hipStreamWaitValue32");
     } else if (sig) {
@@ -288,15 +311,15 @@ void run_sweep(const Sweep& w, const std::vector<at::Tensor>& table, const std::
                                     ex.recv_hi.data(), ex.bytes.data(), ex.peer_lo, ex.peer_hi, ex.stream);
         TORCH_CHECK(rc == 0, "psad: RCCL halo exchange failed: ", psad_rccl_error_string(rc), " (code ", rc, ")");
     }
-    if (n && w.faces_on_halo)                                                // faces beside the interior
+    if (n && w.faces_on_halo && !faces_wait)                                 // faces beside the interior
         for (const auto& f : w.faces) launch_on(f, table, scalars, ex.stream);
-    if (w.has_inner) {                                                       // interior overlaps the exchange
-        if (start_sig) {
-            g_start_sig_sweeps.fetch_add(1);
-            launch_on(w.inner, table, scalars, cur, ex.sig, seq);
-        }
-        else
-            launch(w.inner, table, scalars, device);
+    if (w.has_inner && !start_sig) launch(w.inner, table, scalars, device);   // interior overlaps the exchange
+    if (faces_wait) {
+        // (the halo stream's write is enqueued before the face launches that wait for it: see start_sig)
+        g_face_wait_sweeps.fetch_add(1);
+        hip_ok(hipStreamWriteValue32(ex.stream, ex.sig_halo, seq, 0), "hipStreamWriteValue32");
+        for (const auto& f : w.faces) launch_on(f, table, scalars, cur, nullptr, 0, ex.sig_halo, seq);
+        return;
     }
     if (sig) {
         hip_ok(hipStreamWriteValue32(ex.stream, ex.sig_halo, seq, 0), "hipStreamWriteValue32");
@@ -423,15 +446,19 @@ Launch launch_from(const py::tuple& t, int64_t n_scalars) {
     Launch l = make_launch(t[0].cast<uint64_t>(), t[1].cast<int64_t>(), t[2].cast<int64_t>(), t[3].cast<py::bytes>(),
                            t[4].cast<std::vector<int64_t>>(), t[5].cast<std::vector<std::vector<int64_t>>>(), n_scalars);
     if (t.size() == 7) {
-        const auto sig = t[6].cast<std::vector<int64_t>>();     // (word offset, value offset) or empty
-        TORCH_CHECK(sig.empty() || (sig.size() == 2 && sig[0] >= 8 * static_cast<int64_t>(l.slot.size()) &&
-                                    sig[0] % 8 == 0 && sig[0] + 8 <= static_cast<int64_t>(l.args.size()) &&
-                                    sig[1] >= sig[0] + 8 && sig[1] + 4 <= static_cast<int64_t>(l.args.size())),
-                    "psad: start-signal offsets out of range");
-        if (!sig.empty()) {
-            l.sig_ptr_off = sig[0];
-            l.sig_val_off = sig[1];
+        // (start-signal word, value, halo-wait word, value) byte offsets, -1 where the kernel has none
+        const auto sig = t[6].cast<std::vector<int64_t>>();
+        TORCH_CHECK(sig.size() == 4, "psad: signal offsets are (sig word, sig value, wait word, wait value)");
+        const int64_t n = static_cast<int64_t>(l.args.size()), lo = 8 * static_cast<int64_t>(l.slot.size());
+        for (int k = 0; k < 4; k += 2) {
+            if (sig[k] < 0) continue;
+            TORCH_CHECK(sig[k] >= lo && sig[k] % 8 == 0 && sig[k] + 8 <= n && sig[k + 1] >= sig[k] + 8 &&
+                            sig[k + 1] + 4 <= n, "psad: signal offsets out of range");
         }
+        l.sig_ptr_off = sig[0];
+        l.sig_val_off = sig[1];
+        l.hw_ptr_off = sig[2];
+        l.hw_val_off = sig[3];
     }
     return l;
 }
@@ -494,6 +521,8 @@ Sweep sweep_from(const py::object& inner, const py::list& faces, const py::tuple
             w.ex.faces_by_event = sy != nullptr && std::string(sy) == "mixed";
             const char* ss = std::getenv("PSAD_SLAB_START_SIG");
             w.ex.start_sig = !(ss != nullptr && std::string(ss) == "0");
+            const char* fw = std::getenv("PSAD_SLAB_FACE_WAIT");
+            w.ex.faces_wait = fw != nullptr && std::string(fw) == "1";
         }
     }
     return w;
@@ -580,6 +609,8 @@ PYBIND11_MODULE(_psad_torch, m) {
           "exchanging slab sweeps ordered by event record + wait (PSAD_SLAB_SYNC=event, or another compute stream)");
     m.def("num_start_signal_sweeps", []() { return g_start_sig_sweeps.load(); },
           "exchanging slab sweeps whose interior launch signalled the halo stream itself (tests)");
+    m.def("num_face_wait_sweeps", []() { return g_face_wait_sweeps.load(); },
+          "exchanging slab sweeps whose face launches waited for the halos in-kernel on the compute stream (tests)");
     m.def("set_debug_poison", [](bool on) { g_poison.store(on); },
           "fill the outputs allocated uninitialised with NaN (tests: a kernel that leaves cells unwritten shows)");
     m.def("num_plans", []() {

@@ -695,7 +695,12 @@ class _NativeSlab:
                 nbytes.append(nb)
 
             def resolve(**extra):
-                prep = compiled.prepare(**kw, **scal, **extra)
+                try:
+                    prep = compiled.prepare(**kw, **scal, **extra)
+                except ValueError:
+                    if not extra.get('halo_wait'):
+                        raise
+                    return None                 # no LDS-DMA loader to wait in: the faces stay on the halo stream
                 if prep is None:
                     return None
                 fn, grid, block, packed, xb, _ = prep
@@ -707,17 +712,23 @@ class _NativeSlab:
                 sn = [sc.name for sc in compiled.ir.scalars]
                 slots = [[off, int(f64), scalar_names.index(n)]
                          for (off, f64), n in zip(compiled.last_plan.scalar_slots(len(sn)), sn)]
-                sig = list(compiled.last_plan.sig_offsets or ())
+                pl = compiled.last_plan
+                sig = list(pl.sig_offsets or (-1, -1)) + list(pl.hwait_offsets or (-1, -1))
                 return (int(fn), int(grid), int(block), bytes(packed), [table.index(n) for n in fnames], slots, sig)
             # the interior launch signals its own start (the halo stream's exchange waits for it): no stream-memory
             # write kernel on the compute queue (csrc/psad_torch.cpp run_sweep)
             inner_l = resolve(z_range=inner, start_signal=True) if inner else None
             if inner and inner_l is None:
                 return None
-            if len(faces) == 2 and faces[0][1] - faces[0][0] == faces[1][1] - faces[1][0]:
-                face_l = [resolve(halos=halos, z_range=tuple(faces))]
-            else:
-                face_l = [resolve(halos=halos, z_range=f) for f in faces]
+            def face_launches(**extra):
+                if len(faces) == 2 and faces[0][1] - faces[0][0] == faces[1][1] - faces[1][0]:
+                    return [resolve(halos=halos, z_range=tuple(faces), **extra)]
+                return [resolve(halos=halos, z_range=f, **extra) for f in faces]
+            # the face launches with a halo wait in their loader (they may then run on the compute stream behind the
+            # interior, csrc/psad_torch.cpp run_sweep), or as before where the schedule has no LDS-DMA loader
+            face_l = face_launches(halo_wait=True) if inner_l is not None else [None]
+            if any(f is None for f in face_l):
+                face_l = face_launches()
             if any(f is None for f in face_l):
                 return None
             peer_lo, peer_hi = zop._peers(halo)

@@ -14,7 +14,7 @@ from pystencils_autodiff_amd.backends import hip_kernel as HK  # noqa: E402
 from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel  # noqa: E402
 
 TILES = {
-    'default': {}, 'ws0': dict(WS=0), 'nt0': dict(NT_STORE=0),
+    'default': {}, 'ws0': dict(WS=0), 'nt0': dict(NT_STORE=0), 'slp1': dict(SLP=1), 'ws0_slp1': dict(WS=0, SLP=1),
     'reg': dict(CX=4, NR=4), 'reg_cx2nr2': dict(CX=2, NR=2), 'reg_cx1wx4nr4': dict(CX=1, WX=4, NR=4),
     'ws_cx4nr4': dict(WS=1, CX=4, NR=4, D=2), 'ws_cx4nr2': dict(WS=1, CX=4, NR=2, D=2),
     'ws_cx4nr2d3': dict(WS=1, CX=4, NR=2, D=3), 'ws_cx2nr4': dict(WS=1, CX=2, NR=4, D=2),

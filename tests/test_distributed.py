@@ -579,12 +579,16 @@ def test_zslab_native_plan_on_two_streams(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('face_wait', ['0', '1'], ids=['faces-halo-stream', 'faces-wait-in-kernel'])
 @pytest.mark.parametrize('builder_name,shape', [('asym_7pt', (12, 40, 70)), ('diffusion_7pt', (2, 9, 64)),
-                                                ('stencil_27pt', (9, 24, 80)), ('stencil_27pt', (96, 64, 256))])
-def test_zslab_native_node_loopback(builder_name, shape, monkeypatch):
+                                                ('stencil_27pt', (9, 24, 80)), ('stencil_27pt', (96, 64, 256)),
+                                                ('diffusion_7pt', (40, 64, 256))])
+def test_zslab_native_node_loopback(builder_name, shape, face_wait, monkeypatch):
     """The slab Function through the native node (``_psad_torch.apply_slab``: RCCL group, stream events, interior
     and face launches in C++) on a loopback communicator: the periodic-z oracle, and bitwise the Python Function's
-    sweeps (``PSAD_NATIVE_SLAB=0``) on the same inputs; a second call reuses the plan."""
+    sweeps (``PSAD_NATIVE_SLAB=0``) on the same inputs; a second call reuses the plan. ``face_wait``: the face
+    launches on the halo stream behind the exchange, or (``PSAD_SLAB_FACE_WAIT=1``) on the compute stream behind the
+    interior with their loader waves waiting in-kernel for the halo stream's word (schedules with an LDS-DMA loader)."""
     import sys
     sys.path.insert(0, ROOT)
     import pystencils_autodiff_amd as pa
@@ -601,6 +605,7 @@ def test_zslab_native_node_loopback(builder_name, shape, monkeypatch):
     rng = np.random.default_rng(6)
     u = rng.uniform(0, 1, shape).astype(dt)
     d = rng.uniform(-1, 1, shape).astype(dt)
+    monkeypatch.setenv('PSAD_SLAB_FACE_WAIT', face_wait)
     z = ZSlabOp(op, use_cuda=True)
     z._halo = RcclHalo(loopback=True)
     try:
@@ -609,6 +614,7 @@ def test_zslab_native_node_loopback(builder_name, shape, monkeypatch):
         fn = z.autograd_function()
         n0 = _psad_torch.num_slab_plans()
         s0 = _psad_torch.num_start_signal_sweeps()
+        w0 = _psad_torch.num_face_wait_sweeps()
         res = []
         for native in ('1', '1', '0'):
             monkeypatch.setenv('PSAD_NATIVE_SLAB', native)
@@ -622,6 +628,11 @@ def test_zslab_native_node_loopback(builder_name, shape, monkeypatch):
         # slabs with interior planes: each native sweep's interior launch wrote the halo stream's signal itself (no
         # stream-memory write kernel on the compute queue); a slab of faces only keeps hipStreamWriteValue32
         assert _psad_torch.num_start_signal_sweeps() - s0 == (4 if shape[0] > 2 else 0)
+        if face_wait == '0' or shape[0] <= 2:
+            assert _psad_torch.num_face_wait_sweeps() == w0
+        elif builder_name == 'stencil_27pt' or shape[2] % 4 == 0:
+            # schedules with an LDS-DMA loader (row bands, the WS ring): every native sweep's faces waited in-kernel
+            assert _psad_torch.num_face_wait_sweeps() - w0 == 4
         assert torch.equal(res[0][0], res[2][0]) and torch.equal(res[0][1], res[2][1])
         assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
