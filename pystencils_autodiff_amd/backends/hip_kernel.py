@@ -74,7 +74,7 @@ RING_WS_TILES = ((4, 4), (4, 2), (2, 4), (2, 2), (1, 4), (1, 2), (1, 1))
 # keys are this layer's tile parameters; an unknown one is a typo and raises.
 TILE_KEYS = ('CX', 'WX', 'NR', 'ZMIN', 'ZMAX', 'BLK', 'D', 'NW', 'NT_STORE', 'ZSUM', 'PK', 'WS', 'AR', 'VIEW2D', 'ZC',
              'BLOCKS', 'MAP', 'BAND', 'BTY', 'BTRIM', 'BEDGE', 'BPAD', 'BZF', 'BREG', 'BNT', 'BFREE', 'BTAIL',
-             'SFAST', 'SLP')
+             'SFAST', 'SLP', 'PR', 'PD')
 # Ablation knobs that make results WRONG (timing probes: ``BABL``). They are not tile keys — ``gpu_indexing_params`` and
 # ``PSAD_MARCH`` reject them — and reach the planner only through this dict, which nothing on the op's path writes:
 # a probe script sets it explicitly (``scripts/probes/op_band_ab.py``) and clears it again.
@@ -273,7 +273,7 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             cfg[k] = bool(int(v)) if not isinstance(v, bool) else v
         elif k == 'VIEW2D':
             cfg[k] = str(v)
-        elif k in ('SFAST', 'SLP'):
+        elif k in ('SFAST', 'SLP', 'PR', 'PD'):
             cfg[k] = int(v)
     if ring_ws and PROBE_KNOBS.get('BABL'):
         cfg['BABL'] = int(PROBE_KNOBS['BABL'])   # (timing probe of the march ring, as on the band: 3 = no plane loads)
@@ -284,15 +284,16 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
         cfg['WX'] = min(cfg['WX'], cfg['NW'])
     if cfg['ZSUM'] and zsum_plan(ir, MarchConfig(VE=ve, **cfg)) is None:
         cfg['ZSUM'] = False                                    # not eligible: LDS ring instead
+    cmin = 2 if cfg.get('PR') and not cfg['ZSUM'] else 1      # packed cell pairs: two cells per lane and column
     if shape is not None:
         X = int(shape[-1])
         if 'CX' not in over:
-            while cfg['CX'] > 1 and 64 * cfg['CX'] * cfg['WX'] // 2 >= X:
+            while cfg['CX'] > cmin and 64 * cfg['CX'] * cfg['WX'] // 2 >= X:
                 cfg['CX'] //= 2
             tx = 64 * cfg['CX'] * cfg['WX']
             ws0 = ws_geometry(ir, MarchConfig(VE=ve, **cfg)) if cfg.get('WS') else None
             quads = ws0 is not None and ws0['kind'] == 'h'       # the half ring needs lanes owning quads
-            if cfg.get('WS') and cfg['CX'] > 1 and -(-X // (tx // 2)) * (tx // 2) < -(-X // tx) * tx and \
+            if cfg.get('WS') and cfg['CX'] > cmin and -(-X // (tx // 2)) * (tx // 2) < -(-X // tx) * tx and \
                     (not quads or (cfg['CX'] // 2) % 4 == 0):
                 # WS tiles: half width when it pads x less (384³ 7-point: 0.116 → 0.081 ms with 48-plane
                 # chunks, profiles/r01_tune_odd_sizes.log)
@@ -314,8 +315,8 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
         return ws['lds_bytes'] if ws else march_geometry(ir, mc)['lds_bytes']
     while cfg.get('WS') and cfg.get('D', 3) > 1 and lds(cfg) > 160 * 1024:
         cfg['D'] = cfg.get('D', 3) - 1                          # fewer planes in flight before smaller tiles
-    while lds(cfg) > budget and (cfg['NR'] > 1 or cfg['CX'] > 1):
-        if cfg['NR'] >= cfg['CX'] and cfg['NR'] > 1:
+    while lds(cfg) > budget and (cfg['NR'] > 1 or cfg['CX'] > cmin):
+        if (cfg['NR'] >= cfg['CX'] or cfg['CX'] <= cmin) and cfg['NR'] > 1:
             cfg['NR'] //= 2
         else:
             cfg['CX'] //= 2
@@ -324,8 +325,8 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
         cfg['WS'] = False
         if cfg.get('NW', 4) == 8:                             # (eight compute waves only on the LDS-DMA ring)
             cfg['NW'], cfg['WX'] = 4, min(cfg['WX'], 4)
-        while lds(cfg) > budget and (cfg['NR'] > 1 or cfg['CX'] > 1):
-            if cfg['NR'] >= cfg['CX'] and cfg['NR'] > 1:
+        while lds(cfg) > budget and (cfg['NR'] > 1 or cfg['CX'] > cmin):
+            if (cfg['NR'] >= cfg['CX'] or cfg['CX'] <= cmin) and cfg['NR'] > 1:
                 cfg['NR'] //= 2
             else:
                 cfg['CX'] //= 2

@@ -83,12 +83,10 @@ def _lattice_sweeps(step, which, launches, force=None, dforce=None):
             plan = plans[sig] = K.plan(which, list(ts), mask, om, ids, force, dforce if which == 'adj' else None)
         plan(tuple(t.data_ptr() for t in ts) + mptr, stream, om)
         # link-program walls (HIP): the fix-up kernels over the cells next to them
-        gs = K.fix_launch(which, list(ts), mask, om, ids, force, dforce if which == 'adj' else None, cells, stream)
+        K.fix_launch(which, list(ts), mask, om, ids, force, dforce if which == 'adj' else None, cells, stream)
         if rho is not None:
             # the second pass of density-weighted walls (and, on the CPU, link programs) on this launch's output
             K.rho_pass(ts[2], mask, rho, ts[0], ids, stream)
-        if which == 'adj':
-            K.fix2_launch(ts[2], cells, gs, stream)
 
 
 def _plain_force_field(force, D):

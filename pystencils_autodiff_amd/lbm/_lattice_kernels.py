@@ -84,10 +84,13 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     ``Σ_j J_jk(c) v_j`` to component k of the cell — the Jacobians are evaluated there, on the cells next to a wall,
     not in the first pass, whose registers they would take on every cell (``mode='inline'``, the C target).
     HIP (``mode='main'`` / ``'fix'``): the forward evaluates the programs inline as above; the main adjoint carries
-    no program code and skips the cells marked ``FIX_BIT`` (fluid cells next to a program wall), and list-driven
-    fix-up kernels redo exactly those cells — the regular scatter plus ``G_k = Σ_j J_jk v_j`` into a per-listed-cell
-    scratch (``lbm_adj_fix``), then ``out_k(x) += G_k`` (``lbm_adj_fix2``, after every other store of the step) — so
-    the lattice's bulk runs the plain adjoint (measured: profiles/r05_lbm_pressure.jsonl)."""
+    no program code and leaves the cells marked ``FIX_BIT`` (fluid cells next to a program wall) to ONE list-driven
+    fix-up kernel (``lbm_adj_fix``): the regular scatter plus ``out_k(x) += G_k``, ``G_k = Σ_j J_jk v_j``. An entry
+    out_k(x) that receives G_k is written by the cell x + c_k (or x itself, bounced); when that writer is a listed
+    cell too (so it runs in the same fix-up launch), the main kernel's thread x zeroes the entry and both the
+    writer's value and G_k arrive by atomic adds — two addends onto zero, the same sum in either order, so the result
+    is the one the former second fix-up launch (``out += G`` after every other store) gave. The lattice's bulk runs
+    the plain adjoint (measured: profiles/r05_lbm_pressure.jsonl, r06_lbm_fix_merge.jsonl)."""
     D, Q = stencil.D, stencil.Q
     dirs = [tuple(d) for d in stencil.directions]
     w = [float(x) for x in stencil.weights]
@@ -133,6 +136,9 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                     for k in range(len(links)) for j in range(Q)]
             L.append(f'{qual} {nm}[{len(vals)}] = {{{", ".join(vals)}}};')
     low = f'{(1 << Q) - 1}u'                 # neighbour-mask bits of the Q directions
+    # the components q of a listed cell x that receive G_q = Σ_j J_jq v_j (link programs' Jacobian columns)
+    gq_all = sorted({q for pg in (programs or ()) if pg is not None for row in pg if row is not None
+                     for q, _, _ in row[2]}) if gen else []
 
     def c_(v):
         return f'({ct}){_c(v)}'
@@ -410,7 +416,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
 
     # ---- adjoint (scatter to where the forward pulled from)
     L.append(f'{fn} void lbm_adj_cell({sig_adj}, const int z, const int y, const int x'
-             + (f', {ct}* __restrict__ Gs, const int t' if fix else '') + ')\n{')
+             + ')\n{')
     L.append(f'  (void)Z; (void)s_bytes; (void)g_bytes; (void)o_bytes; (void)wallid; {fstr_unused}')
     rsrc(L, 's', 'src')
     rsrc(L, 'g', 'g')
@@ -429,7 +435,20 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             L.append('    ' + store('o', 'out', i, f'oo_{centre}', load('g', 'g', i, gcoff)))
         L.append('    return;\n  }')
         if mode == 'main':
-            L.append(f'  if ((msk >> {FIX_BIT}) & 1u) return;')
+            # a cell next to a program wall is the fix-up kernel's: it only zeroes the entries out_q(x), q in gq, that
+            # the fix-up kernel adds its G_q into and whose writer also runs there (the cell itself when x + c_q is a
+            # wall, or a listed neighbour x + c_q) — both contributions then arrive by atomic adds onto that zero
+            zl = []
+            for q in gq_all:
+                zero = store('o', 'out', q, f'oo_{centre}', c_(0))
+                if any(dirs[q]):
+                    kn = key(dirs[inv[q]])               # the neighbour x + c_q = x - c_(inv q)
+                    zl.append(f'    if (((msk >> {inv[q]}) & 1u) || ((nbmask[{ncell(kn)}] >> {FIX_BIT}) & 1u)) {zero}')
+                else:
+                    zl.append(f'    {zero}')
+            L.append(f'  if ((msk >> {FIX_BIT}) & 1u) {{')
+            L += zl
+            L.append('    return;\n  }')
     for i in range(Q):
         L.append(f'  const {ct} g{i} = {load("g", "g", i, gcoff)};')
     force_loads(L)
@@ -439,8 +458,7 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     moments(L)
     if rho_links:
         L.append(f'  {ct} Rr = 0;')             # Σ_j βρ_j v_j over the cell's density-weighted links
-    gq = sorted({q for pg in (programs or ()) if pg is not None for row in pg if row is not None
-                 for q, _, _ in row[2]}) if fix else []
+    gq = gq_all if fix else []
     if gq:
         L.append(f'  {ct} ' + ', '.join(f'G{q} = 0' for q in gq) + ';')      # Σ_j J_jq v_j (link programs)
         # the cell's own pdfs, once: every listed cell has a program link (not per link and row)
@@ -567,7 +585,21 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                          f' rho_adj[(IDX){j} * {ncells} + {cell}] = v; break;')
                 L.append('      default: break;\n    }')
             L.append(f'    if ((msk >> {j}) & 1u) v *= lk_g[id{j} * {Q} + {j}];')
-        if walls and any(dirs[j]):
+        if walls and any(dirs[j]) and fix and (j in gq or inv[j] in gq):
+            # a store into a G entry (component q in gq of a listed cell) is an atomic add onto the entry the main
+            # kernel zeroed: the cell itself (bounced, component ī) or a listed neighbour x − c_j (component j)
+            ab = 'true' if inv[j] in gq else 'false'
+            an = f'((nbmask[{ncell(k)}] >> {FIX_BIT}) & 1u)' if j in gq else 'false'
+            if buf:
+                L.append(f'    const unsigned vs = ((msk >> {j}) & 1u) ? oo_{centre} + (unsigned)({inv[j]} * o_qb) : '
+                         f'oo_{k} + (unsigned)({j} * o_qb);')
+                L.append(f'    if (((msk >> {j}) & 1u) ? {ab} : {an}) atomicAdd((T*)((char*)out + vs), (T)v); '
+                         f'else {store_v("o", "vs", "v")} }}')
+            else:
+                L.append(f'    const IDX vs = ((msk >> {j}) & 1u) ? (IDX){inv[j]} * o_q + oo_{centre} : (IDX){j} * o_q + '
+                         f'oo_{k};')
+                L.append(f'    if (((msk >> {j}) & 1u) ? {ab} : {an}) atomicAdd(out + vs, (T)v); else out[vs] = (T)v; }}')
+        elif walls and any(dirs[j]):
             if buf:
                 L.append(f'    const unsigned vs = ((msk >> {j}) & 1u) ? oo_{centre} + (unsigned)({inv[j]} * o_qb) : '
                          f'oo_{k} + (unsigned)({j} * o_qb);')
@@ -575,6 +607,10 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
             else:
                 L.append(f'    out[(msk >> {j}) & 1u ? (IDX){inv[j]} * o_q + oo_{centre} : (IDX){j} * o_q + oo_{k}] '
                          f'= (T)v; }}')
+        elif fix and j in gq:
+            # the rest population of a listed cell: its own G entry
+            L.append(f'    atomicAdd(' + (f'(T*)((char*)out + oo_{k} + (unsigned)({j} * o_qb))' if buf else
+                                         f'out + (IDX){j} * o_q + oo_{k}') + ', (T)v); }')
         else:
             L.append('    ' + store('o', 'out', j, f'oo_{k}', 'v') + ' }')
     inl = gen and mode == 'inline'
@@ -582,7 +618,10 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         # the density term: slot Q of the scratch array with inline link programs, its only slot without
         L.append(f'  if (msk & {low}) rho_adj[' + (f'(IDX){Q} * {ncells} + ' if inl else '') + f'{cell}] = Rr;')
     if gq:
-        L.append('  ' + ' '.join(f'Gs[(IDX)t * {len(gq)} + {n}] = G{q};' for n, q in enumerate(gq)))
+        # out_q(x) += G_q: after the main launch's store of that entry, or (zeroed entry) in either order with this
+        # launch's own atomic store into it — two addends onto zero, so the sum is the same either way
+        L.append('  ' + ' '.join(f'atomicAdd(' + (f'(T*)((char*)out + oo_{centre} + (unsigned)({q} * o_qb))' if buf else
+                                                 f'out + (IDX){q} * o_q + oo_{centre}') + f', G{q});' for q in gq))
     L.append('}')
     if two:
         # second adjoint pass: the density term of the cell's links reaches every component of the cell, whose
@@ -625,28 +664,16 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     args_a = (f'src, g, out, nbmask, wallid{fa_a}, Z, Y, X, s_q, s_z, s_y, s_x, g_q, g_z, g_y, g_x, o_q, o_z, o_y, o_x, '
               f'{fs}s_bytes, g_bytes, o_bytes, omega')
     if hip and fix:
-        # the fix-up kernels: one thread per listed cell (the fluid cells next to a link-program wall)
-        gcols = len(gq)
-        sig_fix2 = (f'T* __restrict__ out, const {ct}* __restrict__ Gs, const int Z, const int Y, const int X, '
-                    'const IDX o_q, const IDX o_z, const IDX o_y, const IDX o_x')
-        for nm, sig, call in (('lbm_adj_fix', sig_adj + f', {ct}* __restrict__ Gs',
-                               f'lbm_adj_cell({args_a}, z, y, x, Gs, t);'),
-                              ('lbm_adj_fix2', sig_fix2, None)):
-            L.append(f'extern "C" __global__ void __launch_bounds__(256) {nm}({sig}, const int* __restrict__ cells, '
-                     'const int ncell)\n{')
-            L.append('  const int t = (int)(blockIdx.x * 256u + threadIdx.x);')
-            L.append('  if (t >= ncell) return;')
-            L.append('  const unsigned cell = (unsigned)cells[t];')
-            L.append('  const unsigned r = cell / (unsigned)X;')
-            L.append('  const int x = (int)(cell - r * (unsigned)X);')
-            L.append('  const int z = (int)(r / (unsigned)Y), y = (int)(r - (unsigned)z * Y);')
-            if call is not None:
-                L.append(f'  {call}\n}}')
-            else:
-                L.append('  const IDX oc = ' + ' + '.join(f'(IDX){a} * o_{a}' for a in axes) + ';')
-                for n, q in enumerate(gq):
-                    L.append(f'  out[(IDX){q} * o_q + oc] += Gs[(IDX)t * {gcols} + {n}];')
-                L.append('}')
+        # the fix-up kernel: one thread per listed cell (the fluid cells next to a link-program wall)
+        L.append(f'extern "C" __global__ void __launch_bounds__(256) lbm_adj_fix({sig_adj}, const int* __restrict__ '
+                 'cells, const int ncell)\n{')
+        L.append('  const int t = (int)(blockIdx.x * 256u + threadIdx.x);')
+        L.append('  if (t >= ncell) return;')
+        L.append('  const unsigned cell = (unsigned)cells[t];')
+        L.append('  const unsigned r = cell / (unsigned)X;')
+        L.append('  const int x = (int)(cell - r * (unsigned)X);')
+        L.append('  const int z = (int)(r / (unsigned)Y), y = (int)(r - (unsigned)z * Y);')
+        L.append(f'  lbm_adj_cell({args_a}, z, y, x);\n}}')
     elif hip:
         # a block = 256 consecutive cells of the lattice in C order (rows of x), and consecutive blocks on one XCD
         # (bijective remap of the round-robin dispatch): a lattice row's x-shifted loads and the adjoint's
@@ -790,7 +817,6 @@ class LatticeKernels:
             any(p is not None for p in programs) else None
         self.link_pass = self.rho_links or (self.programs is not None and target != 'gpu')
         self.program_ids = tuple(k for k, p in enumerate(self.programs or ()) if p is not None)
-        self._gs = {}
         self._rho_bufs = {}
         self.target = target
         self._fns = {}
@@ -816,7 +842,7 @@ class LatticeKernels:
         fn = self._fns.get(key)
         if fn is None:
             from ..backends import hip_runtime as rt
-            code = rt.compile_hip(self.source(idx, addr, fix=which.endswith(('fix', 'fix2'))), name='psad_lbm.hip')
+            code = rt.compile_hip(self.source(idx, addr, fix=which.endswith('fix')), name='psad_lbm.hip')
             fn = self._fns[key] = rt.load_function(code, f'lbm_{which}', device)
         return fn
 
@@ -894,13 +920,12 @@ class LatticeKernels:
         """The launch of ``which`` ('fwd' / 'adj') on tensors of these shapes, strides, dtype and device (with or
         without walls): a ``LaunchPlan`` whose pointer slots and relaxation rate are patched per launch — the
         time-step op launches T of them per apply. ω is not part of the key (a trained or scheduled rate reuses the
-        plan); the plan is built with the first ω it sees. ``fix``: (cells, scratch) — the fix-up kernel of
-        ``which`` over the listed cells (int32 cell indices; the adjoint's per-listed-cell G scratch)."""
+        plan); the plan is built with the first ω it sees. ``fix``: (cells,) — the fix-up kernel of ``which`` over
+        the listed cells (int32 cell indices)."""
         key = (which, mask is not None) + tuple((tuple(t.shape), tuple(t.stride()), t.dtype, t.device)
                                                 for t in tensors) + \
             ((tuple(force.shape), tuple(force.stride())) if force is not None else ()) + \
-            ((fix[0].data_ptr(), int(fix[0].numel()), fix[1].data_ptr() if fix[1] is not None else 0)
-             if fix is not None else ())
+            ((fix[0].data_ptr(), int(fix[0].numel())) if fix is not None else ())
         plan = self._plans.get(key)
         if plan is not None:
             return plan
@@ -928,62 +953,27 @@ class LatticeKernels:
         vals = [*ptrs, Z, Y, X, *strides, *reach, float(omega)]
         om_i = len(fmt) - 1
         if fix is not None:
-            # the fix-up kernel: (+ the G scratch,) the cell list and its length after the main kernel's arguments
-            extra = ([fix[1].data_ptr()] if which == 'adj' else []) + [fix[0].data_ptr(), int(fix[0].numel())]
-            fmt += 'Q' * (len(extra) - 1) + 'i'
-            vals += extra
+            # the fix-up kernel: the cell list and its length after the main kernel's arguments
+            fmt += 'Qi'
+            vals += [fix[0].data_ptr(), int(fix[0].numel())]
         args = _pack(fmt, *vals)
         plan = self._plans[key] = LaunchPlan(fn, nblocks, args, len(ptrs), dev, _offset(fmt, om_i), fmt[om_i])
         return plan
 
-    def fix2_plan(self, out, cells, gs):
-        """The last fix-up launch of the adjoint (``lbm_adj_fix2``: out_k(x) += G_k at the listed cells)."""
-        key = ('fix2', tuple(out.shape), tuple(out.stride()), out.dtype, out.device, cells.data_ptr(),
-               int(cells.numel()), gs.data_ptr())
-        plan = self._plans.get(key)
-        if plan is not None:
-            return plan
-        idx, addr = self._mode([out])
-        dev = out.device.index
-        fn = self._gpu_fn('adj_fix2', idx, addr, dev)
-        Z, Y, X = self._extent(out)
-        code = 'i' if idx == 'int' else 'q'
-        fmt = 'QQ' + 'iii' + code * 4 + 'Qi'
-        args = _pack(fmt, out.data_ptr(), gs.data_ptr(), Z, Y, X, *lattice_strides(out, self.stencil.D),
-                     cells.data_ptr(), int(cells.numel()))
-        plan = self._plans[key] = LaunchPlan(fn, -(-int(cells.numel()) // 256), args, 1, dev, None, None)
-        return plan
-
-    def gs_buffer(self, cells, t):
-        """The fix-up adjoint's scratch: the G columns per listed cell (one per domain list and device, reused)."""
-        import torch
-        ncol = len({q for k in self.program_ids for row in self.programs[k] if row is not None for q, _, _ in row[2]})
-        key = (cells.data_ptr(), int(cells.numel()), t.device, t.dtype)
-        b = self._gs.get(key)
-        if b is None:
-            b = self._gs[key] = torch.empty((max(1, int(cells.numel())), ncol), dtype=t.dtype, device=t.device)
-        return b
-
     def fix_launch(self, which, tensors, mask, omega, ids, force, dforce, cells, stream):
         """The fix-up launch after a main adjoint launch on ``tensors`` (HIP with link programs; nothing for the
-        forward, which runs them inline, or when no cell is listed). ``fix2`` runs later: ``fix2_launch`` (after the
-        density pass)."""
+        forward, which runs them inline, or when no cell is listed): the listed cells' adjoint with their programs'
+        Jacobian terms, added atomically into the entries the main launch left zeroed (no second fix-up launch)."""
         if which != 'adj' or self.programs is None or self.target != 'gpu' or cells is None or \
                 int(cells.numel()) == 0:
-            return None
-        gs = self.gs_buffer(cells, tensors[0]) if which == 'adj' else None
-        plan = self.plan(which, tensors, mask, omega, ids, force, dforce, fix=(cells, gs))
+            return
+        plan = self.plan(which, tensors, mask, omega, ids, force, dforce, fix=(cells,))
         ptrs = tuple(t.data_ptr() for t in tensors) + (mask.data_ptr(), ids.data_ptr())
         if force is not None:
             ptrs += (force.data_ptr(),) + ((dforce.data_ptr(),) if which == 'adj' else ())
         if which == 'adj' and self.link_pass:
             ptrs += (self.rho_buffer(tensors[0]).data_ptr(),)
         plan(ptrs, stream, omega)
-        return gs
-
-    def fix2_launch(self, out, cells, gs, stream):
-        if gs is not None:
-            self.fix2_plan(out, cells, gs)((out.data_ptr(),), stream)
 
     def rho_buffer(self, t):
         """The per-cell scratch array of the second adjoint pass (one per domain and device, reused: stream-ordered):
@@ -1053,10 +1043,9 @@ class LatticeKernels:
              ids.data_ptr() if ids is not None else 0) +
             ((force.data_ptr(), dforce.data_ptr()) if force is not None else ()) +
             ((rho.data_ptr(),) if rho is not None else ()), st, omega)
-        gs = self.fix_launch('adj', [src, g, out], mask, omega, ids, force, dforce, cells, st)
+        self.fix_launch('adj', [src, g, out], mask, omega, ids, force, dforce, cells, st)
         if rho is not None:
             self.rho_pass(out, mask, rho, src, ids, st)
-        self.fix2_launch(out, cells, gs, st)
 
     def rho_pass(self, out, mask, rho, src, ids, stream):
         """Launch the adjoint's second pass (``rho_plan``) for this launch's ``out`` / ``src``."""

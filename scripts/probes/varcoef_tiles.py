@@ -15,6 +15,18 @@ from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel  # noqa: E4
 
 TILES = {
     'default': {}, 'ws0': dict(WS=0), 'nt0': dict(NT_STORE=0), 'slp1': dict(SLP=1), 'ws0_slp1': dict(WS=0, SLP=1),
+    'pr0': dict(PR=0), 'pr': dict(PR=1), 'ws0_pr': dict(WS=0, PR=1), 'ws0_pr0': dict(WS=0, PR=0),
+    'pr_cx2nr4': dict(PR=1, WS=0, CX=2, NR=4), 'pr_cx4nr4': dict(PR=1, WS=0, CX=4, NR=4),
+    'pr_ws_cx4nr2': dict(PR=1, WS=1, CX=4, NR=2, D=2), 'pr_ws8_cx4nr1': dict(PR=1, WS=1, NW=8, CX=4, NR=1, D=2),
+    'pr_ws8_cx2nr2': dict(PR=1, WS=1, NW=8, CX=2, NR=2, D=2), 'pr_sf0': dict(PR=1, SFAST=0),
+    'pd2': dict(PD=2, WS=0), 'pd2_pr': dict(PD=2, WS=0, PR=1), 'pd2_cx2nr4': dict(PD=2, WS=0, CX=2, NR=4),
+    'pd2_cx2nr2': dict(PD=2, WS=0, CX=2, NR=2), 'pd2_cx4nr1': dict(PD=2, WS=0, CX=4, NR=1),
+    'pd2_pr_cx2nr4': dict(PD=2, WS=0, PR=1, CX=2, NR=4), 'cx2nr2': dict(WS=0, CX=2, NR=2),
+    'cx2nr2_pr': dict(WS=0, CX=2, NR=2, PR=1), 'cx2nr1': dict(WS=0, CX=2, NR=1), 'cx1nr2': dict(WS=0, CX=1, NR=2),
+    'cx1nr4': dict(WS=0, CX=1, NR=4), 'cx2wx2nr2': dict(WS=0, CX=2, WX=2, NR=2), 'cx2wx2nr1': dict(WS=0, CX=2, WX=2, NR=1),
+    'cx2nr2_nw2': dict(WS=0, CX=2, NR=2, NW=2), 'cx4nr1': dict(WS=0, CX=4, NR=1), 'cx2nr1_pr': dict(WS=0, CX=2, NR=1, PR=1),
+    'cx2nr4': dict(WS=0, CX=2, NR=4), 'cx2nr2_nt0': dict(WS=0, CX=2, NR=2, NT_STORE=0),
+    'cx4nr2_pr': dict(WS=0, CX=4, NR=2, PR=1), 'cx4nr1_pr': dict(WS=0, CX=4, NR=1, PR=1),
     'reg': dict(CX=4, NR=4), 'reg_cx2nr2': dict(CX=2, NR=2), 'reg_cx1wx4nr4': dict(CX=1, WX=4, NR=4),
     'ws_cx4nr4': dict(WS=1, CX=4, NR=4, D=2), 'ws_cx4nr2': dict(WS=1, CX=4, NR=2, D=2),
     'ws_cx4nr2d3': dict(WS=1, CX=4, NR=2, D=3), 'ws_cx2nr4': dict(WS=1, CX=2, NR=4, D=2),

@@ -187,7 +187,8 @@ def test_varcoef_full_size_gpu():
 @pytest.mark.gpu
 @pytest.mark.parametrize('params', [dict(WS=1, NW=8, CX=4, NR=1, D=2), dict(WS=1, NW=8, CX=2, NR=2, D=3),
                                     dict(WS=1, CX=2, NR=2, D=1), dict(WS=1, CX=1, WX=4, NR=4, D=2),
-                                    dict(WS=0, CX=2, NR=2)], ids=str)
+                                    dict(WS=0, CX=2, NR=2), dict(WS=0, PD=2, CX=2, NR=2),
+                                    dict(WS=0, PD=2, CX=4, NR=1, PR=1)], ids=str)
 def test_varcoef_ring_tilings_gpu(params):
     """The plane ring's tilings (8 compute waves, ring depths, register-prefetch form) on a box of ragged tiles and
     chunks, every cell against the oracle."""
@@ -331,6 +332,99 @@ def test_varcoef_ring_none_mode_and_time_constant_gpu(mode):
         np.testing.assert_allclose(out.double().cpu().numpy(), ref['out'], rtol=1e-5, atol=1e-5)
         np.testing.assert_allclose(du.double().cpu().numpy(), refb['diffu'], rtol=1e-5, atol=1e-5)
         np.testing.assert_allclose(dk.double().cpu().numpy(), refb['diffk'], rtol=1e-5, atol=1e-5)
+
+
+PAIR_PARAMS = [dict(PR=1), dict(PR=1, WS=0), dict(PR=1, WS=0, CX=2, NR=4), dict(PR=1, WS=1, NW=8, CX=2, NR=2, D=2),
+               dict(PR=1, SFAST=0)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('params', PAIR_PARAMS, ids=str)
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float16], ids=['f32', 'f16'])
+@pytest.mark.parametrize('shape', [(19, 37, 200), (17, 33, 45), (9, 20, 129), (6, 5, 3), (12, 40, 256)], ids=str)
+def test_varcoef_pairs_gpu(params, dtype, shape):
+    """Packed cell pairs (``PR``: lanes own x-adjacent cells, f32x2 arithmetic, pair stores where aligned) on the plane
+    ring — LDS-DMA and register forms, fp32 and fp16 storage — on ragged tiles and odd rows (pairs straddling the
+    box edge, rows whose pairs start on odd cells), every cell against the oracle's element-wise bound."""
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    fp16 = dtype == torch.float16
+    if fp16 and params.get('WS', 1) and 'WS' in params:
+        pytest.skip('fp16 storage takes the register ring')
+    op = _op('float16' if fp16 else 'float32')
+    u, k, d = _inputs(shape, dtype, 'cuda', seed=17)
+    fk = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='vcp_f', target='gpu',
+                       gpu_indexing_params=params).compile()
+    bk = StencilKernel(op.backward_assignments, boundary_handling='zeros', function_name='vcp_b', target='gpu',
+                       gpu_indexing_params=params).compile()
+    out, du, dk = (torch.full_like(u, float('nan')) for _ in range(3))
+    fk(u=u, k=k, out=out)
+    bk(u=u, k=k, diffout=d, diffu=du, diffk=dk)
+    torch.cuda.synchronize()
+    for kk in (fk, bk):
+        assert kk.last_variant[0] == 'march' and kk.last_variant[1].PR and not kk.last_variant[1].ZSUM
+    ref, ab = oracle(op, *(x.double().cpu().numpy() for x in (u, k, d)))
+    check(out, ref['out'], ab['out'], False, f'{params} out', fp16)
+    check(du, ref['diffu'], ab['diffu'], False, f'{params} diffu', fp16)
+    check(dk, ref['diffk'], ab['diffk'], False, f'{params} diffk', fp16)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('mode', ['none', 'time_constant'])
+def test_varcoef_pairs_none_mode_and_time_constant_gpu(mode):
+    """Packed pairs under ``boundary_handling=None`` (NaN-poisoned border untouched: pairs straddling the written box
+    store one cell) and with a time-constant conductivity (``diffk`` read back pairwise and accumulated), on a row of
+    odd length."""
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    ac = W.varcoef_diffusion_7pt()
+    bh = None if mode == 'none' else 'zeros'
+    kfield = next(f for f in ac.free_symbols if hasattr(f, 'field') and f.field.name == 'k').field
+    op = pa.AutoDiffOp(ac, boundary_handling=bh, time_constant_fields=[kfield] if mode == 'time_constant' else None)
+    shape = (19, 37, 137)
+    u, k, d = _inputs(shape, torch.float32, 'cuda', seed=19)
+    for params in (dict(PR=1), dict(PR=1, WS=0)):
+        fk = StencilKernel(op.forward_assignments, boundary_handling=bh, function_name='vpn_f', target='gpu',
+                           gpu_indexing_params=params).compile()
+        bk = StencilKernel(op.backward_assignments, boundary_handling=bh, function_name='vpn_b', target='gpu',
+                           gpu_indexing_params=params).compile()
+        fill = float('nan') if mode == 'none' else 0.0
+        out, du = torch.full_like(u, fill), torch.full_like(u, fill)
+        dk = torch.full_like(u, fill) if mode == 'none' else torch.rand(shape, device='cuda')
+        dk0 = dk.clone()
+        fk(u=u, k=k, out=out)
+        bk(u=u, k=k, diffout=d, diffu=du, diffk=dk)
+        torch.cuda.synchronize()
+        assert fk.last_variant[1].PR and bk.last_variant[1].PR
+        arr = {n: t.double().cpu().numpy() for n, t in (('u', u), ('k', k))}
+        ref = OE.evaluate(op.forward_assignments, arr, boundary_handling=bh)
+        refb = OE.evaluate(op.backward_assignments, {**arr, 'diffout': d.double().cpu().numpy()}, boundary_handling=bh,
+                           outputs={'diffk': dk0.double().cpu().numpy()} if mode == 'time_constant' else None)
+        inner = (slice(1, -1),) * 3 if mode == 'none' else (slice(None),) * 3
+        for got, name, r in ((out, 'out', ref), (du, 'diffu', refb), (dk, 'diffk', refb)):
+            g_ = got.double().cpu().numpy()
+            np.testing.assert_allclose(g_[inner], r[name][inner], rtol=1e-5, atol=1e-5, err_msg=f'{params} {name}')
+            if mode == 'none':
+                border = np.ones(shape, bool)
+                border[inner] = False
+                assert np.isnan(g_[border]).all(), f'{params} {name}: a border cell was written'
+
+
+def test_pair_form_eligibility():
+    """``PR`` takes fp32 arithmetic of +, ×, integer powers on scalar fields; functions raise (no GPU needed)."""
+    import sympy as sp
+    from pystencils_autodiff_amd.backends.hip_emitter import pair_ok
+    from pystencils_autodiff_amd.backends.hip_kernel import HipStencilKernel
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    for dts, ok in (('float32', True), ('float16', True), ('float64', False)):
+        k = StencilKernel(_op(dts).backward_assignments, boundary_handling='zeros', function_name='pe', target='gpu')
+        assert pair_ok(HipStencilKernel(k).ir) == ok
+    a, b = ps.fields('a, b: float32[3d]')
+    op = pa.AutoDiffOp(ps.AssignmentCollection({b.center: sp.sin(a[1, 0, 0]) * a[0, 0, -1]}), boundary_handling='zeros')
+    k = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='pe2', target='gpu',
+                      gpu_indexing_params=dict(PR=1))
+    hk = HipStencilKernel(k)
+    assert not pair_ok(hk.ir)
+    with pytest.raises(ValueError, match='PR=1'):
+        hk.source(('march', hk._march_cfg(4, (16, 16, 256))))
 
 
 # ------------------------------------------------------------------------------------------------------------------
