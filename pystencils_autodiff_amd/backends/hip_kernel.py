@@ -240,6 +240,12 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
                 cfg.update(c)
                 ring_ws = True
                 break
+    if ir.ndim == 3 and not zsum_ok and not ring_ws:
+        # nonlinear stencils on the register-prefetch ring (fp16 storage: the LDS-DMA ring holds the compute type):
+        # 128×8 tiles, four workgroups per CU — varcoef fp16 768³ fwd / bwd 0.69–0.71 / 1.16–1.18 ms vs 0.81 / 1.31–1.34
+        # with the budget's 256×16 / 256×8 (profiles/r06_varcoef_f16_tiles.log: latency, not VALU — packed cell pairs
+        # or two planes in flight on the wide tiles gave nothing, r06_varcoef_pairs_f16.log, r06_varcoef_pd2_f16.log)
+        cfg.update(CX=2, NR=2)
     if ir.ndim == 2:
         cfg.update(CX=4, WX=1, NR=4, VIEW2D='yx', NT_STORE=False)   # 256×16 tiles (4096²: 0.024 ms, 5.6 TB/s)
     if ir.has_index_dims and not ring_ws:
