@@ -15,8 +15,8 @@ import numpy as np
 
 from . import hip_runtime as rt
 from .hip_band import band_choice, band_esize, band_geometry, band_plans, emit_band
-from .hip_emitter import (MarchConfig, emit_generic, emit_march, emit_pointwise, emit_zsum, march_geometry, ws_geometry,
-                          zsum_plan)
+from .hip_emitter import (MarchConfig, emit_generic, emit_march, emit_pointwise, emit_zsum, march_geometry, pair_ok,
+                          storage_ctype, ws_geometry, zsum_plan)
 
 __all__ = ['HipStencilKernel', 'default_march_config']
 
@@ -233,13 +233,25 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
     if ir.ndim == 3 and not zsum_ok:
         # stencils not linear off the centre plane (products / functions of neighbour taps): the plane ring fed by
         # an LDS-DMA loader wave, 2 planes in flight, the widest tile whose ring fits the LDS
-        for cx, nr in RING_WS_TILES:
-            c = {**cfg, 'CX': cx, 'NR': nr, 'WS': True, 'D': 2, 'ZMIN': 8, 'ZMAX': 128, 'BLK': 256}
+        tiles = RING_WS_TILES
+        if pair_ok(ir) and any(storage_ctype(f) == '_Float16' for f in ir.stencil_fields):
+            # fp16 planes in the ring, taps as whole dwords of cell pairs (PR): 128×8 tiles, two planes in flight, for
+            # two ring fields (varcoef forward), 128×4 and three in flight for more (its adjoint: three fields). 768³
+            # fwd / bwd 0.618–0.634 / 1.066–1.095 ms vs 0.67–0.69 / 1.16–1.17 on the register ring
+            # (profiles/r06_hring_f16.log, r06_hring_f16b.log: 20 tilings, 8 compute waves and deeper rings slower)
+            two = len(ir.stencil_fields) <= 2
+            tiles = [(2, 2 if two else 1)]
+            cfg['PR'] = 1
+        for cx, nr in tiles:
+            c = {**cfg, 'CX': cx, 'NR': nr, 'WS': True, 'D': 2 if nr == 2 or not cfg.get('PR') else 3, 'ZMIN': 8,
+                 'ZMAX': 128, 'BLK': 256}
             w = ws_geometry(ir, MarchConfig(VE=ve, **c))
             if w is not None and w['lds_bytes'] <= 160 * 1024:
                 cfg.update(c)
                 ring_ws = True
                 break
+        if not ring_ws:
+            cfg['PR'] = 0                 # (the register ring stores fp32 images: pairs measured neutral there)
     if ir.ndim == 3 and not zsum_ok and not ring_ws:
         # nonlinear stencils on the register-prefetch ring (fp16 storage: the LDS-DMA ring holds the compute type):
         # 128×8 tiles, four workgroups per CU — varcoef fp16 768³ fwd / bwd 0.69–0.71 / 1.16–1.18 ms vs 0.81 / 1.31–1.34

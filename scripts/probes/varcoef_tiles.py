@@ -27,6 +27,15 @@ TILES = {
     'cx2nr2_nw2': dict(WS=0, CX=2, NR=2, NW=2), 'cx4nr1': dict(WS=0, CX=4, NR=1), 'cx2nr1_pr': dict(WS=0, CX=2, NR=1, PR=1),
     'cx2nr4': dict(WS=0, CX=2, NR=4), 'cx2nr2_nt0': dict(WS=0, CX=2, NR=2, NT_STORE=0),
     'cx4nr2_pr': dict(WS=0, CX=4, NR=2, PR=1), 'cx4nr1_pr': dict(WS=0, CX=4, NR=1, PR=1),
+    'h_ws_cx4nr2': dict(PR=1, WS=1, CX=4, NR=2, D=2), 'h_ws_cx4nr4': dict(PR=1, WS=1, CX=4, NR=4, D=2),
+    'h_ws_cx2nr2': dict(PR=1, WS=1, CX=2, NR=2, D=2), 'h_ws_cx2nr4': dict(PR=1, WS=1, CX=2, NR=4, D=2),
+    'h_ws_cx4nr2_d3': dict(PR=1, WS=1, CX=4, NR=2, D=3), 'h_ws_cx2nr2_d3': dict(PR=1, WS=1, CX=2, NR=2, D=3),
+    'h_ws8_cx4nr1': dict(PR=1, WS=1, NW=8, CX=4, NR=1, D=2), 'h_ws8_cx2nr2': dict(PR=1, WS=1, NW=8, CX=2, NR=2, D=2),
+    'h_ws_cx4nr1': dict(PR=1, WS=1, CX=4, NR=1, D=2), 'h_ws_cx2nr1_d3': dict(PR=1, WS=1, CX=2, NR=1, D=3),
+    'h_ws_cx2nr1': dict(PR=1, WS=1, CX=2, NR=1, D=2), 'h_ws8_cx2nr1': dict(PR=1, WS=1, NW=8, CX=2, NR=1, D=2),
+    'h_ws8_cx2nr1_d3': dict(PR=1, WS=1, NW=8, CX=2, NR=1, D=3), 'h_ws8_cx2nr2_d3': dict(PR=1, WS=1, NW=8, CX=2, NR=2, D=3),
+    'h_ws_cx2nr1_d4': dict(PR=1, WS=1, CX=2, NR=1, D=4), 'h_ws_cx2nr2_d4': dict(PR=1, WS=1, CX=2, NR=2, D=4),
+    'h_ws_cx2wx2nr1_d3': dict(PR=1, WS=1, CX=2, WX=2, NR=1, D=3), 'h_ws_cx2wx2nr2': dict(PR=1, WS=1, CX=2, WX=2, NR=2, D=2),
     'reg': dict(CX=4, NR=4), 'reg_cx2nr2': dict(CX=2, NR=2), 'reg_cx1wx4nr4': dict(CX=1, WX=4, NR=4),
     'ws_cx4nr4': dict(WS=1, CX=4, NR=4, D=2), 'ws_cx4nr2': dict(WS=1, CX=4, NR=2, D=2),
     'ws_cx4nr2d3': dict(WS=1, CX=4, NR=2, D=3), 'ws_cx2nr4': dict(WS=1, CX=2, NR=4, D=2),

@@ -335,7 +335,7 @@ def test_varcoef_ring_none_mode_and_time_constant_gpu(mode):
 
 
 PAIR_PARAMS = [dict(PR=1), dict(PR=1, WS=0), dict(PR=1, WS=0, CX=2, NR=4), dict(PR=1, WS=1, NW=8, CX=2, NR=2, D=2),
-               dict(PR=1, SFAST=0)]
+               dict(PR=1, SFAST=0), dict(PR=1, WS=1, CX=4, NR=2, D=2), dict(PR=1, WS=1, CX=2, NR=2, D=3)]
 
 
 @pytest.mark.gpu
@@ -348,8 +348,6 @@ def test_varcoef_pairs_gpu(params, dtype, shape):
     box edge, rows whose pairs start on odd cells), every cell against the oracle's element-wise bound."""
     from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
     fp16 = dtype == torch.float16
-    if fp16 and params.get('WS', 1) and 'WS' in params:
-        pytest.skip('fp16 storage takes the register ring')
     op = _op('float16' if fp16 else 'float32')
     u, k, d = _inputs(shape, dtype, 'cuda', seed=17)
     fk = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='vcp_f', target='gpu',
