@@ -88,26 +88,47 @@ def assert_cells(actual, ref, absterms, nterms, storage, what='', rtol=1e-6, sla
                              f'(Σ|terms| {absterms[i]:.3e})')
 
 
-def abs_linear(collection):
-    """The collection with every main assignment's right-hand side (subexpressions substituted) replaced by
-    Σ|c|·access over its linear expansion — evaluated on |inputs| it gives Σ|terms| per cell. None if a right-hand
-    side is not linear in the field accesses with numeric coefficients."""
+def _degree(rest):
+    """Degree of a monomial of field accesses (positive integer powers), or None for anything else."""
+    import sympy as sp
+
+    from pystencils_autodiff_amd import ps
+    deg = 0
+    for f in sp.Mul.make_args(rest):
+        b, e = f.as_base_exp()
+        if not isinstance(b, ps.Field.Access) or not (e.is_Integer and int(e) > 0):
+            return None
+        deg += int(e)
+    return deg
+
+
+def abs_poly(collection, max_degree=1):
+    """(collection, degree): every main assignment's right-hand side (subexpressions substituted) replaced by
+    Σ|c|·monomial over its polynomial expansion — evaluated on |inputs| it gives Σ|terms| per cell — and the highest
+    monomial degree. None if a right-hand side is not a polynomial of degree <= ``max_degree`` in the field accesses
+    with numeric coefficients (functions, divisions by accesses, symbolic parameters)."""
     import sympy as sp
 
     from pystencils_autodiff_amd import ps
     flat = collection.new_without_subexpressions()
-    mains = []
+    mains, top = [], 0
     for a in flat.main_assignments:
-        rhs = sp.expand(a.rhs)
-        terms = sp.Add.make_args(rhs)
         new = 0
-        for t in terms:
+        for t in sp.Add.make_args(sp.expand(a.rhs)):
             c, rest = t.as_coeff_Mul()
-            if not isinstance(rest, ps.Field.Access) or not c.is_number:
+            d = _degree(rest)
+            if d is None or d > max_degree or not c.is_number:
                 return None
+            top = max(top, d)
             new += abs(float(c)) * rest
         mains.append(ps.Assignment(a.lhs, new))
-    return ps.AssignmentCollection(mains)
+    return ps.AssignmentCollection(mains), top
+
+
+def abs_linear(collection):
+    """``abs_poly`` of a linear collection (Σ|c|·access per main assignment), None if one is not linear."""
+    r = abs_poly(collection)
+    return r[0] if r is not None else None
 
 
 def abs_terms(collection, inputs, boundary_handling='zeros'):
@@ -120,15 +141,21 @@ def abs_terms(collection, inputs, boundary_handling='zeros'):
 
 
 def assert_cells_linear(actual, ref, collection, inputs, boundary_handling, storage, what=''):
-    """``assert_cells`` for a linear ``collection`` (Σ|terms| from the inputs, its term count); a nonlinear one keeps
-    the caller's field-scaled check only. Returns whether the element-wise check ran."""
-    if abs_linear(collection) is None:
+    """``assert_cells`` for a polynomial ``collection`` (Σ|terms| of its expansion from the inputs, its term count;
+    products of d accesses round d − 1 more times: ``slack`` 4·d); one with functions of the accesses keeps the
+    caller's field-scaled check only. Returns whether the element-wise check ran."""
+    from oracle import evaluate as OE
+    pr = abs_poly(collection, max_degree=4)
+    if pr is None:
         return False
-    absr = abs_terms(collection, inputs, boundary_handling)
+    ac, deg = pr
+    absr = OE.evaluate(ac, {n: np.abs(np.asarray(a, dtype=np.float64)) for n, a in inputs.items()},
+                       boundary_handling=boundary_handling)
+    nt = max(len(__import__('sympy').Add.make_args(a.rhs)) for a in ac.main_assignments)
     for name, r in (ref.items() if isinstance(ref, dict) else [(None, ref)]):
         a = actual[name] if isinstance(actual, dict) else actual
         n = name if name is not None else next(iter(absr))
-        assert_cells(a, r, absr[n], n_terms(collection), storage, f'{what} {n}')
+        assert_cells(a, r, absr[n], nt, storage, f'{what} {n}', slack=4.0 * max(1, deg))
     return True
 
 

@@ -118,6 +118,28 @@ def test_varcoef_cpu_backend_vs_oracle():
     _run((5, 8, 13), torch.float32, 'cpu', seed=1)
 
 
+def test_polynomial_cell_bound_engages_on_varcoef():
+    """``conftest.assert_cells_linear`` takes polynomial (not only linear) collections: the varcoef forward and its
+    TF-MAD adjoint (products of two taps) are checked cell by cell with Σ|terms| of their expansion — here on the C
+    kernels (fp32 arithmetic); the GPU tests call the same helper. A stencil with a function of its taps still returns
+    False (the caller's field-scaled check only)."""
+    from tests.conftest import abs_poly, assert_cells_linear
+    op = _op('float32')
+    u, k, d = _inputs((9, 14, 20), torch.float32, 'cpu', seed=21)
+    out, gu, gk = _apply(op, u, k, d, 'cpu')
+    arr = {'u': u.double().numpy(), 'k': k.double().numpy(), 'diffout': d.double().numpy()}
+    ref = {**OE.evaluate(op.forward_assignments, arr, boundary_handling='zeros'),
+           **OE.evaluate(op.backward_assignments, arr, boundary_handling='zeros')}
+    assert abs_poly(op.forward_assignments, 4)[1] == 2 and abs_poly(op.backward_assignments, 4)[1] == 2
+    assert assert_cells_linear({'out': out.detach().numpy()}, {'out': ref['out']}, op.forward_assignments,
+                               {'u': arr['u'], 'k': arr['k']}, 'zeros', np.float32, 'fwd')
+    assert assert_cells_linear({'diffu': gu.numpy(), 'diffk': gk.numpy()},
+                               {'diffu': ref['diffu'], 'diffk': ref['diffk']}, op.backward_assignments, arr, 'zeros',
+                               np.float32, 'bwd')
+    a, b = ps.fields('a, b: float32[3d]')
+    assert abs_poly(ps.AssignmentCollection({b.center: sp.sin(a[1, 0, 0]) * a[0, 0, -1]}), 4) is None
+
+
 def test_varcoef_tfmad_is_reverse_mode_for_uniform_k():
     """With a uniform conductivity the TF-MAD ``diffu`` is the true gradient away from the zero border (where
     ``k[nb]`` reads 0 and the derivative varies in space); with a varying one it is not, and ``diffk`` (whose
