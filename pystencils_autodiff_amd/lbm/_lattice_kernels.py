@@ -44,6 +44,7 @@ def _c(v):
 
 SELF_BIT = 30      # bit of a cell's neighbour mask: the cell itself is an obstacle (bits 0..Q-1: x − c_i is one)
 FIX_BIT = 31       # ... the cell is a fluid cell next to a wall with a link program (the HIP fix-up kernels' cells)
+FIX_BLOCK = 64     # threads per workgroup of the fix-up kernel
 
 
 def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=None, force_model=None, force=None,
@@ -260,12 +261,20 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
         used = sorted({int(m) for m in re.findall(r'\bc(\d+)\b', code)})
         return ' '.join(f'const {ct} c{q} = {rd(q)};' for q in used)
 
-    def pull_loads(L, prefix, arr, progs=True):
+    def pull_loads(L, prefix, arr, progs=True, hoisted=False):
+        """``hoisted`` (the fix-up kernel, whose every cell has program links): the wall ids are loaded for every
+        direction up front and the cell's own pdfs ``c<q>`` are already loaded, so no load waits on the mask."""
         for i in range(Q):
             k = key(dirs[i])
             cq = '' if links is not None and walls and any(dirs[i]) else 'const '
             if walls and any(dirs[i]):
-                if buf:
+                if hoisted and buf:
+                    # (fix-up kernel: both candidates loaded, then selected — no load waits on the mask)
+                    L.append(f'  const {ct} fb{i} = '
+                             f'{load_v(prefix, f"{prefix}o_{centre} + (unsigned)({inv[i]} * {prefix}_qb)")}, '
+                             f'fs{i} = {load_v(prefix, f"{prefix}o_{k} + (unsigned)({i} * {prefix}_qb)")};')
+                    L.append(f'  {cq}{ct} f{i} = ((msk >> {i}) & 1u) ? fb{i} : fs{i};')
+                elif buf:
                     # a bounced component is read from the cell itself: ONE load whose per-lane offset selects
                     # (component, cell) — not both loads and a select
                     L.append(f'  const unsigned vo{i} = ((msk >> {i}) & 1u) ? {prefix}o_{centre} + '
@@ -277,16 +286,21 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
                 if links is not None:
                     # the wall cell's link (moving wall: α = 1, β = 6 w (c·u)); its id is loaded on this path only
                     rterm = f' + lk_r[id{i} * {Q} + {i}] * rs' if rho_links else ''
-                    L.append(f'  unsigned id{i} = 0;')
-                    L.append(f'  if ((msk >> {i}) & 1u) {{ id{i} = wallid[{ncell(k)}]; '
-                             f'f{i} = lk_a[id{i} * {Q} + {i}] * f{i} + lk_b[id{i} * {Q} + {i}]{rterm}; }}')
+                    if hoisted:
+                        L.append(f'  const unsigned id{i} = ((msk >> {i}) & 1u) ? (unsigned)wid{i} : 0u;')
+                        L.append(f'  if ((msk >> {i}) & 1u) f{i} = lk_a[id{i} * {Q} + {i}] * f{i} + lk_b[id{i} * {Q} + '
+                                 f'{i}]{rterm};')
+                    else:
+                        L.append(f'  unsigned id{i} = 0;')
+                        L.append(f'  if ((msk >> {i}) & 1u) {{ id{i} = wallid[{ncell(k)}]; '
+                                 f'f{i} = lk_a[id{i} * {Q} + {i}] * f{i} + lk_b[id{i} * {Q} + {i}]{rterm}; }}')
                     cases = program_cases(i) if progs else []
                     if cases:
                         L.append(f'  if ((msk >> {i}) & 1u) switch (id{i}) {{')
                         for wid, pg in cases:
                             lines, val, _ = pg
                             body = ' '.join(lines) + f' f{i} = {val};'
-                            ld = own_loads(body, lambda q: load(prefix, arr, q, f'{prefix}o_{centre}'))
+                            ld = '' if hoisted else own_loads(body, lambda q: load(prefix, arr, q, f'{prefix}o_{centre}'))
                             L.append(f'    case {wid}: {{ {ld} {body} }} break;')
                         L.append('    default: break;\n  }')
             else:
@@ -454,18 +468,25 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
     force_loads(L)
     cell_density(L, 's', 'src')
     adj_progs = gen and mode != 'main'          # the main HIP adjoint leaves the program cells to the fix-up kernels
-    pull_loads(L, 's', 'src', adj_progs)
+    gq = gq_all if fix else []
+    if gq:
+        # the fix-up kernel: every listed cell has a program link, so its own pdfs (read by the links' programs and
+        # their Jacobians) and the wall ids of all its neighbours are loaded once, up front, beside the mask — no load
+        # of the kernel's latency-bound chain waits on the mask or on an id
+        used = sorted({int(m) for pg in programs if pg is not None for row in pg if row is not None
+                       for m in re.findall(r'\bc(\d+)\b', ' '.join(row[0]) + ' ' + row[1] + ' ' +
+                                           ' '.join(' '.join(jl) + ' ' + je for _, jl, je in row[2]))})
+        if used:
+            L.append('  ' + ' '.join(f'const {ct} c{q} = {load("s", "src", q, f"so_{centre}")};' for q in used))
+        if links is not None and walls:
+            L.append('  ' + ' '.join(f'const unsigned char wid{i} = wallid[{ncell(key(dirs[i]))}];'
+                                     for i in range(Q) if any(dirs[i])))
+    pull_loads(L, 's', 'src', adj_progs, hoisted=bool(gq) and links is not None and walls)
     moments(L)
     if rho_links:
         L.append(f'  {ct} Rr = 0;')             # Σ_j βρ_j v_j over the cell's density-weighted links
-    gq = gq_all if fix else []
     if gq:
         L.append(f'  {ct} ' + ', '.join(f'G{q} = 0' for q in gq) + ';')      # Σ_j J_jq v_j (link programs)
-        # the cell's own pdfs, once: every listed cell has a program link (not per link and row)
-        used = sorted({int(m) for pg in programs if pg is not None for row in pg if row is not None
-                       for _, jl, je in row[2] for m in re.findall(r'\bc(\d+)\b', ' '.join(jl) + ' ' + je)})
-        if used:
-            L.append('  ' + ' '.join(f'const {ct} c{q} = {load("s", "src", q, f"so_{centre}")};' for q in used))
     if mrt is not None:
         # h = Aᵀ g
         for i in range(Q):
@@ -665,9 +686,11 @@ def _emit(stencil, compressible, ctype, walls, target, idx, addr='ptr', links=No
               f'{fs}s_bytes, g_bytes, o_bytes, omega')
     if hip and fix:
         # the fix-up kernel: one thread per listed cell (the fluid cells next to a link-program wall)
-        L.append(f'extern "C" __global__ void __launch_bounds__(256) lbm_adj_fix({sig_adj}, const int* __restrict__ '
+        # one wave per workgroup (FIX_BLOCK lanes): the few listed cells spread over as many CUs as possible — each wave
+        # runs a long, branchy, latency-bound chain, and waves of one CU would share its scalar unit
+        L.append(f'extern "C" __global__ void __launch_bounds__({FIX_BLOCK}) lbm_adj_fix({sig_adj}, const int* __restrict__ '
                  'cells, const int ncell)\n{')
-        L.append('  const int t = (int)(blockIdx.x * 256u + threadIdx.x);')
+        L.append(f'  const int t = (int)(blockIdx.x * {FIX_BLOCK}u + threadIdx.x);')
         L.append('  if (t >= ncell) return;')
         L.append('  const unsigned cell = (unsigned)cells[t];')
         L.append('  const unsigned r = cell / (unsigned)X;')
@@ -940,7 +963,7 @@ class LatticeKernels:
         fn = self._gpu_fn(which + ('_fix' if fix is not None else ''), idx, addr, dev)
         Z, Y, X = self._extent(tensors[0])
         code = 'i' if idx == 'int' else 'q'
-        nblocks = self._blocks(X, Y, Z) if fix is None else -(-int(fix[0].numel()) // 256)
+        nblocks = self._blocks(X, Y, Z) if fix is None else -(-int(fix[0].numel()) // FIX_BLOCK)
         reach = [self._reach(t) * t.element_size() for t in tensors]
         ptrs = [t.data_ptr() for t in tensors] + [mask.data_ptr() if mask is not None else 0,
                                                   ids.data_ptr() if ids is not None else 0]
@@ -958,6 +981,8 @@ class LatticeKernels:
             vals += [fix[0].data_ptr(), int(fix[0].numel())]
         args = _pack(fmt, *vals)
         plan = self._plans[key] = LaunchPlan(fn, nblocks, args, len(ptrs), dev, _offset(fmt, om_i), fmt[om_i])
+        if fix is not None:
+            plan.block = FIX_BLOCK
         return plan
 
     def fix_launch(self, which, tensors, mask, omega, ids, force, dforce, cells, stream):
@@ -1125,12 +1150,13 @@ class LaunchPlan:
     """One lattice kernel launch with its argument buffer; ``plan(ptrs, stream, omega)`` patches the leading pointer
     slots (the pdf arrays, then the neighbour mask) and the relaxation rate, and launches on the plan's device
     (made current for the launch when it is not: the function handle belongs to that device's module)."""
-    __slots__ = ('fn', 'nblocks', 'template', 'fmt', 'device', 'om_off', 'om_fmt', 'extra')
+    __slots__ = ('fn', 'nblocks', 'template', 'fmt', 'device', 'om_off', 'om_fmt', 'extra', 'block')
 
     def __init__(self, fn, nblocks, template, nptr, device, om_off, om_code):
         self.fn, self.nblocks, self.template, self.fmt = fn, nblocks, template, f'<{nptr}Q'
         self.device, self.om_off, self.om_fmt = device, om_off, None if om_code is None else '<' + om_code
         self.extra = None              # byte offset of two more pointer slots patched per launch (second pass)
+        self.block = 256
 
     def __call__(self, ptrs, stream, omega=None, extra=None):
         from ..backends import hip_runtime as rt
@@ -1143,9 +1169,9 @@ class LaunchPlan:
         import torch
         if self.device is not None and self.device != torch.cuda.current_device():
             with torch.cuda.device(self.device):
-                rt.launch(self.fn, (self.nblocks,), (256,), bytes(buf), stream)
+                rt.launch(self.fn, (self.nblocks,), (self.block,), bytes(buf), stream)
         else:
-            rt.launch(self.fn, (self.nblocks,), (256,), bytes(buf), stream)
+            rt.launch(self.fn, (self.nblocks,), (self.block,), bytes(buf), stream)
 
 
 def _stream(stream, t):
