@@ -234,23 +234,28 @@ def test_varcoef_ring_tilings_gpu(params):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('params', [None, dict(WS=0)], ids=['ring_dma', 'ring_registers'])
-def test_varcoef_slab_halos_and_two_range_launches_gpu(params):
+@pytest.mark.parametrize('params,dts', [(None, 'float32'), (dict(WS=0), 'float32'), (None, 'float16'),
+                                        (dict(WS=0, PR=0), 'float16')],
+                         ids=['ring_dma', 'ring_registers', 'ring_dma_f16_pairs', 'ring_registers_f16'])
+def test_varcoef_slab_halos_and_two_range_launches_gpu(params, dts):
     """The z-slab launch pattern on the plane ring, forward and adjoint: halo planes of every stencil field read in
-    place, interior planes first, both faces in one two-range launch == one full-domain launch, bitwise."""
+    place, interior planes first, both faces in one two-range launch == one full-domain launch, bitwise (fp16: the
+    LDS-DMA ring of fp16 images with cell-pair taps, and the register ring)."""
     from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
-    op = _op()
+    op = _op(dts)
+    tdt = torch.float16 if dts == 'float16' else torch.float32
     kf = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='vch_f', target='gpu',
                        gpu_indexing_params=params).compile()
     kb = StencilKernel(op.backward_assignments, boundary_handling='zeros', function_name='vch_b', target='gpu',
                        gpu_indexing_params=params).compile()
     Z = 30
-    u, k, d = _inputs((Z, 21, 136), torch.float32, 'cuda', seed=11)
+    u, k, d = _inputs((Z, 21, 136), tdt, 'cuda', seed=11)
     full = torch.empty_like(u)
     kf(u=u, k=k, out=full)
     fdu, fdk = torch.empty_like(u), torch.empty_like(u)
     kb(u=u, k=k, diffout=d, diffu=fdu, diffk=fdk)
     assert kf.last_variant[1].WS == (params is None) and kb.last_variant[1].WS == (params is None)
+    assert kf.last_variant[1].PR == (dts == 'float16' and params is None)
     outs, dus, dks = [], [], []
     for a, b in [(0, 11), (11, 19), (19, Z)]:
         sl = {n: t[a:b].contiguous() for n, t in (('u', u), ('k', k), ('diffout', d))}
@@ -270,8 +275,9 @@ def test_varcoef_slab_halos_and_two_range_launches_gpu(params):
     assert torch.equal(torch.cat(dus), fdu)
     assert torch.equal(torch.cat(dks), fdk)
     ref, ab = oracle(op, *(x.double().cpu().numpy() for x in (u, k, d)))
-    check(full, ref['out'], ab['out'], False, 'out')
-    check(fdu, ref['diffu'], ab['diffu'], False, 'diffu')
+    check(full, ref['out'], ab['out'], False, 'out', dts == 'float16')
+    check(fdu, ref['diffu'], ab['diffu'], False, 'diffu', dts == 'float16')
+    check(fdk, ref['diffk'], ab['diffk'], False, 'diffk', dts == 'float16')
 
 
 @pytest.mark.gpu
