@@ -321,6 +321,44 @@ def test_plane_ring_radius2_full_ring_fields_gpu(params, dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('shape', [(23, 35, 140), (9, 20, 131)], ids=str)
+def test_fp16_nonlinear_functions_register_ring_gpu(shape):
+    """fp16 storage with a function of the taps (no packed-pair form: ``pair_ok`` is False) keeps the register ring on
+    128×8 tiles (the fp16 LDS-DMA ring needs the pair form) — the radius-2 collection of
+    ``test_plane_ring_radius2_full_ring_fields_gpu`` in fp16, forward and adjoint vs the oracle on the fp16-rounded
+    inputs (bound: fp16 rounding of outputs of magnitude <= a few units)."""
+    import sympy as sp
+    from pystencils_autodiff_amd import ps
+    from pystencils_autodiff_amd.backends.hip_emitter import pair_ok
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    a, b, o1, o2 = ps.fields('a, b, o1, o2: float16[3d]')
+    ac = ps.AssignmentCollection({
+        o1.center: a[0, 0, 2] * b[0, 0, -2] + sp.sin(a[-2, 1, 0]) * b.center + 0.5 * a[1, -1, -1] * a[-1, 2, 0],
+        o2.center: b[2, 0, 1] * b[-1, -2, 0] - a[0, 1, 0] * b[-2, 0, 0]})
+    op = pa.AutoDiffOp(ac, boundary_handling='zeros')
+    g = torch.Generator().manual_seed(31)
+    A, Bf, D1, D2 = (torch.rand(shape, generator=g, dtype=torch.float64).mul(2).sub(1).half().cuda() for _ in range(4))
+    fk = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='h16_f', target='gpu').compile()
+    bk = StencilKernel(op.backward_assignments, boundary_handling='zeros', function_name='h16_b', target='gpu').compile()
+    O1, O2, DA, DB = (torch.zeros_like(A) for _ in range(4))
+    fk(a=A, b=Bf, o1=O1, o2=O2)
+    bk(a=A, b=Bf, diffo1=D1, diffo2=D2, diffa=DA, diffb=DB)
+    torch.cuda.synchronize()
+    for k in (fk, bk):
+        assert not pair_ok(k.ir) and k.last_variant[0] == 'march'
+        assert not k.last_variant[1].WS and not k.last_variant[1].PR and not k.last_variant[1].ZSUM
+    arr = {n: t.double().cpu().numpy() for n, t in (('a', A), ('b', Bf))}
+    ref = {**OE.evaluate(op.forward_assignments, arr, boundary_handling='zeros'),
+           **OE.evaluate(op.backward_assignments, {**arr, 'diffo1': D1.double().cpu().numpy(),
+                                                   'diffo2': D2.double().cpu().numpy()}, boundary_handling='zeros')}
+    for name, got in (('o1', O1), ('o2', O2), ('diffa', DA), ('diffb', DB)):
+        r = ref[name]
+        bound = 2.0 ** -10 * np.abs(r) + 2e-3
+        err = np.abs(got.double().cpu().numpy() - r)
+        assert (err <= bound).all(), f'{name}: worst {err.max():.3e}'
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('mode', ['none', 'time_constant'])
 def test_varcoef_ring_none_mode_and_time_constant_gpu(mode):
     """The plane ring under ``boundary_handling=None`` (interior cells only, the border untouched) and with a
