@@ -260,6 +260,12 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
         cfg.update(CX=2, NR=2)
     if ir.ndim == 2:
         cfg.update(CX=4, WX=1, NR=4, VIEW2D='yx', NT_STORE=False)   # 256×16 tiles (4096²: 0.024 ms, 5.6 TB/s)
+        plans2 = zsum_plan(ir, probe)
+        if plans2 is None or any(pl['rest'] != 0 for pl in plans2):
+            # nonlinear 2-D stencils (one tile per workgroup, nothing to pipeline): 128×8 tiles, more workgroups in
+            # flight — 2-D varcoef 4096² fp32 fwd / bwd 0.52 / 0.51 of 8 TB/s vs 0.49 / 0.38 on 256×16, fp16 0.30 /
+            # 0.35 vs 0.28 / 0.21 (profiles/r06_nl2d.log)
+            cfg.update(CX=2, NR=2)
     if ir.has_index_dims and not ring_ws:
         # vector fields (components interleaved in the plane image) linear off the centre plane: the zsum schedule;
         # narrower tiles keep the image (TX + 2H)·C elements wide (the plane ring picked its tile above)

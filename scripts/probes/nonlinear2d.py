@@ -1,0 +1,69 @@
+"""2-D variable-coefficient diffusion (5-point, nonlinear: ``u + α Σ₄ ½(k + k[nb])(u[nb] − u)``) through the op,
+forward and TF-MAD adjoint kernels timed alone with HIP events (median of 20), fraction of 8 TB/s from the algorithmic
+bytes (fwd 3, bwd 5 fields per cell). Timing only (parity: tests/test_varcoef.py::test_varcoef_2d_gpu_vs_oracle).
+python scripts/probes/nonlinear2d.py [n=4096] [tiles=default,...] [f16]"""
+import os
+import sys
+
+import sympy as sp
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', '..'))
+import pystencils_autodiff_amd as pa  # noqa: E402
+from pystencils_autodiff_amd import ps  # noqa: E402
+from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel  # noqa: E402
+
+TILES = {'default': {}, 'old': dict(CX=4, NR=4), 'cx2nr2': dict(CX=2, NR=2), 'cx4nr2': dict(CX=4, NR=2), 'cx2nr4': dict(CX=2, NR=4),
+         'cx4nr8': dict(CX=4, NR=8), 'cx8nr4': dict(CX=8, NR=4), 'cx4nr4_pr': dict(CX=4, NR=4, PR=1),
+         'cx2nr2_pr': dict(CX=2, NR=2, PR=1), 'cx4nr1': dict(CX=4, NR=1), 'cx2nr8': dict(CX=2, NR=8),
+         'nw1_cx4nr8': dict(NW=1, CX=4, NR=8), 'cx4wx2nr4': dict(CX=4, WX=2, NR=4)}
+
+
+def varcoef2d(dts):
+    u, k, out = ps.fields(f'u, k, out: {dts}[2d]')
+    nb = [(1, 0), (-1, 0), (0, 1), (0, -1)]
+    return ps.AssignmentCollection({out.center: u.center + 0.1 * sp.Add(
+        *[sp.Rational(1, 2) * (k.center + k[o]) * (u[o] - u.center) for o in nb])})
+
+
+def timed(fn, reps=20):
+    for _ in range(5):
+        fn()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    names = sys.argv[2].split(',') if len(sys.argv) > 2 else list(TILES)
+    f16 = len(sys.argv) > 3 and sys.argv[3] == 'f16'
+    dt, es = (torch.float16, 2) if f16 else (torch.float32, 4)
+    op = pa.AutoDiffOp(varcoef2d('float16' if f16 else 'float32'), boundary_handling='zeros')
+    shape = (n, n)
+    u, k, d = (torch.rand(shape, device='cuda').to(dt) for _ in range(3))
+    out, du, dk = (torch.empty(shape, device='cuda', dtype=dt) for _ in range(3))
+    for name in names:
+        p = dict(TILES[name])
+        fk = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='v2f', target='gpu',
+                           gpu_indexing_params=p or None).compile()
+        bk = StencilKernel(op.backward_assignments, boundary_handling='zeros', function_name='v2b', target='gpu',
+                           gpu_indexing_params=p or None).compile()
+        tf = timed(lambda: fk(u=u, k=k, out=out))
+        tb = timed(lambda: bk(u=u, k=k, diffout=d, diffu=du, diffk=dk))
+        v = fk.last_variant
+        print(f'varcoef2d {n}^2 {"f16" if f16 else "f32"} {name:12s} fwd {tf * 1e3:.1f} us ({3 * es * n * n / tf / 1e6 / 8000:.3f})  '
+              f'bwd {tb * 1e3:.1f} us ({5 * es * n * n / tb / 1e6 / 8000:.3f})  {v[0]} '
+              f'{dict(CX=v[1].CX, NR=v[1].NR, WS=v[1].WS, PR=v[1].PR) if len(v) > 1 and hasattr(v[1], "CX") else ""}',
+              flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -320,6 +320,33 @@ def test_plane_ring_radius2_full_ring_fields_gpu(params, dtype):
         np.testing.assert_allclose(got.double().cpu().numpy(), ref[name], rtol=tol, atol=tol * 4, err_msg=name)
 
 
+def _varcoef2d(dts):
+    u, k, out = ps.fields(f'u, k, out: {dts}[2d]')
+    nb = [(1, 0), (-1, 0), (0, 1), (0, -1)]
+    return ps.AssignmentCollection({out.center: u.center + 0.1 * sp.Add(
+        *[sp.Rational(1, 2) * (k.center + k[o]) * (u[o] - u.center) for o in nb])})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dts', ['float32', 'float16'])
+@pytest.mark.parametrize('shape', [(100, 300), (37, 129), (5, 3), (64, 256)], ids=str)
+def test_varcoef_2d_gpu_vs_oracle(dts, shape):
+    """2-D variable-coefficient diffusion (nonlinear 5-point; the register ring on 128×8 tiles, one tile per
+    workgroup) through the drop-in Function, forward and TF-MAD adjoint vs the oracle, cell by cell."""
+    op = pa.AutoDiffOp(_varcoef2d(dts), boundary_handling='zeros')
+    tdt = torch.float16 if dts == 'float16' else torch.float32
+    u, k, d = _inputs(shape, tdt, 'cuda', seed=23)
+    out, gu, gk = _apply(op, u, k, d, 'cuda')
+    fk, bk = op.forward_ast_gpu.compile(), op.backward_ast_gpu.compile()
+    for kk in (fk, bk):
+        if shape[1] * (2 if dts == 'float16' else 4) % 16 == 0:      # rows of whole 16-byte vectors: the ring
+            assert kk.last_variant[0] == 'march' and (kk.last_variant[1].CX, kk.last_variant[1].NR) in ((2, 2), (1, 2))
+    ref, ab = oracle(op, *(x.double().cpu().numpy() for x in (u, k, d)))
+    check(out, ref['out'], ab['out'], False, f'{shape} out', dts == 'float16')
+    check(gu, ref['diffu'], ab['diffu'], False, f'{shape} diffu', dts == 'float16')
+    check(gk, ref['diffk'], ab['diffk'], False, f'{shape} diffk', dts == 'float16')
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize('shape', [(23, 35, 140), (9, 20, 131)], ids=str)
 def test_fp16_nonlinear_functions_register_ring_gpu(shape):
