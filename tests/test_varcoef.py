@@ -348,6 +348,32 @@ def test_varcoef_2d_gpu_vs_oracle(dts, shape):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('dts', ['float32', 'float16'])
+@pytest.mark.parametrize('shape', [(64, 256), (37, 136), (9, 520)], ids=str)
+def test_varcoef_2d_pairs_gpu(dts, shape):
+    """The packed-pair form (``PR=1``) on a 2-D field (one (1, Y, X) plane on the register ring), forward and adjoint
+    kernels vs the oracle, cell by cell."""
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    op = pa.AutoDiffOp(_varcoef2d(dts), boundary_handling='zeros')
+    tdt = torch.float16 if dts == 'float16' else torch.float32
+    u, k, d = _inputs(shape, tdt, 'cuda', seed=29)
+    fk = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='v2p_f', target='gpu',
+                       gpu_indexing_params=dict(PR=1)).compile()
+    bk = StencilKernel(op.backward_assignments, boundary_handling='zeros', function_name='v2p_b', target='gpu',
+                       gpu_indexing_params=dict(PR=1)).compile()
+    out, du, dk = (torch.full_like(u, float('nan')) for _ in range(3))
+    fk(u=u, k=k, out=out)
+    bk(u=u, k=k, diffout=d, diffu=du, diffk=dk)
+    torch.cuda.synchronize()
+    for kk in (fk, bk):
+        assert kk.last_variant[0] == 'march' and kk.last_variant[1].PR
+    ref, ab = oracle(op, *(x.double().cpu().numpy() for x in (u, k, d)))
+    check(out, ref['out'], ab['out'], False, f'{shape} out', dts == 'float16')
+    check(du, ref['diffu'], ab['diffu'], False, f'{shape} diffu', dts == 'float16')
+    check(dk, ref['diffk'], ab['diffk'], False, f'{shape} diffk', dts == 'float16')
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('shape', [(23, 35, 140), (9, 20, 131)], ids=str)
 def test_fp16_nonlinear_functions_register_ring_gpu(shape):
     """fp16 storage with a function of the taps (no packed-pair form: ``pair_ok`` is False) keeps the register ring on
