@@ -242,9 +242,17 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             two = len(ir.stencil_fields) <= 2
             tiles = [(2, 2 if two else 1)]
             cfg['PR'] = 1
+        half_vec = ir.has_index_dims and any(storage_ctype(f) == '_Float16' for f in ir.stencil_fields)
+        if half_vec:
+            # vector fields in fp16 (each tap one half, converted): 128×8 tiles, eight compute waves when the ring holds
+            # more than one field (the adjoint). Advection u(3) 256³ fwd / bwd 0.063 / 0.063 ms vs 0.139 / 0.069 on
+            # the widest fitting tile (256×16) and 0.131 / 0.153 one thread per cell (profiles/r06_vec16_tiles.log)
+            tiles = [(2, 2)]
         for cx, nr in tiles:
             c = {**cfg, 'CX': cx, 'NR': nr, 'WS': True, 'D': 2 if nr == 2 or not cfg.get('PR') else 3, 'ZMIN': 8,
                  'ZMAX': 128, 'BLK': 256}
+            if half_vec and len(ir.stencil_fields) > 1:
+                c['NW'] = 8
             w = ws_geometry(ir, MarchConfig(VE=ve, **c))
             if w is not None and w['lds_bytes'] <= 160 * 1024:
                 cfg.update(c)

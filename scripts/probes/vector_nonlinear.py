@@ -14,15 +14,17 @@ from pystencils_autodiff_amd import ps  # noqa: E402
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-    u, out = ps.fields('u(3), out(3): float32[3d]')
+    dts = sys.argv[2] if len(sys.argv) > 2 else 'float32'
+    tdt = getattr(torch, dts)
+    u, out = ps.fields(f'u(3), out(3): {dts}[3d]')
     e = [(1, 0, 0), (0, 1, 0), (0, 0, 1)]
     m = [(-1, 0, 0), (0, -1, 0), (0, 0, -1)]
     ac = ps.AssignmentCollection({out.center(c): u.center(c) - 0.05 * sp.Add(
         *[u.center(d) * (u[e[d]](c) - u[m[d]](c)) / 2 for d in range(3)]) for c in range(3)})
     op = pa.AutoDiffOp(ac, boundary_handling='zeros')
     fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
-    x = torch.rand((n, n, n, 3), device='cuda').requires_grad_(True)
-    g = torch.rand((n, n, n, 3), device='cuda')
+    x = torch.rand((n, n, n, 3), device='cuda').to(tdt).requires_grad_(True)
+    g = torch.rand((n, n, n, 3), device='cuda').to(tdt)
     for _ in range(5):
         (o,) = fn.apply(x)
         o.backward(g)
@@ -41,9 +43,9 @@ def main():
         bw.append(ev[1].elapsed_time(ev[2]))
     fw.sort()
     bw.sort()
-    b = n ** 3 * 3 * 4
-    print(f'vector advection {n}^3x3 fp32: fwd {fw[10]:.4f} ms ({2 * b / fw[10] / 1e6 / 8000:.3f} of 8 TB/s at 24 B/cell), '
-          f'bwd {bw[10]:.4f} ms ({3 * b / bw[10] / 1e6 / 8000:.3f} at 36 B/cell); schedules '
+    b = n ** 3 * 3 * tdt.itemsize
+    print(f'vector advection {n}^3x3 {dts}: fwd {fw[10]:.4f} ms ({2 * b / fw[10] / 1e6 / 8000:.3f} of 8 TB/s), '
+          f'bwd {bw[10]:.4f} ms ({3 * b / bw[10] / 1e6 / 8000:.3f}); schedules '
           f'{op.forward_ast_gpu.compile().last_variant[0]} / {op.backward_ast_gpu.compile().last_variant[0]}', flush=True)
 
 

@@ -580,29 +580,36 @@ def test_vector_nonlinear_takes_the_plane_ring():
     from pystencils_autodiff_amd.backends import hip_runtime as rt
     from pystencils_autodiff_amd.backends.hip_kernel import HipStencilKernel
     from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
-    op = pa.AutoDiffOp(_advection(), boundary_handling='zeros')
-    assert [str(a.lhs) for a in op.backward_assignments.main_assignments] == ['\\hat{u}[0,0,0,2]']   # the quirk
-    for asg in (op.forward_assignments, op.backward_assignments):
-        hk = HipStencilKernel(StencilKernel(asg, boundary_handling='zeros', function_name='advr', target='gpu'))
-        assert hk.schedule() == 'march'
-        cfg = hk._march_cfg(4, (64, 64, 256))
-        assert cfg.WS and not cfg.ZSUM, cfg
-        src = hk.source(('march', cfg))[0]
-        assert 'LDS-DMA loader wave' in src and len(rt.compile_hip(src)) > 0
+    for dts, ve in (('float32', 4), ('float16', 8)):
+        op = pa.AutoDiffOp(_advection(dts), boundary_handling='zeros')
+        assert [str(a.lhs) for a in op.backward_assignments.main_assignments] == ['\\hat{u}[0,0,0,2]']   # the quirk
+        for asg in (op.forward_assignments, op.backward_assignments):
+            hk = HipStencilKernel(StencilKernel(asg, boundary_handling='zeros', function_name='advr', target='gpu'))
+            assert hk.schedule() == 'march'
+            cfg = hk._march_cfg(ve, (64, 64, 256))
+            assert cfg.WS and not cfg.ZSUM, cfg
+            if dts == 'float16':          # fp16 images in the ring: 128×8 tiles, 8 compute waves for two ring fields
+                assert (cfg.CX, cfg.NR, cfg.NW) == (2, 2, 4 if asg is op.forward_assignments else 8), cfg
+            src = hk.source(('march', cfg))[0]
+            assert 'LDS-DMA loader wave' in src and len(rt.compile_hip(src)) > 0
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('shape', [(17, 33, 45), (9, 20, 128), (40, 64, 256), (5, 7, 3), (33, 50, 130),
                                    (21, 30, 132), (70, 9, 264)])
 @pytest.mark.parametrize('bh', ['zeros', None])
-def test_vector_advection_ring_gpu_vs_oracle(shape, bh):
+@pytest.mark.parametrize('dts', ['float32', 'float16'])
+def test_vector_advection_ring_gpu_vs_oracle(shape, bh, dts):
     """The advection op through the drop-in Function on the vector plane ring, forward and TF-MAD adjoint vs the
-    float64 oracle, cell by cell (``check``: 1e-6·|ref| + 32·2⁻²⁴·Σ|terms|), both boundary modes; the adjoint's
-    first two components are the zeros of the reference's last-component quirk (``_autodiff.py:138-152``)."""
-    op = pa.AutoDiffOp(_advection(), boundary_handling=bh)
+    float64 oracle, cell by cell (``check``: 1e-6·|ref| + 32·2⁻²⁴·Σ|terms|, plus half an fp16 ulp of the stored
+    result for fp16 fields), both boundary modes; the adjoint's first two components are the zeros of the
+    reference's last-component quirk (``_autodiff.py:138-152``). fp16 fields: the ring holds fp16 plane images, each
+    tap read as one half and converted (128×8 tiles, eight compute waves for the adjoint's two ring fields)."""
+    op = pa.AutoDiffOp(_advection(dts), boundary_handling=bh)
+    tdt = getattr(torch, dts)
     g = torch.Generator().manual_seed(sum(shape))
-    u = (torch.rand(shape + (3,), generator=g, dtype=torch.float64) * 2 - 1).float()
-    d = (torch.rand(shape + (3,), generator=g, dtype=torch.float64) * 2 - 1).float()
+    u = (torch.rand(shape + (3,), generator=g, dtype=torch.float64) * 2 - 1).to(tdt)
+    d = (torch.rand(shape + (3,), generator=g, dtype=torch.float64) * 2 - 1).to(tdt)
     fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
     uu = u.cuda().requires_grad_(True)
     (out,) = fn.apply(uu)
@@ -610,24 +617,29 @@ def test_vector_advection_ring_gpu_vs_oracle(shape, bh):
     torch.cuda.synchronize()
     fk, bk = op.forward_ast_gpu.compile(), op.backward_ast_gpu.compile()
     for k in (fk, bk):
-        if shape[2] % 4 == 0:             # rows of whole 16-byte pieces (the others: one thread per cell)
+        if (shape[2] * 3 * tdt.itemsize) % 16 == 0:   # rows of whole 16-byte pieces (the others: one thread per cell)
             assert k.last_variant[0] == 'march' and k.last_variant[1].WS and not k.last_variant[1].ZSUM, k.last_variant
+            if dts == 'float16':
+                assert k.last_variant[1].NW == (8 if k is bk else 4), k.last_variant
     ref, ab = _adv_oracle(op, bh, u.double().numpy(), d.double().numpy())
-    check(out, ref['out'], ab['out'], False, f'{shape} {bh} out')
-    check(uu.grad, ref['diffu'], ab['diffu'], False, f'{shape} {bh} diffu')
+    half = dts == 'float16'
+    check(out, ref['out'], ab['out'], False, f'{shape} {bh} {dts} out', fp16=half)
+    check(uu.grad, ref['diffu'], ab['diffu'], False, f'{shape} {bh} {dts} diffu', fp16=half)
     assert not uu.grad[..., :2].any()
 
 
 @pytest.mark.gpu
-def test_vector_advection_ring_tilings_and_slab_gpu():
+@pytest.mark.parametrize('dts', ['float32', 'float16'])
+def test_vector_advection_ring_tilings_and_slab_gpu(dts):
     """Other ring tilings of the vector advection (8 compute waves, depth 1 and 3) and the z-slab launch pattern
-    (interior z range, then both faces in one launch reading halo planes in place) bitwise equal to one full launch."""
+    (interior z range, then both faces in one launch reading halo planes in place) bitwise equal to one full launch;
+    fp32 and fp16 fields."""
     from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
     from pystencils_autodiff_amd.zslab import ZSlabOp
-    op = pa.AutoDiffOp(_advection(), boundary_handling='zeros')
+    op = pa.AutoDiffOp(_advection(dts), boundary_handling='zeros')
     shape = (23, 37, 200)
     g = torch.Generator().manual_seed(4)
-    u = (torch.rand(shape + (3,), generator=g) * 2 - 1).cuda()
+    u = (torch.rand(shape + (3,), generator=g) * 2 - 1).to(getattr(torch, dts)).cuda()
     ref, ab = _adv_oracle(op, 'zeros', u.double().cpu().numpy(), np.zeros(shape + (3,)))
     for params in (dict(WS=1, NW=8, CX=2, NR=1, D=2), dict(WS=1, CX=1, NR=4, D=1), dict(WS=1, CX=2, NR=2, D=3)):
         k = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='advt', target='gpu',
@@ -636,7 +648,7 @@ def test_vector_advection_ring_tilings_and_slab_gpu():
         k(u=u, out=out)
         torch.cuda.synchronize()
         assert k.last_variant[1].WS and not k.last_variant[1].ZSUM
-        check(out, ref['out'], ab['out'], False, f'{params} out')
+        check(out, ref['out'], ab['out'], False, f'{params} {dts} out', fp16=dts == 'float16')
     k = op.forward_ast_gpu.compile()
     full = torch.zeros_like(u)
     k(u=u, out=full)
