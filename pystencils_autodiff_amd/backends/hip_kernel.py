@@ -244,10 +244,15 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             cfg['PR'] = 1
         half_vec = ir.has_index_dims and any(storage_ctype(f) == '_Float16' for f in ir.stencil_fields)
         if half_vec:
-            # vector fields in fp16 (each tap one half, converted): 128×8 tiles, eight compute waves when the ring holds
-            # more than one field (the adjoint). Advection u(3) 256³ fwd / bwd 0.063 / 0.063 ms vs 0.139 / 0.069 on
-            # the widest fitting tile (256×16) and 0.131 / 0.153 one thread per cell (profiles/r06_vec16_tiles.log)
+            # vector fields in fp16 (fp16 images, taps converted): 128×8 tiles. Lanes own x-adjacent cell pairs with
+            # packed fp32 statements (PR) where the statements allow — a lane's elements are then contiguous from an
+            # even offset and its reads merge; eight compute waves for the adjoint's two ring fields. Advection u(3)
+            # 256³ fwd / bwd 0.052 / 0.054 ms vs 0.063 / 0.063 per cell, 0.139 / 0.069 on the widest fitting tile
+            # (256×16), 0.131 / 0.153 one thread per cell (profiles/r06_vec16_tiles.log, r06_vec16_pairs.log; fp32
+            # vector fields measured slower as pairs: 0.075 / 0.12 vs 0.071 / 0.095)
             tiles = [(2, 2)]
+            if pair_ok(ir, vectors=True):
+                cfg['PR'] = 1
         for cx, nr in tiles:
             c = {**cfg, 'CX': cx, 'NR': nr, 'WS': True, 'D': 2 if nr == 2 or not cfg.get('PR') else 3, 'ZMIN': 8,
                  'ZMAX': 128, 'BLK': 256}
@@ -307,6 +312,8 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             cfg[k] = str(v)
         elif k in ('SFAST', 'SLP', 'PR', 'PD'):
             cfg[k] = int(v)
+    if cfg.get('PR') and 'PR' not in over and (cfg['CX'] % 2 or not pair_ok(ir, vectors=bool(cfg.get('WS')))):
+        cfg['PR'] = 0          # a tile override the default pair form cannot take (odd CX; vector fields off the ring)
     if ring_ws and PROBE_KNOBS.get('BABL'):
         cfg['BABL'] = int(PROBE_KNOBS['BABL'])   # (timing probe of the march ring, as on the band: 3 = no plane loads)
     bc = _band_config(ir, ve, shape, over) if band else None

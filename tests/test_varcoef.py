@@ -588,8 +588,8 @@ def test_vector_nonlinear_takes_the_plane_ring():
             assert hk.schedule() == 'march'
             cfg = hk._march_cfg(ve, (64, 64, 256))
             assert cfg.WS and not cfg.ZSUM, cfg
-            if dts == 'float16':          # fp16 images in the ring: 128×8 tiles, 8 compute waves for two ring fields
-                assert (cfg.CX, cfg.NR, cfg.NW) == (2, 2, 4 if asg is op.forward_assignments else 8), cfg
+            if dts == 'float16':          # fp16 images in the ring: 128×8 tiles of x-adjacent cell pairs
+                assert (cfg.CX, cfg.NR, cfg.NW, cfg.PR) == (2, 2, 4 if asg is op.forward_assignments else 8, 1), cfg
             src = hk.source(('march', cfg))[0]
             assert 'LDS-DMA loader wave' in src and len(rt.compile_hip(src)) > 0
 
@@ -603,8 +603,8 @@ def test_vector_advection_ring_gpu_vs_oracle(shape, bh, dts):
     """The advection op through the drop-in Function on the vector plane ring, forward and TF-MAD adjoint vs the
     float64 oracle, cell by cell (``check``: 1e-6·|ref| + 32·2⁻²⁴·Σ|terms|, plus half an fp16 ulp of the stored
     result for fp16 fields), both boundary modes; the adjoint's first two components are the zeros of the
-    reference's last-component quirk (``_autodiff.py:138-152``). fp16 fields: the ring holds fp16 plane images, each
-    tap read as one half and converted (128×8 tiles, eight compute waves for the adjoint's two ring fields)."""
+    reference's last-component quirk (``_autodiff.py:138-152``). fp16 fields: the ring holds fp16 plane images, lanes
+    own x-adjacent cell pairs evaluated as packed fp32 (``PR``), 128×8 tiles, eight compute waves for the adjoint."""
     op = pa.AutoDiffOp(_advection(dts), boundary_handling=bh)
     tdt = getattr(torch, dts)
     g = torch.Generator().manual_seed(sum(shape))
@@ -620,7 +620,7 @@ def test_vector_advection_ring_gpu_vs_oracle(shape, bh, dts):
         if (shape[2] * 3 * tdt.itemsize) % 16 == 0:   # rows of whole 16-byte pieces (the others: one thread per cell)
             assert k.last_variant[0] == 'march' and k.last_variant[1].WS and not k.last_variant[1].ZSUM, k.last_variant
             if dts == 'float16':
-                assert k.last_variant[1].NW == (8 if k is bk else 4), k.last_variant
+                assert k.last_variant[1].PR and k.last_variant[1].NW == (8 if k is bk else 4), k.last_variant
     ref, ab = _adv_oracle(op, bh, u.double().numpy(), d.double().numpy())
     half = dts == 'float16'
     check(out, ref['out'], ab['out'], False, f'{shape} {bh} {dts} out', fp16=half)
@@ -641,13 +641,16 @@ def test_vector_advection_ring_tilings_and_slab_gpu(dts):
     g = torch.Generator().manual_seed(4)
     u = (torch.rand(shape + (3,), generator=g) * 2 - 1).to(getattr(torch, dts)).cuda()
     ref, ab = _adv_oracle(op, 'zeros', u.double().cpu().numpy(), np.zeros(shape + (3,)))
-    for params in (dict(WS=1, NW=8, CX=2, NR=1, D=2), dict(WS=1, CX=1, NR=4, D=1), dict(WS=1, CX=2, NR=2, D=3)):
+    for params in (dict(WS=1, NW=8, CX=2, NR=1, D=2), dict(WS=1, CX=1, NR=4, D=1), dict(WS=1, CX=2, NR=2, D=3),
+                   dict(WS=1, CX=4, NR=2, PR=1), dict(WS=1, CX=2, NR=2, PR=0)):    # cell pairs on and off
         k = StencilKernel(op.forward_assignments, boundary_handling='zeros', function_name='advt', target='gpu',
                           gpu_indexing_params=params).compile()
         out = torch.full_like(u, float('nan'))
         k(u=u, out=out)
         torch.cuda.synchronize()
         assert k.last_variant[1].WS and not k.last_variant[1].ZSUM
+        # (fp16: the default pair form, which yields to an odd CX)
+        assert k.last_variant[1].PR == params.get('PR', int(dts == 'float16' and params['CX'] % 2 == 0)), params
         check(out, ref['out'], ab['out'], False, f'{params} {dts} out', fp16=dts == 'float16')
     k = op.forward_ast_gpu.compile()
     full = torch.zeros_like(u)
