@@ -229,7 +229,7 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             # profiles/r02_tune_small_*.log)
             cfg.update(WS=True, CX=4, NR=8 if ws0['kind'] == 'h' else 4, D=4, ZMIN=8, ZMAX=128, BLK=256)
             star_ws = True
-    ring_ws = False
+    ring_ws = False                       # (the LDS-DMA plane ring of nonlinear stencils, 3-D or 2-D along axis 0)
     if ir.ndim == 3 and not zsum_ok:
         # stencils not linear off the centre plane (products / functions of neighbour taps): the plane ring fed by
         # an LDS-DMA loader wave, 2 planes in flight, the widest tile whose ring fits the LDS
@@ -279,6 +279,19 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             # flight — 2-D varcoef 4096² fp32 fwd / bwd 0.52 / 0.51 of 8 TB/s vs 0.49 / 0.38 on 256×16, fp16 0.30 /
             # 0.35 vs 0.28 / 0.21 (profiles/r06_nl2d.log)
             cfg.update(CX=2, NR=2)
+            # ... and on long 16-byte-piece rows: march along axis 0 (VIEW2D='zy', rows as the planes of the LDS-DMA
+            # ring, four waves side by side in x: 512-cell row strips; fp16 as x-adjacent cell pairs), 512 / 1024
+            # workgroups of 64 / 32 rows at 4096²: 2-D varcoef 4096² fp32 fwd / bwd 0.61 / 0.57–0.58 of 8 TB/s,
+            # fp16 0.40–0.42 / 0.49 (profiles/r06_nl2d_zy.log: 40 tilings and chunkings; the register ring along
+            # axis 0 was slower, 0.41 / 0.41, and 128-row chunks 0.51 / 0.49)
+            half2 = any(storage_ctype(f) == '_Float16' for f in ir.stencil_fields)
+            zy = dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=2, WS=True, D=2, ZMIN=16 if half2 else 32, ZMAX=64,
+                      BLK=1024 if half2 else 512, PR=1 if half2 and pair_ok(ir) else 0)
+            if ir.stencil_fields and (shape is None or int(shape[-1]) >= 64 * zy['CX'] * zy['WX']):
+                w = ws_geometry(ir, MarchConfig(VE=ve, **{**cfg, **zy}))
+                if w is not None and w['lds_bytes'] <= 160 * 1024:
+                    cfg.update(zy)
+                    ring_ws = True
     if ir.has_index_dims and not ring_ws:
         # vector fields (components interleaved in the plane image) linear off the centre plane: the zsum schedule;
         # narrower tiles keep the image (TX + 2H)·C elements wide (the plane ring picked its tile above)
@@ -301,6 +314,8 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             over[k.strip()] = v.strip() if k.strip() == 'VIEW2D' else int(v)
     if ring_ws and any(k in over for k in ('CX', 'WX', 'NR', 'NW')) and 'WS' not in over:
         cfg.update(WS=False, D=3)           # a tile override on the ring: the register-prefetch form it was sized for
+        if ir.ndim == 2 and 'VIEW2D' not in over:
+            cfg.update(VIEW2D='yx', NW=4, WX=1, PR=0, ZMIN=32, ZMAX=64, BLK=512)   # (... the 2-D one: (1, Y, X) tiles)
     for k, v in over.items():
         if k not in TILE_KEYS:
             raise ValueError(f"unknown tile parameter '{k}' (gpu_indexing_params / PSAD_MARCH)")
@@ -788,7 +803,10 @@ class HipStencilKernel:
         # workgroups per CU it can pick an unbalanced grid (512³ D=3: 0.249 vs 0.188 ms), so those keep
         # the block-count target
         overridden = any(k in self.kernel.tuning for k in ('CX', 'NR', 'D', 'WX', 'NW'))
-        if slots and cfg.WS and nz and not explicit and (slots <= cus or not overridden):
+        # (not for the 2-D row ring, whose block-count target measured faster: 2-D varcoef 4096² fp32 adjoint 0.072 vs
+        # 0.085 ms, profiles/r06_nl2d_zy.log)
+        rows2d = ir.ndim == 2 and not cfg.ZSUM
+        if slots and cfg.WS and nz and not explicit and (slots <= cus or not overridden) and not rows2d:
             ws = ws_geometry(ir, cfg)
             # workgroups that saturate HBM: ~64 KiB in flight per CU (one 256×16 fp32 ring of 4 planes)
             wsat = max(cus, math.ceil(cus * 65536 / (ws['D'] * ws['per_plane'] * 1024)))

@@ -16,7 +16,39 @@ from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel  # noqa: E4
 TILES = {'default': {}, 'old': dict(CX=4, NR=4), 'cx2nr2': dict(CX=2, NR=2), 'cx4nr2': dict(CX=4, NR=2), 'cx2nr4': dict(CX=2, NR=4),
          'cx4nr8': dict(CX=4, NR=8), 'cx8nr4': dict(CX=8, NR=4), 'cx4nr4_pr': dict(CX=4, NR=4, PR=1),
          'cx2nr2_pr': dict(CX=2, NR=2, PR=1), 'cx4nr1': dict(CX=4, NR=1), 'cx2nr8': dict(CX=2, NR=8),
-         'nw1_cx4nr8': dict(NW=1, CX=4, NR=8), 'cx4wx2nr4': dict(CX=4, WX=2, NR=4)}
+         'nw1_cx4nr8': dict(NW=1, CX=4, NR=8), 'cx4wx2nr4': dict(CX=4, WX=2, NR=4),
+         # march along axis 0 (VIEW2D='zy': rows are the ring's planes), waves side by side in x
+         'zy_cx1': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=1), 'zy_cx2': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=2),
+         'zy_cx4': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=4), 'zy_wx2': dict(VIEW2D='zy', NR=1, NW=2, WX=2, CX=2),
+         'zy_cx2_pr': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=2, PR=1),
+         # ... fed by the LDS-DMA loader wave (WS)
+         'zyws_cx2': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=2, WS=1, D=2),
+         'zyws_cx1': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=1, WS=1, D=2),
+         'zyws_cx4': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=4, WS=1, D=2),
+         'zyws_d4': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=2, WS=1, D=4),
+         'zyws_nw8': dict(VIEW2D='zy', NR=1, NW=8, WX=8, CX=1, WS=1, D=2),
+         'zyws_nw8c2': dict(VIEW2D='zy', NR=1, NW=8, WX=8, CX=2, WS=1, D=2),
+         'zyws_pr': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=2, WS=1, D=2, PR=1),
+         'zyws_pr4': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=4, WS=1, D=2, PR=1),
+         'zyws_pr8': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=8, WS=1, D=2, PR=1),
+         'zyws_pr4d3': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=4, WS=1, D=3, PR=1),
+         'zyws_pr4d1': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=4, WS=1, D=1, PR=1),
+         'zyws_pr_nw8': dict(VIEW2D='zy', NR=1, NW=8, WX=8, CX=2, WS=1, D=2, PR=1),
+         'zyws_pr4_nw8': dict(VIEW2D='zy', NR=1, NW=8, WX=8, CX=4, WS=1, D=2, PR=1),
+         'zyws_pr4_wx2': dict(VIEW2D='zy', NR=1, NW=2, WX=2, CX=4, WS=1, D=2, PR=1),
+         'zyws_nw8c4': dict(VIEW2D='zy', NR=1, NW=8, WX=8, CX=4, WS=1, D=2),
+         'zyws_nw8d3': dict(VIEW2D='zy', NR=1, NW=8, WX=8, CX=2, WS=1, D=3),
+         'zyws_cx8': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=8, WS=1, D=2),
+         # chunking along axis 0 (rows per workgroup): ZMIN / ZMAX / BLK
+         'zyws_c32': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=2, WS=1, D=2, ZMIN=32, ZMAX=64, BLK=512),
+         'zyws_c8': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=2, WS=1, D=2, ZMIN=8, ZMAX=128, BLK=256),
+         'zyws_c16': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=2, WS=1, D=2, ZMIN=16, ZMAX=64, BLK=1024),
+         'zyws_c64': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=2, WS=1, D=2, ZMIN=64, ZMAX=128, BLK=256),
+         'zyws_c128': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=2, WS=1, D=2, ZMIN=128, ZMAX=256, BLK=256),
+         'zyws_pr4_c32': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=4, WS=1, D=2, PR=1, ZMIN=32, ZMAX=64, BLK=512),
+         'zyws_pr4_c8': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=4, WS=1, D=2, PR=1, ZMIN=8, ZMAX=128, BLK=256),
+         'zyws_pr4_c64': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=4, WS=1, D=2, PR=1, ZMIN=64, ZMAX=128, BLK=256),
+         'zyws_pr4_c128': dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=4, WS=1, D=2, PR=1, ZMIN=128, ZMAX=256, BLK=256)}
 
 
 def varcoef2d(dts):
@@ -59,9 +91,14 @@ def main():
         tf = timed(lambda: fk(u=u, k=k, out=out))
         tb = timed(lambda: bk(u=u, k=k, diffout=d, diffu=du, diffk=dk))
         v = fk.last_variant
+        got = [t.float().clone() for t in (out, du, dk)]
+        if name == names[0]:
+            first = got            # (the first tiling's results: the others are compared with them)
+        dev = max(float((a - b).abs().max() / (b.abs().max() + 1e-30)) for a, b in zip(got, first))
         print(f'varcoef2d {n}^2 {"f16" if f16 else "f32"} {name:12s} fwd {tf * 1e3:.1f} us ({3 * es * n * n / tf / 1e6 / 8000:.3f})  '
               f'bwd {tb * 1e3:.1f} us ({5 * es * n * n / tb / 1e6 / 8000:.3f})  {v[0]} '
-              f'{dict(CX=v[1].CX, NR=v[1].NR, WS=v[1].WS, PR=v[1].PR) if len(v) > 1 and hasattr(v[1], "CX") else ""}',
+              f'{dict(CX=v[1].CX, NR=v[1].NR, WS=v[1].WS, PR=v[1].PR, V=v[1].VIEW2D) if len(v) > 1 and hasattr(v[1], "CX") else ""}'
+              f'  rel.dev {dev:.1e}',
               flush=True)
 
 

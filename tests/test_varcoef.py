@@ -349,6 +349,88 @@ def test_varcoef_2d_gpu_vs_oracle(dts, shape):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('dts', ['float32', 'float16'])
+@pytest.mark.parametrize('shape', [(40, 1024), (23, 1160), (3, 2048), (130, 520)], ids=str)
+def test_varcoef_2d_row_ring_gpu(dts, shape):
+    """2-D nonlinear stencils on long rows march along axis 0 (``VIEW2D='zy'``: rows are the planes of the LDS-DMA
+    ring; fp16 as x-adjacent cell pairs): forward and adjoint through the drop-in Function vs the oracle, cell by cell,
+    on whole and ragged tiles and fewer rows than a chunk; then the z-slab launch pattern (interior rows, then both
+    faces reading halo rows in place) bitwise equal to one full launch."""
+    from pystencils_autodiff_amd.zslab import ZSlabOp
+    op = pa.AutoDiffOp(_varcoef2d(dts), boundary_handling='zeros')
+    tdt = torch.float16 if dts == 'float16' else torch.float32
+    u, k, d = _inputs(shape, tdt, 'cuda', seed=31)
+    out, gu, gk = _apply(op, u, k, d, 'cuda')
+    fk, bk = op.forward_ast_gpu.compile(), op.backward_ast_gpu.compile()
+    row_ring = shape[1] >= 512
+    for kk in (fk, bk):
+        c = kk.last_variant[1]
+        assert kk.last_variant[0] == 'march' and (c.VIEW2D == 'zy' and c.WS) == row_ring, kk.last_variant
+        assert bool(c.PR) == (row_ring and dts == 'float16'), kk.last_variant
+    ref, ab = oracle(op, *(x.double().cpu().numpy() for x in (u, k, d)))
+    check(out, ref['out'], ab['out'], False, f'{shape} out', dts == 'float16')
+    check(gu, ref['diffu'], ab['diffu'], False, f'{shape} diffu', dts == 'float16')
+    check(gk, ref['diffk'], ab['diffk'], False, f'{shape} diffk', dts == 'float16')
+    if shape[0] < 8 or not row_ring:
+        return
+    full = torch.zeros_like(u)
+    fk(u=u, k=k, out=full)
+    outs, Z = [], shape[0]
+    cuts = [0, Z // 3, 2 * Z // 3, Z]
+    for a, b in zip(cuts, cuts[1:]):
+        sl = {n: t[a:b].contiguous() for n, t in (('u', u), ('k', k))}
+        o = torch.zeros_like(sl['u'])
+        halos = {n: (t[a - 1:a].contiguous() if a > 0 else None, t[b:b + 1].contiguous() if b < Z else None)
+                 for n, t in (('u', u), ('k', k))}
+        inner, faces = ZSlabOp._launches(b - a, 1, (0, b - a))
+        if inner:
+            fk(u=sl['u'], k=sl['k'], out=o, z_range=inner)
+        ZSlabOp._launch_faces(fk, halos, faces, None, {**sl, 'out': o})
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(outs), full)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dts', ['float32', 'float16'])
+@pytest.mark.parametrize('mode', ['none', 'time_constant'])
+def test_varcoef_2d_row_ring_none_mode_and_time_constant_gpu(mode, dts):
+    """The 2-D row ring (``VIEW2D='zy'``) under ``boundary_handling=None`` (NaN-poisoned border rows and columns left
+    untouched) and with a time-constant conductivity (``diffk`` accumulated), vs the oracle."""
+    f16 = dts == 'float16'
+    tdt = torch.float16 if f16 else torch.float32
+    bh = None if mode == 'none' else 'zeros'
+    ac = _varcoef2d(dts)
+    kfield = next(f for f in ac.free_symbols if hasattr(f, 'field') and f.field.name == 'k').field
+    op = pa.AutoDiffOp(ac, boundary_handling=bh, time_constant_fields=[kfield] if mode == 'time_constant' else None)
+    shape = (45, 1032)
+    u, k, d = _inputs(shape, tdt, 'cuda', seed=37)
+    fk, bk = op.forward_ast_gpu.compile(), op.backward_ast_gpu.compile()
+    fill = float('nan') if mode == 'none' else 0.0
+    out, du = torch.full_like(u, fill), torch.full_like(u, fill)
+    dk = torch.full_like(u, fill) if mode == 'none' else torch.rand(shape, device='cuda').to(tdt)
+    dk0 = dk.clone()
+    fk(u=u, k=k, out=out)
+    bk(u=u, k=k, diffout=d, diffu=du, diffk=dk)
+    torch.cuda.synchronize()
+    for kk in (fk, bk):
+        assert kk.last_variant[1].VIEW2D == 'zy' and kk.last_variant[1].WS, kk.last_variant
+    arr = {n: t.double().cpu().numpy() for n, t in (('u', u), ('k', k))}
+    ref = OE.evaluate(op.forward_assignments, arr, boundary_handling=bh)
+    refb = OE.evaluate(op.backward_assignments, {**arr, 'diffout': d.double().cpu().numpy()}, boundary_handling=bh,
+                       outputs={'diffk': dk0.double().cpu().numpy()} if mode == 'time_constant' else None)
+    inner = (slice(1, -1),) * 2 if mode == 'none' else (slice(None),) * 2
+    for got, name, r in ((out, 'out', ref), (du, 'diffu', refb), (dk, 'diffk', refb)):
+        g_ = got.double().cpu().numpy()
+        tol = 2e-3 if f16 else 1e-5
+        np.testing.assert_allclose(g_[inner], r[name][inner], rtol=tol, atol=tol, err_msg=f'{mode} {name}')
+        if mode == 'none':
+            border = np.ones(shape, bool)
+            border[inner] = False
+            assert np.isnan(g_[border]).all(), f'{name}: a border cell was written'
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dts', ['float32', 'float16'])
 @pytest.mark.parametrize('shape', [(64, 256), (37, 136), (9, 520)], ids=str)
 def test_varcoef_2d_pairs_gpu(dts, shape):
     """The packed-pair form (``PR=1``) on a 2-D field (one (1, Y, X) plane on the register ring), forward and adjoint
