@@ -53,6 +53,9 @@ TILES = {
     'ws8_cx2nr2d3': dict(WS=1, NW=8, CX=2, NR=2, D=3),
     # timing only (wrong results): the default ring with no plane loads — the compute waves' time alone
     'abl_noload': dict(BABL=3), 'abl_noload_ws8': dict(WS=1, NW=8, CX=4, NR=1, D=2, BABL=3),
+    # chunk length along z (explicit ZC: the block-count path instead of the quantised chunk model)
+    'zc24': dict(ZC=24), 'zc32': dict(ZC=32), 'zc48': dict(ZC=48), 'zc64': dict(ZC=64), 'zc96': dict(ZC=96),
+    'zc128': dict(ZC=128), 'blk512': dict(BLOCKS=512), 'blk1024': dict(BLOCKS=1024),
 }
 
 
