@@ -348,7 +348,7 @@ def test_varcoef_2d_gpu_vs_oracle(dts, shape):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('dts', ['float32', 'float16'])
+@pytest.mark.parametrize('dts', ['float32', 'float16', 'float64'])
 @pytest.mark.parametrize('shape', [(40, 1024), (23, 1160), (3, 2048), (130, 520)], ids=str)
 def test_varcoef_2d_row_ring_gpu(dts, shape):
     """2-D nonlinear stencils on long rows march along axis 0 (``VIEW2D='zy'``: rows are the planes of the LDS-DMA
@@ -357,7 +357,8 @@ def test_varcoef_2d_row_ring_gpu(dts, shape):
     faces reading halo rows in place) bitwise equal to one full launch."""
     from pystencils_autodiff_amd.zslab import ZSlabOp
     op = pa.AutoDiffOp(_varcoef2d(dts), boundary_handling='zeros')
-    tdt = torch.float16 if dts == 'float16' else torch.float32
+    tdt = getattr(torch, dts)
+    fp64 = dts == 'float64'
     u, k, d = _inputs(shape, tdt, 'cuda', seed=31)
     out, gu, gk = _apply(op, u, k, d, 'cuda')
     fk, bk = op.forward_ast_gpu.compile(), op.backward_ast_gpu.compile()
@@ -367,9 +368,9 @@ def test_varcoef_2d_row_ring_gpu(dts, shape):
         assert kk.last_variant[0] == 'march' and (c.VIEW2D == 'zy' and c.WS) == row_ring, kk.last_variant
         assert bool(c.PR) == (row_ring and dts == 'float16'), kk.last_variant
     ref, ab = oracle(op, *(x.double().cpu().numpy() for x in (u, k, d)))
-    check(out, ref['out'], ab['out'], False, f'{shape} out', dts == 'float16')
-    check(gu, ref['diffu'], ab['diffu'], False, f'{shape} diffu', dts == 'float16')
-    check(gk, ref['diffk'], ab['diffk'], False, f'{shape} diffk', dts == 'float16')
+    check(out, ref['out'], ab['out'], fp64, f'{shape} out', dts == 'float16')
+    check(gu, ref['diffu'], ab['diffu'], fp64, f'{shape} diffu', dts == 'float16')
+    check(gk, ref['diffk'], ab['diffk'], fp64, f'{shape} diffk', dts == 'float16')
     if shape[0] < 8 or not row_ring:
         return
     full = torch.zeros_like(u)
