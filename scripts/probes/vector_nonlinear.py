@@ -1,6 +1,7 @@
 """A nonlinear stencil on a vector field (index dimension, components fastest): first-order upwind-free advection
 ``out(c) = u(c) − α Σ_d u(d)·(u[+e_d](c) − u[−e_d](c))/2`` on u(3) fp32 — which schedule it takes and its forward /
-adjoint rate through the op (HIP events, median of 20). Timing only.  python scripts/probes/vector_nonlinear.py [n=256]"""
+adjoint rate through the op (HIP events, median of 20). Timing only.
+python scripts/probes/vector_nonlinear.py [n=256] [dtype=float32] [2d: u(2) on n x n]"""
 import os
 import sys
 
@@ -15,16 +16,17 @@ from pystencils_autodiff_amd import ps  # noqa: E402
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
     dts = sys.argv[2] if len(sys.argv) > 2 else 'float32'
+    D = 2 if len(sys.argv) > 3 and sys.argv[3] == '2d' else 3     # '2d': u(2) on n x n
     tdt = getattr(torch, dts)
-    u, out = ps.fields(f'u(3), out(3): {dts}[3d]')
-    e = [(1, 0, 0), (0, 1, 0), (0, 0, 1)]
-    m = [(-1, 0, 0), (0, -1, 0), (0, 0, -1)]
+    u, out = ps.fields(f'u({D}), out({D}): {dts}[{D}d]')
+    e = [tuple(int(i == a) for i in range(D)) for a in range(D)]
+    m = [tuple(-v for v in o) for o in e]
     ac = ps.AssignmentCollection({out.center(c): u.center(c) - 0.05 * sp.Add(
-        *[u.center(d) * (u[e[d]](c) - u[m[d]](c)) / 2 for d in range(3)]) for c in range(3)})
+        *[u.center(d) * (u[e[d]](c) - u[m[d]](c)) / 2 for d in range(D)]) for c in range(D)})
     op = pa.AutoDiffOp(ac, boundary_handling='zeros')
     fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
-    x = torch.rand((n, n, n, 3), device='cuda').to(tdt).requires_grad_(True)
-    g = torch.rand((n, n, n, 3), device='cuda').to(tdt)
+    x = torch.rand((n,) * D + (D,), device='cuda').to(tdt).requires_grad_(True)
+    g = torch.rand((n,) * D + (D,), device='cuda').to(tdt)
     for _ in range(5):
         (o,) = fn.apply(x)
         o.backward(g)
@@ -43,8 +45,8 @@ def main():
         bw.append(ev[1].elapsed_time(ev[2]))
     fw.sort()
     bw.sort()
-    b = n ** 3 * 3 * tdt.itemsize
-    print(f'vector advection {n}^3x3 {dts}: fwd {fw[10]:.4f} ms ({2 * b / fw[10] / 1e6 / 8000:.3f} of 8 TB/s), '
+    b = n ** D * D * tdt.itemsize
+    print(f'vector advection {n}^{D}x{D} {dts}: fwd {fw[10]:.4f} ms ({2 * b / fw[10] / 1e6 / 8000:.3f} of 8 TB/s), '
           f'bwd {bw[10]:.4f} ms ({3 * b / bw[10] / 1e6 / 8000:.3f}); schedules '
           f'{op.forward_ast_gpu.compile().last_variant[0]} / {op.backward_ast_gpu.compile().last_variant[0]}', flush=True)
 

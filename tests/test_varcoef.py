@@ -713,6 +713,41 @@ def test_vector_advection_ring_gpu_vs_oracle(shape, bh, dts):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('dts', ['float32', 'float16'])
+@pytest.mark.parametrize('shape', [(40, 1024), (17, 600), (9, 100)], ids=str)
+def test_vector_advection_2d_gpu_vs_oracle(shape, dts):
+    """2-D advection on u(2) (components interleaved): on rows of >= 512 cells the 2-D row ring (``VIEW2D='zy'``, the
+    LDS-DMA ring with rows as planes), shorter rows the (1, Y, X) zsum plane or one thread per cell — forward and
+    TF-MAD adjoint vs the float64 oracle, cell by cell, with the reference's last-component quirk
+    (``_autodiff.py:138-152``)."""
+    u, out = ps.fields(f'u(2), out(2): {dts}[2d]')
+    E2, M2 = [(1, 0), (0, 1)], [(-1, 0), (0, -1)]
+    ac = ps.AssignmentCollection({out.center(c): u.center(c) - 0.05 * sp.Add(
+        *[u.center(d) * (u[E2[d]](c) - u[M2[d]](c)) / 2 for d in range(2)]) for c in range(2)})
+    op = pa.AutoDiffOp(ac, boundary_handling='zeros')
+    tdt = getattr(torch, dts)
+    g = torch.Generator().manual_seed(sum(shape))
+    uu0 = (torch.rand(shape + (2,), generator=g, dtype=torch.float64) * 2 - 1).to(tdt)
+    d = (torch.rand(shape + (2,), generator=g, dtype=torch.float64) * 2 - 1).to(tdt)
+    fn = op.create_tensorflow_op(use_cuda=True, backend='torch_native')
+    uu = uu0.cuda().requires_grad_(True)
+    (o,) = fn.apply(uu)
+    o.backward(d.cuda())
+    torch.cuda.synchronize()
+    for k in (op.forward_ast_gpu.compile(), op.backward_ast_gpu.compile()):
+        if shape[1] >= 512:
+            assert k.last_variant[0] == 'march' and k.last_variant[1].VIEW2D == 'zy' and k.last_variant[1].WS, \
+                k.last_variant
+        else:                             # (the (1, Y, X) zsum plane or one thread per cell)
+            assert not (k.last_variant[0] == 'march' and k.last_variant[1].WS), k.last_variant
+    ref, ab = _adv_oracle(op, 'zeros', uu0.double().numpy(), d.double().numpy())
+    half = dts == 'float16'
+    check(o, ref['out'], ab['out'], False, f'{shape} {dts} out', fp16=half)
+    check(uu.grad, ref['diffu'], ab['diffu'], False, f'{shape} {dts} diffu', fp16=half)
+    assert not uu.grad[..., :1].any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dts', ['float32', 'float16'])
 def test_vector_advection_ring_tilings_and_slab_gpu(dts):
     """Other ring tilings of the vector advection (8 compute waves, depth 1 and 3) and the z-slab launch pattern
     (interior z range, then both faces in one launch reading halo planes in place) bitwise equal to one full launch;
