@@ -286,7 +286,7 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             # axis 0 was slower, 0.41 / 0.41, and 128-row chunks 0.51 / 0.49)
             half2 = any(storage_ctype(f) == '_Float16' for f in ir.stencil_fields)
             zy = dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=2, WS=True, D=2, ZMIN=16 if half2 else 32, ZMAX=64,
-                      BLK=1024 if half2 else 512, PR=1 if half2 and pair_ok(ir) else 0)
+                      BLK=1024 if half2 else 512, PR=1 if half2 and pair_ok(ir, vectors=True) else 0)
             if ir.stencil_fields and (shape is None or int(shape[-1]) >= 64 * zy['CX'] * zy['WX']):
                 w = ws_geometry(ir, MarchConfig(VE=ve, **{**cfg, **zy}))
                 if w is not None and w['lds_bytes'] <= 160 * 1024:
@@ -312,10 +312,14 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
         for kv in env.split(','):
             k, v = kv.split('=')
             over[k.strip()] = v.strip() if k.strip() == 'VIEW2D' else int(v)
-    if ring_ws and any(k in over for k in ('CX', 'WX', 'NR', 'NW')) and 'WS' not in over:
+    view_yx = ir.ndim == 2 and str(over.get('VIEW2D', cfg['VIEW2D'])) != cfg['VIEW2D']
+    if ring_ws and (any(k in over for k in ('CX', 'WX', 'NR', 'NW')) or view_yx) and 'WS' not in over:
         cfg.update(WS=False, D=3)           # a tile override on the ring: the register-prefetch form it was sized for
-        if ir.ndim == 2 and 'VIEW2D' not in over:
-            cfg.update(VIEW2D='yx', NW=4, WX=1, PR=0, ZMIN=32, ZMAX=64, BLK=512)   # (... the 2-D one: (1, Y, X) tiles)
+        if ir.ndim == 2:
+            cfg.update(VIEW2D='yx', NW=4, WX=1, NR=2, PR=0, ZMIN=32, ZMAX=64, BLK=512)   # (the 2-D one: (1, Y, X) tiles)
+            if ir.has_index_dims:
+                cfg.update(ZSUM=True, PK=False, AR=False)     # (vector fields: the zsum plane, as without the ring)
+            ring_ws = False
     for k, v in over.items():
         if k not in TILE_KEYS:
             raise ValueError(f"unknown tile parameter '{k}' (gpu_indexing_params / PSAD_MARCH)")

@@ -347,6 +347,34 @@ def test_varcoef_2d_gpu_vs_oracle(dts, shape):
     check(gk, ref['diffk'], ab['diffk'], False, f'{shape} diffk', dts == 'float16')
 
 
+def test_2d_row_ring_selection_and_overrides():
+    """Schedule selection (no GPU): nonlinear 2-D stencils on long rows take the row ring (``VIEW2D='zy'``, LDS-DMA
+    loader, fp16 as cell pairs), short rows the (1, Y, X) tiles; a tile or ``VIEW2D='yx'`` override falls back to the
+    (1, Y, X) form (vector fields: its zsum plane) instead of a ring configuration it cannot take; every emitted source
+    compiles for gfx950."""
+    from pystencils_autodiff_amd.backends import hip_runtime as rt
+    from pystencils_autodiff_amd.backends.hip_kernel import HipStencilKernel
+    from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel
+    u2, o2 = ps.fields('u(2), o(2): float16[2d]')
+    E2, M2 = [(1, 0), (0, 1)], [(-1, 0), (0, -1)]
+    adv = ps.AssignmentCollection({o2.center(c): u2.center(c) - 0.05 * sp.Add(
+        *[u2.center(d) * (u2[E2[d]](c) - u2[M2[d]](c)) / 2 for d in range(2)]) for c in range(2)})
+    for ac, ve, vec in ((_varcoef2d('float32'), 4, False), (_varcoef2d('float16'), 8, False), (adv, 8, True)):
+        op = pa.AutoDiffOp(ac, boundary_handling='zeros')
+        for params in (None, {'VIEW2D': 'yx'}, {'CX': 2, 'NR': 2}):
+            hk = HipStencilKernel(StencilKernel(op.backward_assignments, boundary_handling='zeros', function_name='r2',
+                                                target='gpu', gpu_indexing_params=params))
+            for shape in ((4096, 4096), (64, 256)):
+                c = hk._march_cfg(ve, shape)
+                ring = params is None and shape[1] >= 512
+                assert (c.VIEW2D == 'zy' and c.WS) == ring, (params, shape, c)
+                assert bool(c.PR) == (ring and ve == 8), (params, shape, c)
+                if vec and not ring:
+                    assert c.ZSUM, (params, shape, c)
+                v = ('march', c)
+                assert len(rt.compile_hip(hk.source(v)[0], HipStencilKernel.options(v))) > 0
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize('dts', ['float32', 'float16', 'float64'])
 @pytest.mark.parametrize('shape', [(40, 1024), (23, 1160), (3, 2048), (130, 520)], ids=str)
@@ -734,9 +762,10 @@ def test_vector_advection_2d_gpu_vs_oracle(shape, dts):
     o.backward(d.cuda())
     torch.cuda.synchronize()
     for k in (op.forward_ast_gpu.compile(), op.backward_ast_gpu.compile()):
-        if shape[1] >= 512:
+        if shape[1] >= 512:             # (fp16: as x-adjacent cell pairs)
             assert k.last_variant[0] == 'march' and k.last_variant[1].VIEW2D == 'zy' and k.last_variant[1].WS, \
                 k.last_variant
+            assert k.last_variant[1].PR == int(dts == 'float16'), k.last_variant
         else:                             # (the (1, Y, X) zsum plane or one thread per cell)
             assert not (k.last_variant[0] == 'march' and k.last_variant[1].WS), k.last_variant
     ref, ab = _adv_oracle(op, 'zeros', uu0.double().numpy(), d.double().numpy())
