@@ -284,9 +284,12 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
             # workgroups of 64 / 32 rows at 4096²: 2-D varcoef 4096² fp32 fwd / bwd 0.61 / 0.57–0.58 of 8 TB/s,
             # fp16 0.40–0.42 / 0.49 (profiles/r06_nl2d_zy.log: 40 tilings and chunkings; the register ring along
             # axis 0 was slower, 0.41 / 0.41, and 128-row chunks 0.51 / 0.49)
+            # (fp64: 1024-cell strips, not halved below — fwd / bwd 0.56–0.62 / 0.58–0.61 vs 0.55–0.56 / 0.53–0.56 on
+            # the (1, Y, X) tiles; 256-cell strips lost the adjoint, 0.53, profiles/r06_nl2d_f64.log)
             half2 = any(storage_ctype(f) == '_Float16' for f in ir.stencil_fields)
-            zy = dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=2, WS=True, D=2, ZMIN=16 if half2 else 32, ZMAX=64,
-                      BLK=1024 if half2 else 512, PR=1 if half2 and pair_ok(ir, vectors=True) else 0)
+            wide = np.dtype(ir.compute_dtype).itemsize == 8
+            zy = dict(VIEW2D='zy', NR=1, NW=4, WX=4, CX=4 if wide else 2, WS=True, D=2, ZMIN=16 if half2 else 32,
+                      ZMAX=64, BLK=1024 if half2 else 512, PR=1 if half2 and pair_ok(ir, vectors=True) else 0)
             if ir.stencil_fields and (shape is None or int(shape[-1]) >= 64 * zy['CX'] * zy['WX']):
                 w = ws_geometry(ir, MarchConfig(VE=ve, **{**cfg, **zy}))
                 if w is not None and w['lds_bytes'] <= 160 * 1024:
@@ -300,7 +303,7 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
         cfg.update(ZSUM=True, PK=False, AR=False)
         while cfg['CX'] > 1 and cfg['CX'] * cmax > 4:
             cfg['CX'] //= 2
-    if np.dtype(ir.compute_dtype).itemsize == 8:
+    if np.dtype(ir.compute_dtype).itemsize == 8 and not (ir.ndim == 2 and ring_ws):
         cfg['CX'] = max(1, cfg['CX'] // 2)                     # fp64: half-width tiles (512³: 0.380 vs 0.536 ms)
     elif ir.ndim == 3 and cfg['ZSUM'] and not cfg['PK'] and not cfg.get('WS'):
         # star stencils: 128×32 tiles, two workgroups per CU. 512³ / one 8-GPU slab of 1024³
@@ -316,7 +319,8 @@ def default_march_config(ir, ve, shape=None, tuning=None, band=True):
     if ring_ws and (any(k in over for k in ('CX', 'WX', 'NR', 'NW')) or view_yx) and 'WS' not in over:
         cfg.update(WS=False, D=3)           # a tile override on the ring: the register-prefetch form it was sized for
         if ir.ndim == 2:
-            cfg.update(VIEW2D='yx', NW=4, WX=1, NR=2, PR=0, ZMIN=32, ZMAX=64, BLK=512)   # (the 2-D one: (1, Y, X) tiles)
+            cfg.update(VIEW2D='yx', NW=4, WX=1, NR=2, PR=0, ZMIN=32, ZMAX=64, BLK=512,   # (the 2-D one: (1, Y, X) tiles)
+                       CX=1 if np.dtype(ir.compute_dtype).itemsize == 8 else 2)
             if ir.has_index_dims:
                 cfg.update(ZSUM=True, PK=False, AR=False)     # (vector fields: the zsum plane, as without the ring)
             ring_ws = False

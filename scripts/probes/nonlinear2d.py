@@ -1,7 +1,7 @@
 """2-D variable-coefficient diffusion (5-point, nonlinear: ``u + α Σ₄ ½(k + k[nb])(u[nb] − u)``) through the op,
 forward and TF-MAD adjoint kernels timed alone with HIP events (median of 20), fraction of 8 TB/s from the algorithmic
 bytes (fwd 3, bwd 5 fields per cell). Timing only (parity: tests/test_varcoef.py::test_varcoef_2d_gpu_vs_oracle).
-python scripts/probes/nonlinear2d.py [n=4096] [tiles=default,...] [f16]"""
+python scripts/probes/nonlinear2d.py [n=4096] [tiles=default,...] [f16|f32|f64]"""
 import os
 import sys
 
@@ -13,7 +13,7 @@ import pystencils_autodiff_amd as pa  # noqa: E402
 from pystencils_autodiff_amd import ps  # noqa: E402
 from pystencils_autodiff_amd.backends.kernel_ir import StencilKernel  # noqa: E402
 
-TILES = {'default': {}, 'old': dict(CX=4, NR=4), 'cx2nr2': dict(CX=2, NR=2), 'cx4nr2': dict(CX=4, NR=2), 'cx2nr4': dict(CX=2, NR=4),
+TILES = {'default': {}, 'yx': dict(VIEW2D='yx'), 'old': dict(CX=4, NR=4), 'cx2nr2': dict(CX=2, NR=2), 'cx4nr2': dict(CX=4, NR=2), 'cx2nr4': dict(CX=2, NR=4),
          'cx4nr8': dict(CX=4, NR=8), 'cx8nr4': dict(CX=8, NR=4), 'cx4nr4_pr': dict(CX=4, NR=4, PR=1),
          'cx2nr2_pr': dict(CX=2, NR=2, PR=1), 'cx4nr1': dict(CX=4, NR=1), 'cx2nr8': dict(CX=2, NR=8),
          'nw1_cx4nr8': dict(NW=1, CX=4, NR=8), 'cx4wx2nr4': dict(CX=4, WX=2, NR=4),
@@ -76,9 +76,11 @@ def timed(fn, reps=20):
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     names = sys.argv[2].split(',') if len(sys.argv) > 2 else list(TILES)
-    f16 = len(sys.argv) > 3 and sys.argv[3] == 'f16'
-    dt, es = (torch.float16, 2) if f16 else (torch.float32, 4)
-    op = pa.AutoDiffOp(varcoef2d('float16' if f16 else 'float32'), boundary_handling='zeros')
+    prec = sys.argv[3] if len(sys.argv) > 3 else 'f32'
+    dts = {'f16': 'float16', 'f32': 'float32', 'f64': 'float64'}[prec]
+    dt = getattr(torch, dts)
+    es = dt.itemsize
+    op = pa.AutoDiffOp(varcoef2d(dts), boundary_handling='zeros')
     shape = (n, n)
     u, k, d = (torch.rand(shape, device='cuda').to(dt) for _ in range(3))
     out, du, dk = (torch.empty(shape, device='cuda', dtype=dt) for _ in range(3))
@@ -95,7 +97,7 @@ def main():
         if name == names[0]:
             first = got            # (the first tiling's results: the others are compared with them)
         dev = max(float((a - b).abs().max() / (b.abs().max() + 1e-30)) for a, b in zip(got, first))
-        print(f'varcoef2d {n}^2 {"f16" if f16 else "f32"} {name:12s} fwd {tf * 1e3:.1f} us ({3 * es * n * n / tf / 1e6 / 8000:.3f})  '
+        print(f'varcoef2d {n}^2 {prec} {name:12s} fwd {tf * 1e3:.1f} us ({3 * es * n * n / tf / 1e6 / 8000:.3f})  '
               f'bwd {tb * 1e3:.1f} us ({5 * es * n * n / tb / 1e6 / 8000:.3f})  {v[0]} '
               f'{dict(CX=v[1].CX, NR=v[1].NR, WS=v[1].WS, PR=v[1].PR, V=v[1].VIEW2D) if len(v) > 1 and hasattr(v[1], "CX") else ""}'
               f'  rel.dev {dev:.1e}',

@@ -390,7 +390,7 @@ def test_varcoef_2d_row_ring_gpu(dts, shape):
     u, k, d = _inputs(shape, tdt, 'cuda', seed=31)
     out, gu, gk = _apply(op, u, k, d, 'cuda')
     fk, bk = op.forward_ast_gpu.compile(), op.backward_ast_gpu.compile()
-    row_ring = shape[1] >= 512
+    row_ring = shape[1] >= (1024 if fp64 else 512)      # (fp64: 1024-cell strips)
     for kk in (fk, bk):
         c = kk.last_variant[1]
         assert kk.last_variant[0] == 'march' and (c.VIEW2D == 'zy' and c.WS) == row_ring, kk.last_variant
